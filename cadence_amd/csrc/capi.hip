@@ -1,0 +1,128 @@
+// capi.hip -- the extern "C" boundary (include/cadence_replay.h) around the replay kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "cadence_replay.h"
+
+namespace crr {
+__global__ void replay_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
+}
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Timing {
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool valid[2] = {false, false};
+  int device = -1;
+};
+thread_local Timing g_timing;
+
+bool ensure_events() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (g_timing.ev[0] && g_timing.device == dev) return true;
+  for (auto& e : g_timing.ev) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+  }
+  for (auto& e : g_timing.ev)
+    if (hipEventCreate(&e) != hipSuccess) return false;
+  g_timing.device = dev;
+  return true;
+}
+
+bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
+  if (!in || !out) return false;
+  if (in->stride == 0) return false;
+  if (in->n_wf == 0) return true;
+  if (!in->wf || !out->exec) return false;
+  const crr_events& e = in->ev;
+  if (!e.etype || !e.event_id || !e.version || !e.timestamp || !e.task_id || !e.ref || !e.key || !e.aux) return false;
+  if (!in->act_side || !in->start_side || !in->reset_keys || !in->arena) return false;
+  if (!out->act || !out->timer || !out->child || !out->rc || !out->sig || !out->vh || !out->rp) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crr_abi_version(void) { return CRR_ABI_VERSION; }
+
+size_t crr_sizeof(int which) {
+  switch (which) {
+    case 0: return sizeof(crr_workflow);
+    case 1: return sizeof(crr_exec_row);
+    case 2: return sizeof(crr_activity_row);
+    case 3: return sizeof(crr_timer_row);
+    case 4: return sizeof(crr_child_row);
+    case 5: return sizeof(crr_initiated_row);
+    case 6: return sizeof(crr_vh_item);
+    case 7: return sizeof(crr_reset_point_row);
+    case 8: return sizeof(crr_activity_side);
+    case 9: return sizeof(crr_start_side);
+    default: return 0;
+  }
+}
+
+int crr_set_device(int device) { return (int)hipSetDevice(device); }
+
+int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
+  if (!valid_inputs(in, out)) return -1;
+  if (in->n_wf == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool timed = ensure_events();
+  const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
+  g_timing.valid[0] = g_timing.valid[1] = false;
+  for (int phase = 0; phase < 2; ++phase) {
+    if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
+    if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
+    hipLaunchKernelGGL(crr::replay_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return (int)err;
+    if (timed) {
+      (void)hipEventRecord(g_timing.ev[2 * phase + 1], s);
+      g_timing.valid[phase] = true;
+    }
+  }
+  return 0;
+}
+
+int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksums, void* stream) {
+  if (!valid_inputs(in, out) || (!checksums && in->n_wf)) return -1;
+  if (in->n_wf == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(crr::checksum_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, checksums);
+  return (int)hipGetLastError();
+}
+
+float crr_last_kernel_ms(int phase) {
+  if (phase < 0 || phase > 1 || !g_timing.valid[phase]) return -1.0f;
+  float ms = -1.0f;
+  if (hipEventElapsedTime(&ms, g_timing.ev[2 * phase], g_timing.ev[2 * phase + 1]) != hipSuccess) return -1.0f;
+  return ms;
+}
+
+uint32_t crr_crc32_ieee(const uint8_t* data, size_t len) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+      table[i] = c;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < len; ++i) c = table[(c ^ data[i]) & 0xff] ^ (c >> 8);
+  return ~c;
+}
+
+}  // extern "C"

@@ -1,0 +1,169 @@
+"""Device engine: binds ``libcadence_replay.so`` (the C ABI) and manages HBM-resident batches.
+
+PyTorch is used only as plumbing (device allocation, streams, copies).  There is no CPU fallback:
+if the HIP library is missing or no GPU is visible the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import os
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import abi
+from .flatten import HistoryBatch
+from .result import ReplayResult
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcadence_replay.so")
+_lib = None
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the HIP library (raises EngineUnavailable when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineUnavailable(f"{LIB_PATH} not built: run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        L.crr_replay.argtypes = [vp, vp, vp]
+        L.crr_replay.restype = ctypes.c_int
+        L.crr_checksum.argtypes = [vp, vp, vp, vp]
+        L.crr_checksum.restype = ctypes.c_int
+        L.crr_set_device.argtypes = [ctypes.c_int]
+        L.crr_set_device.restype = ctypes.c_int
+        L.crr_abi_version.restype = ctypes.c_int
+        L.crr_crc32_ieee.argtypes = [vp, ctypes.c_size_t]
+        L.crr_crc32_ieee.restype = ctypes.c_uint32
+        L.crr_last_kernel_ms.argtypes = [ctypes.c_int]
+        L.crr_last_kernel_ms.restype = ctypes.c_float
+        if L.crr_abi_version() != abi.ABI_VERSION:
+            raise EngineUnavailable("ABI version mismatch")
+        abi.check_layout(L)
+        _lib = L
+    return _lib
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise EngineUnavailable("no HIP device visible (torch.cuda.is_available() is False)")
+    return torch
+
+
+@dataclasses.dataclass
+class DeviceBatch:
+    """A HistoryBatch resident in HBM plus its output buffers."""
+    batch: HistoryBatch
+    tensors: Dict[str, object]
+    c_in: abi.CInputs
+    c_out: abi.COutputs
+    device: int
+
+    @property
+    def n_wf(self):
+        return self.batch.n_wf
+
+
+def _dev_bytes(torch, arr: np.ndarray, device, pad: int = 16):
+    """Copy a numpy array to a uint8 device tensor (padded so empty arrays still get an address)."""
+    raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+    t = torch.empty(max(raw.size, 1) + pad, dtype=torch.uint8, device=device)
+    if raw.size:
+        t[:raw.size].copy_(torch.from_numpy(raw), non_blocking=False)
+    return t
+
+
+class ReplayEngine:
+    """Batched ``StateBuilder.ApplyEvents`` on one MI355X (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self.torch = _torch()
+        self.device = device
+        self.lib = lib()
+        rc = self.lib.crr_set_device(device)
+        if rc != 0:
+            raise EngineUnavailable(f"crr_set_device({device}) failed: {rc}")
+        self.dev = self.torch.device("cuda", device)
+
+    # -- upload ------------------------------------------------------------------------------------
+    def upload(self, batch: HistoryBatch) -> DeviceBatch:
+        torch = self.torch
+        dev = self.dev
+        T = {}
+        ev = abi.CEvents()
+        for name, t in abi.EVENT_COLUMNS:
+            T["ev_" + name] = _dev_bytes(torch, np.asarray(batch.cols[name], dtype=t), dev)
+            setattr(ev, name, T["ev_" + name].data_ptr())
+        ci = abi.CInputs()
+        ci.ev = ev
+        # the device reads branch tokens as 8-byte words: keep the arena 8-byte padded
+        arena = np.concatenate([batch.arena, np.zeros(16, np.uint8)])
+        for field, arr in (("act_side", batch.act_side), ("start_side", batch.start_side),
+                           ("reset_keys", batch.reset_keys), ("arena", arena), ("wf", batch.wf)):
+            T[field] = _dev_bytes(torch, arr, dev)
+            setattr(ci, field, T[field].data_ptr())
+        ci.n_wf = batch.n_wf
+        ci.stride = batch.stride
+        has_new_run = bool((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()) if batch.n_wf else False
+        ci.flags = abi.IN_HAS_NEW_RUN if has_new_run else 0
+        co = abi.COutputs()
+        T["exec"] = torch.zeros(max(batch.n_wf, 1) * abi.EXEC_ROW.itemsize, dtype=torch.uint8, device=dev)
+        co.exec = T["exec"].data_ptr()
+        for name, dt, *_ in abi.TABLES:
+            rows = max(batch.table_rows.get(name, 0), 1)
+            T["out_" + name] = torch.zeros(rows * dt.itemsize, dtype=torch.uint8, device=dev)
+            setattr(co, name, T["out_" + name].data_ptr())
+        return DeviceBatch(batch, T, ci, co, self.device)
+
+    # -- launch ------------------------------------------------------------------------------------
+    def launch(self, db: DeviceBatch, stream=None):
+        """Enqueue crr_replay on ``stream`` (torch stream; default: current stream)."""
+        torch = self.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        rc = self.lib.crr_replay(ctypes.byref(db.c_in), ctypes.byref(db.c_out), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_replay failed: {rc}")
+
+    def last_kernel_ms(self):
+        return [self.lib.crr_last_kernel_ms(0), self.lib.crr_last_kernel_ms(1)]
+
+    def checksum(self, db: DeviceBatch, stream=None) -> np.ndarray:
+        """Recompute checksums of the replayed rows on the device (Load verify path)."""
+        torch = self.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        out = torch.zeros(max(db.n_wf, 1), dtype=torch.int32, device=self.dev)
+        rc = self.lib.crr_checksum(ctypes.byref(db.c_in), ctypes.byref(db.c_out), ctypes.c_void_p(out.data_ptr()),
+                                   ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_checksum failed: {rc}")
+        torch.cuda.synchronize(self.dev)
+        return out.cpu().numpy().view(np.uint32)[:db.n_wf]
+
+    # -- download ----------------------------------------------------------------------------------
+    def download(self, db: DeviceBatch) -> ReplayResult:
+        self.torch.cuda.synchronize(self.dev)
+        T = db.tensors
+        ex = T["exec"].cpu().numpy().view(abi.EXEC_ROW)[:db.n_wf].copy()
+        tables = {}
+        for name, dt, *_ in abi.TABLES:
+            tables[name] = T["out_" + name].cpu().numpy().view(dt).copy()
+        return ReplayResult(ex, tables)
+
+    def replay(self, batch: HistoryBatch) -> ReplayResult:
+        db = self.upload(batch)
+        self.launch(db)
+        return self.download(db)
+
+
+def crc32(data: bytes) -> int:
+    """hash/crc32.ChecksumIEEE via the library's host helper."""
+    a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    return int(lib().crr_crc32_ieee(a.ctypes.data_as(ctypes.c_void_p), len(data)))

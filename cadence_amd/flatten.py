@@ -1,0 +1,354 @@
+"""Host flattening: workflow histories -> structure-of-arrays columns (``crr_inputs``).
+
+This is the work the Go side of the cgo shim does before calling the engine (north star: "Go host
+code flattens decoded HistoryEvent batches into structure-of-arrays columns").  Two layouts:
+
+* canonical  (stride 1): events of a workflow are contiguous; slot tables likewise.
+* interleaved (stride 64): workflows sorted by length, 64 per group; column index
+  ``group_base + step * 64 + lane`` so that a wavefront's 64 lanes (one workflow each) read one
+  contiguous 64-element run per column per step -- fully coalesced HBM loads.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .abi import EventType as ET
+from .history import WorkflowHistory, thrift_history_branch_token
+
+WAVE = 64
+
+
+@dataclasses.dataclass
+class HistoryBatch:
+    """Flattened input of one crr_replay call (host numpy arrays)."""
+    cols: Dict[str, np.ndarray]           # event columns, see abi.EVENT_COLUMNS
+    act_side: np.ndarray                  # abi.ACTIVITY_SIDE
+    start_side: np.ndarray                # abi.START_SIDE
+    reset_keys: np.ndarray                # uint32
+    arena: np.ndarray                     # uint8 branch-token bytes
+    wf: np.ndarray                        # abi.WORKFLOW
+    stride: int
+    # test / oracle only: per-event key strings (never shipped to the device)
+    key_off: Optional[np.ndarray] = None
+    key_len: Optional[np.ndarray] = None
+    key_arena: Optional[np.ndarray] = None
+    # interleaved batches: device position p holds canonical workflow perm[p]
+    perm: Optional[np.ndarray] = None
+    # sizes of the slot tables (rows)
+    table_rows: Dict[str, int] = dataclasses.field(default_factory=dict)
+
+    @property
+    def n_wf(self) -> int:
+        return int(self.wf.shape[0])
+
+    @property
+    def n_events(self) -> int:
+        return int(self.wf["ev_count"].sum())
+
+    @property
+    def n_slots(self) -> int:
+        return int(self.cols["etype"].shape[0])
+
+
+def _zeros_cols(n):
+    return {name: np.zeros(n, dtype=t) for name, t in abi.EVENT_COLUMNS}
+
+
+class _Interner:
+    def __init__(self):
+        self.ids = {"": 0}
+
+    def __call__(self, s) -> int:
+        s = "" if s is None else str(s)
+        v = self.ids.get(s)
+        if v is None:
+            v = len(self.ids)
+            self.ids[s] = v
+        return v
+
+
+def _domain_status(name, known_domains) -> int:
+    if not name:
+        return abi.DOMAIN_NOT_SET
+    if known_domains is None or name in known_domains:
+        return abi.DOMAIN_RESOLVED
+    return abi.DOMAIN_UNKNOWN
+
+
+def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
+            new_run_index: Optional[Dict[int, int]] = None) -> HistoryBatch:
+    """Flatten object histories into a canonical HistoryBatch.
+
+    ``known_domains``: domain names the domain cache resolves (None: all resolve).
+    CAN events reference their new-run history through attrs["new_run"] = workflow index.
+    """
+    n_ev = sum(len(b) for h in histories for b in h.batches)
+    cols = _zeros_cols(n_ev)
+    key_off = np.zeros(n_ev, np.uint32)
+    key_len = np.zeros(n_ev, np.uint32)
+    key_arena = bytearray()
+    key_cache: Dict[str, int] = {}
+    act_side, start_side, reset_keys = [], [], []
+    arena = bytearray()
+    wf = np.zeros(len(histories), dtype=abi.WORKFLOW)
+    caps = {t[3]: np.zeros(len(histories), np.int64) for t in abi.TABLES}
+
+    def put_key_str(i, s):
+        s = "" if s is None else str(s)
+        off = key_cache.get(s)
+        if off is None:
+            off = len(key_arena)
+            key_arena.extend(s.encode())
+            key_cache[s] = off
+        key_off[i] = off
+        key_len[i] = len(s.encode())
+
+    i = 0
+    for w, h in enumerate(histories):
+        intern = _Interner()
+        begin = i
+        empty_at = -1
+        n_act = n_timer = n_child = n_rc = n_sig = n_dtc = 0
+        max_prev = 0
+        vh_items = 0
+        last_ver = None
+        for bi, batch in enumerate(h.batches):
+            if not batch:
+                if empty_at < 0:
+                    empty_at = i - begin
+                continue
+            for j, e in enumerate(batch):
+                t = int(e.event_type)
+                flags = (abi.BATCH_FIRST if j == 0 else 0) | (abi.BATCH_LAST if j == len(batch) - 1 else 0)
+                cols["etype"][i] = (t & abi.ETYPE_MASK) | flags if 0 <= t < abi.EV_TYPE_COUNT else (abi.EV_PAD - 1) | flags
+                cols["event_id"][i] = e.id
+                cols["version"][i] = e.version
+                cols["timestamp"][i] = e.timestamp
+                cols["task_id"][i] = e.task_id
+                if last_ver is None or e.version > last_ver:
+                    vh_items += 1
+                    last_ver = e.version
+                ref = 0
+                key = 0
+                aux = 0
+                ks = None
+                a = e.get
+                if t == ET.WorkflowExecutionStarted:
+                    prev = e.attrs.get("prev_auto_reset_points", None)
+                    if prev is None:
+                        prev_off, prev_cnt = 0, -1
+                    elif prev == "nil_points":
+                        prev_off, prev_cnt = 0, -2
+                    else:
+                        prev_off, prev_cnt = len(reset_keys), len(prev)
+                        reset_keys.extend(intern(p) for p in prev)
+                        max_prev = max(max_prev, len(prev))
+                    pdid = e.attrs.get("parent_workflow_domain_id")
+                    pdom = a("parent_workflow_domain", "")
+                    pstat = abi.DOMAIN_NOT_SET if pdid is not None else _domain_status(pdom, known_domains)
+                    init = e.attrs.get("initiator")
+                    start_side.append((a("task_start_to_close_timeout_seconds", 0), a("execution_start_to_close_timeout_seconds", 0),
+                                       a("first_decision_task_backoff_seconds", 0),
+                                       abi.INITIATOR_NIL if init is None else int(init), pstat, prev_off, prev_cnt, 0))
+                    aux = len(start_side) - 1
+                elif t == ET.DecisionTaskScheduled:
+                    ref = a("attempt", 0)
+                    aux = a("start_to_close_timeout_seconds", 0)
+                elif t == ET.DecisionTaskStarted:
+                    ref = a("scheduled_event_id", 0)
+                elif t == ET.DecisionTaskCompleted:
+                    ref = a("started_event_id", 0)
+                    ks = a("binary_checksum", "")
+                    key = intern(ks)
+                    n_dtc += 1
+                elif t == ET.DecisionTaskTimedOut:
+                    aux = a("timeout_type", 0)
+                elif t == ET.ActivityTaskScheduled:
+                    ks = a("activity_id", "")
+                    key = intern(ks)
+                    rp = e.attrs.get("retry_policy")
+                    act_side.append((a("schedule_to_start_timeout_seconds", 0), a("schedule_to_close_timeout_seconds", 0),
+                                     a("start_to_close_timeout_seconds", 0), a("heartbeat_timeout_seconds", 0),
+                                     1 if rp is not None else 0,
+                                     (rp or {}).get("expiration_interval_in_seconds", 0) if isinstance(rp, dict) else 0,
+                                     _domain_status(a("domain", ""), known_domains), 0))
+                    aux = len(act_side) - 1
+                    n_act += 1
+                elif t in (ET.ActivityTaskStarted, ET.ActivityTaskCompleted, ET.ActivityTaskFailed,
+                           ET.ActivityTaskTimedOut, ET.ActivityTaskCanceled):
+                    ref = a("scheduled_event_id", 0)
+                elif t == ET.ActivityTaskCancelRequested:
+                    ks = a("activity_id", "")
+                    key = intern(ks)
+                elif t == ET.TimerStarted:
+                    ks = a("timer_id", "")
+                    key = intern(ks)
+                    ref = a("start_to_fire_timeout_seconds", 0)
+                    n_timer += 1
+                elif t in (ET.TimerFired, ET.TimerCanceled):
+                    ks = a("timer_id", "")
+                    key = intern(ks)
+                elif t == ET.StartChildWorkflowExecutionInitiated:
+                    aux = _domain_status(a("domain", ""), known_domains)
+                    n_child += 1
+                elif t == ET.RequestCancelExternalWorkflowExecutionInitiated:
+                    aux = _domain_status(a("domain", ""), known_domains)
+                    n_rc += 1
+                elif t == ET.SignalExternalWorkflowExecutionInitiated:
+                    aux = _domain_status(a("domain", ""), known_domains)
+                    n_sig += 1
+                elif t in (ET.StartChildWorkflowExecutionFailed, ET.ChildWorkflowExecutionStarted,
+                           ET.ChildWorkflowExecutionCompleted, ET.ChildWorkflowExecutionFailed,
+                           ET.ChildWorkflowExecutionCanceled, ET.ChildWorkflowExecutionTimedOut,
+                           ET.ChildWorkflowExecutionTerminated, ET.RequestCancelExternalWorkflowExecutionFailed,
+                           ET.ExternalWorkflowExecutionCancelRequested, ET.SignalExternalWorkflowExecutionFailed,
+                           ET.ExternalWorkflowExecutionSignaled):
+                    ref = a("initiated_event_id", 0)
+                elif t == ET.WorkflowExecutionContinuedAsNew:
+                    nr = e.attrs.get("new_run")
+                    aux = -1 if nr is None else int(nr)
+                cols["ref"][i] = ref
+                cols["key"][i] = key
+                cols["aux"][i] = aux
+                put_key_str(i, ks)
+                i += 1
+        n = i - begin
+        if empty_at < 0 and h.batches and not h.batches[-1]:
+            empty_at = n
+        if not h.batches:
+            empty_at = 0
+        tok = thrift_history_branch_token(h.run_id, h.branch_id)
+        r = wf[w]
+        r["ev_begin"] = begin
+        r["ev_count"] = n
+        r["empty_batch_at"] = empty_at
+        r["init_version"] = h.domain_failover_version
+        r["now_ns"] = h.now_ns
+        r["start_token_off"] = len(arena)
+        r["start_token_len"] = len(tok)
+        arena.extend(tok)
+        if h.final_token is not None:
+            r["final_token_off"] = len(arena)
+            r["final_token_len"] = len(h.final_token)
+            arena.extend(h.final_token)
+            r["rebuild_last_event_id"] = h.rebuild_last_event_id
+            r["rebuild_last_event_version"] = h.rebuild_last_event_version
+        else:
+            r["final_token_off"] = 0
+            r["final_token_len"] = abi.NO_TOKEN
+        r["flags"] = abi.WF_FLAG_NEW_RUN if h.is_new_run else 0
+        caps["act_cap"][w] = n_act
+        caps["timer_cap"][w] = n_timer
+        caps["child_cap"][w] = n_child
+        caps["rc_cap"][w] = n_rc
+        caps["sig_cap"][w] = n_sig
+        caps["vh_cap"][w] = vh_items
+        caps["rp_cap"][w] = max_prev * max(1, sum(1 for e in h.events if e.event_type == ET.WorkflowExecutionStarted)) + n_dtc
+    batch = HistoryBatch(
+        cols=cols,
+        act_side=np.array(act_side or [(0,) * 8], dtype=abi.ACTIVITY_SIDE),
+        start_side=np.array(start_side or [(0,) * 8], dtype=abi.START_SIDE),
+        reset_keys=np.array(reset_keys or [0], dtype=np.uint32),
+        arena=np.frombuffer(bytes(arena) or b"\0", dtype=np.uint8).copy(),
+        wf=wf, stride=1,
+        key_off=key_off, key_len=key_len,
+        key_arena=np.frombuffer(bytes(key_arena) or b"\0", dtype=np.uint8).copy())
+    assign_canonical_tables(batch, caps)
+    return batch
+
+
+def assign_canonical_tables(batch: HistoryBatch, caps: Dict[str, np.ndarray]):
+    """Canonical slot-table bases: prefix sums of per-workflow capacities."""
+    for name, _dt, base_f, cap_f, _n in abi.TABLES:
+        c = np.maximum(caps[cap_f].astype(np.int64), 0)
+        base = np.zeros_like(c)
+        if c.size:
+            base[1:] = np.cumsum(c)[:-1]
+        batch.wf[base_f] = base
+        batch.wf[cap_f] = c
+        batch.table_rows[name] = int(c.sum()) if c.size else 0
+
+
+def interleave(batch: HistoryBatch, wave: int = WAVE) -> HistoryBatch:
+    """Permute a canonical batch into the wave-interleaved device layout.
+
+    Workflows are sorted by event count (descending; ties by index) and packed 64 per group.
+    Group g occupies ``group_len[g] * 64`` event slots; lanes shorter than the group's longest
+    workflow see CRR_EV_PAD slots.  CAN ``aux`` references are remapped to device positions.
+    """
+    assert batch.stride == 1
+    n = batch.n_wf
+    counts = batch.wf["ev_count"].astype(np.int64)
+    perm = np.lexsort((np.arange(n), -counts)).astype(np.int64)     # device pos -> canonical wf
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    n_groups = (n + wave - 1) // wave
+    pos = np.arange(n_groups * wave)
+    lane = pos % wave
+    group = pos // wave
+    valid = pos < n
+    cnt_sorted = np.zeros(n_groups * wave, np.int64)
+    cnt_sorted[:n] = counts[perm]
+    glen = cnt_sorted.reshape(n_groups, wave).max(axis=1)
+    gbase = np.zeros(n_groups, np.int64)
+    if n_groups:
+        gbase[1:] = np.cumsum(glen * wave)[:-1]
+    total_slots = int((glen * wave).sum())
+
+    # event permutation
+    src_begin = batch.wf["ev_begin"][perm].astype(np.int64)
+    wf_pos = np.repeat(np.arange(n), counts[perm])
+    step = np.arange(wf_pos.size) - np.repeat(np.cumsum(counts[perm]) - counts[perm], counts[perm])
+    src_idx = src_begin[wf_pos] + step
+    dst_idx = gbase[group[wf_pos]] + step * wave + lane[wf_pos]
+    cols = {}
+    for name, t in abi.EVENT_COLUMNS:
+        c = np.zeros(total_slots, dtype=t)
+        if name == "etype":
+            c[:] = abi.EV_PAD | abi.BATCH_FIRST | abi.BATCH_LAST
+        c[dst_idx] = batch.cols[name][src_idx]
+        cols[name] = c
+    # CAN new-run references -> device positions
+    can = (cols["etype"] & abi.ETYPE_MASK) == ET.WorkflowExecutionContinuedAsNew
+    can &= cols["aux"] >= 0
+    if can.any():
+        cols["aux"][can] = inv[cols["aux"][can]]
+    key_off = key_len = None
+    if batch.key_off is not None:
+        key_off = np.zeros(total_slots, np.uint32)
+        key_len = np.zeros(total_slots, np.uint32)
+        key_off[dst_idx] = batch.key_off[src_idx]
+        key_len[dst_idx] = batch.key_len[src_idx]
+
+    wf = batch.wf[perm].copy()
+    wf["ev_begin"] = gbase[group[:n]] + lane[:n]
+    out = HistoryBatch(cols=cols, act_side=batch.act_side, start_side=batch.start_side,
+                       reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
+                       key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm)
+    for name, _dt, base_f, cap_f, _n in abi.TABLES:
+        cap = np.zeros(n_groups * wave, np.int64)
+        cap[:n] = wf[cap_f]
+        gcap = cap.reshape(n_groups, wave).max(axis=1)
+        tbase = np.zeros(n_groups, np.int64)
+        if n_groups:
+            tbase[1:] = np.cumsum(gcap * wave)[:-1]
+        wf[base_f] = tbase[group[:n]] + lane[:n]
+        wf[cap_f] = gcap[group[:n]]
+        out.table_rows[name] = int((gcap * wave).sum())
+    return out
+
+
+def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, np.ndarray], w: int):
+    """Live rows of workflow ``w`` (batch order) from output tables: {table: structured array}."""
+    r = batch.wf[w]
+    out = {}
+    for name, _dt, base_f, _cap_f, n_f in abi.TABLES:
+        n = int(exec_rows[w][n_f])
+        n = min(n, int(r[_cap_f]))
+        idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * batch.stride
+        out[name] = tables[name][idx]
+    return out

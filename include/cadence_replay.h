@@ -1,0 +1,389 @@
+/*
+ * cadence_replay.h -- C ABI of the MI355X batched history-replay engine.
+ *
+ * This is the drop-in boundary for Cadence's mutable-state rebuild hot path:
+ *
+ *   service/history/execution/state_builder.go:41-51   StateBuilder.ApplyEvents
+ *   service/history/execution/state_builder.go:90-648  stateBuilderImpl.ApplyEvents
+ *   service/history/execution/mutable_state_builder.go:1751-3810  Replicate*Event
+ *   service/history/execution/checksum.go:36-114       mutable-state checksum
+ *
+ * The reference is Go; its FFI for this path would be cgo.  Every entry point below takes
+ * plain pointers and sizes (no torch / HIP-runtime types beyond an opaque stream handle) so
+ * that a cgo shim can bind it one-to-one.
+ *
+ * Data model
+ * ----------
+ * A *batch* of workflows is replayed in one call.  Each workflow is a sequence of persisted
+ * event batches (the unit ApplyEvents is called with; state_rebuilder.go:135-148).  Events are
+ * flattened into structure-of-arrays columns (crr_events).  Event `k` of workflow `w` lives at
+ * column index  wf[w].ev_begin + k * stride, where `stride` is 1 for the canonical
+ * (contiguous-per-workflow) layout and 64 for the wave-interleaved layout the GPU kernel is
+ * tuned for (64 workflows of similar length share one "group"; step k of all 64 is one
+ * contiguous 64-element run, so every column load is fully coalesced).  Batch boundaries are
+ * carried in the two high bits of the event-type byte.
+ *
+ * Strings never reach the device.  The host interns ActivityID / TimerID / BinaryChecksum into
+ * per-workflow u32 keys (string equality preserved) and every string-valued output field is
+ * returned as a *source reference* (the event step that supplied it), which the host shim
+ * materialises.  Non-deterministic inputs of the reference (uuid.New(), timeSource.Now(),
+ * the random branchID) are host-supplied per workflow.
+ *
+ * Pending activity / timer / child / request-cancel / signal maps, the version-history items
+ * and the auto-reset-point list live in per-workflow slot tables ("workspace rows") addressed
+ * with the same base + slot * stride rule.  After a call the first n_* slots of each table hold
+ * the live rows sorted by their event ID, which is also the order the checksum encodes them in.
+ */
+#ifndef CADENCE_REPLAY_H_
+#define CADENCE_REPLAY_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRR_ABI_VERSION 1
+
+/* ---- constants restated from the reference ------------------------------------------------ */
+/* common/constants.go:30-58 */
+#define CRR_FIRST_EVENT_ID      1LL
+#define CRR_EMPTY_EVENT_ID      (-23LL)
+#define CRR_EMPTY_VERSION       (-24LL)
+#define CRR_BUFFERED_EVENT_ID   (-123LL)
+#define CRR_TRANSIENT_EVENT_ID  (-124LL)
+/* Go time.Time{} (zero value) is not representable as Unix nanoseconds; rows use this sentinel. */
+#define CRR_ZERO_TIME           ((int64_t)0x8000000000000000ULL)
+/* "no source event" for string-valued fields; -2 = the constant common.EmptyUUID ("emptyUuid"). */
+#define CRR_SRC_NONE            (-1)
+#define CRR_SRC_EMPTY_UUID      (-2)
+
+/* types.EventType, common/types/shared.go:3272-3357 (iota order). */
+enum crr_event_type {
+    CRR_EV_WORKFLOW_EXECUTION_STARTED = 0,
+    CRR_EV_WORKFLOW_EXECUTION_COMPLETED = 1,
+    CRR_EV_WORKFLOW_EXECUTION_FAILED = 2,
+    CRR_EV_WORKFLOW_EXECUTION_TIMED_OUT = 3,
+    CRR_EV_DECISION_TASK_SCHEDULED = 4,
+    CRR_EV_DECISION_TASK_STARTED = 5,
+    CRR_EV_DECISION_TASK_COMPLETED = 6,
+    CRR_EV_DECISION_TASK_TIMED_OUT = 7,
+    CRR_EV_DECISION_TASK_FAILED = 8,
+    CRR_EV_ACTIVITY_TASK_SCHEDULED = 9,
+    CRR_EV_ACTIVITY_TASK_STARTED = 10,
+    CRR_EV_ACTIVITY_TASK_COMPLETED = 11,
+    CRR_EV_ACTIVITY_TASK_FAILED = 12,
+    CRR_EV_ACTIVITY_TASK_TIMED_OUT = 13,
+    CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED = 14,
+    CRR_EV_REQUEST_CANCEL_ACTIVITY_TASK_FAILED = 15,
+    CRR_EV_ACTIVITY_TASK_CANCELED = 16,
+    CRR_EV_TIMER_STARTED = 17,
+    CRR_EV_TIMER_FIRED = 18,
+    CRR_EV_CANCEL_TIMER_FAILED = 19,
+    CRR_EV_TIMER_CANCELED = 20,
+    CRR_EV_WORKFLOW_EXECUTION_CANCEL_REQUESTED = 21,
+    CRR_EV_WORKFLOW_EXECUTION_CANCELED = 22,
+    CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED = 23,
+    CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED = 24,
+    CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED = 25,
+    CRR_EV_MARKER_RECORDED = 26,
+    CRR_EV_WORKFLOW_EXECUTION_SIGNALED = 27,
+    CRR_EV_WORKFLOW_EXECUTION_TERMINATED = 28,
+    CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW = 29,
+    CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED = 30,
+    CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED = 31,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED = 32,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED = 33,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED = 34,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED = 35,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT = 36,
+    CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED = 37,
+    CRR_EV_SIGNAL_EXTERNAL_INITIATED = 38,
+    CRR_EV_SIGNAL_EXTERNAL_FAILED = 39,
+    CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED = 40,
+    CRR_EV_UPSERT_WORKFLOW_SEARCH_ATTRIBUTES = 41,
+    CRR_EV_TYPE_COUNT = 42,
+    CRR_EV_PAD = 63          /* padding slot in the interleaved layout: never replayed */
+};
+#define CRR_ETYPE_MASK        0x3F
+#define CRR_ETYPE_BATCH_FIRST 0x80   /* event is history[0] of its ApplyEvents batch */
+#define CRR_ETYPE_BATCH_LAST  0x40   /* event is history[len-1] of its ApplyEvents batch */
+
+/* persistence.WorkflowState* / WorkflowCloseStatus*, common/persistence/dataManagerInterfaces.go:118-135 */
+enum crr_workflow_state {
+    CRR_STATE_CREATED = 0, CRR_STATE_RUNNING = 1, CRR_STATE_COMPLETED = 2,
+    CRR_STATE_ZOMBIE = 3, CRR_STATE_VOID = 4, CRR_STATE_CORRUPTED = 5
+};
+enum crr_close_status {
+    CRR_CLOSE_NONE = 0, CRR_CLOSE_COMPLETED = 1, CRR_CLOSE_FAILED = 2, CRR_CLOSE_CANCELED = 3,
+    CRR_CLOSE_TERMINATED = 4, CRR_CLOSE_CONTINUED_AS_NEW = 5, CRR_CLOSE_TIMED_OUT = 6
+};
+/* types.TimeoutType, common/types/shared.go:8792-8799 == execution.TimerType */
+enum crr_timeout_type {
+    CRR_TIMEOUT_START_TO_CLOSE = 0, CRR_TIMEOUT_SCHEDULE_TO_START = 1,
+    CRR_TIMEOUT_SCHEDULE_TO_CLOSE = 2, CRR_TIMEOUT_HEARTBEAT = 3
+};
+/* execution/timer_sequence.go:51-67 */
+#define CRR_TIMER_TASK_STATUS_NONE     0
+#define CRR_TIMER_TASK_STATUS_CREATED  1
+#define CRR_TTS_CREATED_START_TO_CLOSE    1
+#define CRR_TTS_CREATED_SCHEDULE_TO_START 2
+#define CRR_TTS_CREATED_SCHEDULE_TO_CLOSE 4
+#define CRR_TTS_CREATED_HEARTBEAT         8
+/* types.ContinueAsNewInitiator, common/types/shared.go:1253-1258; -1 = nil pointer */
+#define CRR_INITIATOR_NIL        (-1)
+#define CRR_INITIATOR_DECIDER      0
+#define CRR_INITIATOR_RETRY_POLICY 1
+#define CRR_INITIATOR_CRON         2
+
+/* Domain-cache lookups on the path resolve on the host; the device only sees the outcome. */
+#define CRR_DOMAIN_NOT_SET   0   /* attribute domain name empty -> execution's own DomainID */
+#define CRR_DOMAIN_RESOLVED  1   /* domain cache lookup succeeded                          */
+#define CRR_DOMAIN_UNKNOWN (-1)  /* lookup fails -> EntityNotExists error from the cache   */
+
+/* ---- per-workflow status (maps 1:1 onto the Go error returned by ApplyEvents) ------------- */
+enum crr_status_code {
+    CRR_OK = 0,
+    CRR_ERR_EMPTY_HISTORY = 1,            /* InternalFailure  state_builder.go:98-100              */
+    CRR_ERR_UNKNOWN_EVENT_TYPE = 2,       /* BadRequest       state_builder.go:629-630             */
+    CRR_ERR_VH_LOWER_VERSION = 3,         /* BadRequest       versionHistory.go:204-209            */
+    CRR_ERR_VH_EVENT_ID_NOT_INCREASING=4, /* BadRequest       versionHistory.go:211-216            */
+    CRR_ERR_VH_INVALID_ITEM = 5,          /* panic            versionHistory.go:37-43              */
+    CRR_ERR_VH_EMPTY = 6,                 /* BadRequest       versionHistory.go:303-308 (via UpdateCurrentVersion) */
+    CRR_ERR_INVALID_STATE_TRANSITION = 7, /* InternalService  workflowExecutionInfo.go:45-165      */
+    CRR_ERR_UNKNOWN_WORKFLOW_STATE = 8,   /* InternalService  workflowExecutionInfo.go:143-147     */
+    CRR_ERR_MISSING_ACTIVITY_INFO = 9,    /* InternalService  mutable_state_builder.go:64-65       */
+    CRR_ERR_MISSING_CHILD_INFO = 10,      /* InternalService  mutable_state_builder.go:66-67       */
+    CRR_ERR_DECISION_NOT_FOUND = 11,      /* InternalFailure  mutable_state_decision_task_manager.go:211-214 */
+    CRR_ERR_DOMAIN_NOT_FOUND = 12,        /* EntityNotExists  domain cache                         */
+    CRR_ERR_BAD_INITIATOR = 13,           /* InternalService  mutable_state_task_generator.go:269-277 */
+    CRR_ERR_TIMER_SEQUENCE = 14,          /* InternalService  timer_sequence.go:141-145,176-180    */
+    CRR_ERR_REBUILD_LAST_ITEM = 15,       /* BadRequest       state_rebuilder.go:160-176           */
+    CRR_ERR_NEW_RUN_MISSING = 16,         /* engine: CAN new-run workflow index out of range       */
+    CRR_ERR_CAPACITY = 100                /* engine: a slot table was sized too small by the host  */
+};
+
+/* ---- input ---------------------------------------------------------------------------------- */
+/*
+ * Event columns.  Per-type meaning of ref / key / aux (attribute getters cited):
+ *   WorkflowExecutionStarted   aux = index into start side records
+ *   DecisionTaskScheduled      ref = Attempt (int64), aux = StartToCloseTimeoutSeconds
+ *   DecisionTaskStarted        ref = ScheduledEventID
+ *   DecisionTaskCompleted      ref = StartedEventID, key = BinaryChecksum (0 == "")
+ *   DecisionTaskTimedOut       aux = TimeoutType
+ *   ActivityTaskScheduled      key = ActivityID, aux = index into activity side records
+ *   ActivityTaskStarted / Completed / Failed / TimedOut / Canceled   ref = ScheduledEventID
+ *   ActivityTaskCancelRequested key = ActivityID
+ *   TimerStarted               key = TimerID, ref = StartToFireTimeoutSeconds
+ *   TimerFired / TimerCanceled key = TimerID
+ *   StartChildWorkflowExecutionInitiated  aux = domain status (CRR_DOMAIN_*)
+ *   RequestCancelExternal...Initiated / SignalExternal...Initiated  aux = domain status
+ *   child close/started, RC failed/cancel-requested, signal failed/signaled  ref = InitiatedEventID
+ *   WorkflowExecutionContinuedAsNew       aux = workflow index of the new-run history (-1: none)
+ */
+typedef struct crr_events {
+    const uint8_t*  etype;      /* crr_event_type | CRR_ETYPE_BATCH_* */
+    const int64_t*  event_id;   /* HistoryEvent.ID        */
+    const int64_t*  version;    /* HistoryEvent.Version   */
+    const int64_t*  timestamp;  /* HistoryEvent.Timestamp (Unix ns) */
+    const int64_t*  task_id;    /* HistoryEvent.TaskID    */
+    const int64_t*  ref;
+    const uint32_t* key;
+    const int32_t*  aux;
+} crr_events;
+
+/* ActivityTaskScheduledEventAttributes fields the state machine reads (32 B). */
+typedef struct crr_activity_side {
+    int32_t schedule_to_start;      /* GetScheduleToStartTimeoutSeconds */
+    int32_t schedule_to_close;      /* GetScheduleToCloseTimeoutSeconds */
+    int32_t start_to_close;         /* GetStartToCloseTimeoutSeconds    */
+    int32_t heartbeat;              /* GetHeartbeatTimeoutSeconds       */
+    int32_t has_retry_policy;       /* RetryPolicy != nil               */
+    int32_t expiration_interval;    /* RetryPolicy.GetExpirationIntervalInSeconds */
+    int32_t domain_status;          /* CRR_DOMAIN_* for attributes.Domain */
+    int32_t reserved;
+} crr_activity_side;
+
+/* WorkflowExecutionStartedEventAttributes fields the state machine reads (32 B). */
+typedef struct crr_start_side {
+    int32_t decision_start_to_close;   /* GetTaskStartToCloseTimeoutSeconds (DecisionStartToCloseTimeout) */
+    int32_t workflow_timeout;          /* GetExecutionStartToCloseTimeoutSeconds */
+    int32_t first_decision_backoff;    /* GetFirstDecisionTaskBackoffSeconds */
+    int32_t initiator;                 /* CRR_INITIATOR_* */
+    int32_t parent_domain_status;      /* CRR_DOMAIN_* of the ParentWorkflowDomain lookup (state_builder.go:137-147) */
+    uint32_t prev_reset_key_off;       /* PrevAutoResetPoints binary checksums (keys) in crr_inputs.reset_keys */
+    int32_t prev_reset_count;          /* -1 == PrevAutoResetPoints nil (or Points nil) */
+    int32_t reserved;
+} crr_start_side;
+
+/* Per-workflow descriptor (160 B). */
+typedef struct crr_workflow {
+    int64_t  ev_begin;          /* column index of step 0 */
+    int32_t  ev_count;          /* number of real events */
+    int32_t  empty_batch_at;    /* step index before which an empty batch sits (-1 none) */
+    int64_t  init_version;      /* domainEntry.GetFailoverVersion() (mutable_state_builder.go:207) */
+    int64_t  now_ns;            /* injected timeSource.Now().UnixNano() */
+    uint32_t start_token_off;   /* branch token SetHistoryTree installs (state_builder.go:179-183) */
+    uint32_t start_token_len;
+    uint32_t final_token_off;   /* rebuild target token (state_rebuilder.go:150), len==UINT32_MAX: none */
+    uint32_t final_token_len;
+    int64_t  rebuild_last_event_id;       /* state_rebuilder.go:160 check, used when final token set */
+    int64_t  rebuild_last_event_version;
+    /* slot-table row bases (row = base + slot * stride) and capacities */
+    int64_t  act_base;  int64_t timer_base; int64_t child_base; int64_t rc_base;
+    int64_t  sig_base;  int64_t vh_base;    int64_t rp_base;
+    int32_t  act_cap, timer_cap, child_cap, rc_cap, sig_cap, vh_cap, rp_cap;
+    int32_t  flags;             /* bit0: is a CAN new-run history (replayed in the first phase) */
+    int64_t  reserved;
+} crr_workflow;
+
+#define CRR_WF_FLAG_NEW_RUN 1
+
+typedef struct crr_inputs {
+    crr_events               ev;
+    const crr_activity_side* act_side;
+    const crr_start_side*    start_side;
+    const uint32_t*          reset_keys;   /* interned binary checksums of PrevAutoResetPoints */
+    const uint8_t*           arena;        /* branch-token bytes */
+    const crr_workflow*      wf;
+    uint32_t                 n_wf;
+    uint32_t                 stride;       /* 1 (canonical) or 64 (wave-interleaved) */
+    uint32_t                 flags;        /* CRR_IN_* */
+    uint32_t                 reserved;
+} crr_inputs;
+
+#define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
+
+/* ---- output rows ---------------------------------------------------------------------------- */
+/* WorkflowExecutionInfo numeric image + engine status (192 B). */
+typedef struct crr_exec_row {
+    int32_t  status;                 /* crr_status_code */
+    int32_t  fail_step;              /* step index of the failing event, or -1 */
+    int32_t  inconsistencies;        /* logDataInconsistency() calls (mutable_state_builder.go:4720) */
+    uint32_t flags;                  /* CRR_EXEC_* */
+    int32_t  state, close_status;
+    int32_t  signal_count;           /* int32 SignalCount */
+    int32_t  decision_timeout;       /* int32 DecisionTimeout */
+    int64_t  next_event_id, last_first_event_id, last_event_task_id, last_processed_event;
+    int64_t  completion_event_batch_id;
+    int64_t  decision_version, decision_schedule_id, decision_started_id, decision_attempt;
+    int64_t  decision_started_ts, decision_scheduled_ts, decision_orig_scheduled_ts;
+    int64_t  current_version;        /* in-memory currentVersion */
+    int32_t  decision_request_src;   /* DecisionRequestID: step of DecisionTaskStarted, or CRR_SRC_EMPTY_UUID */
+    int32_t  start_src;              /* step of the (last) WorkflowExecutionStarted event, or -1 */
+    int32_t  n_activity, n_timer, n_child, n_rc, n_signal, n_vh_items, n_reset_points;
+    int32_t  token_src;              /* 0: none (empty token), 1: start token, 2: final token */
+    uint32_t checksum;               /* crc32.ChecksumIEEE of the thriftrw payload (crc.go:46) */
+    uint32_t payload_len;            /* bytes the checksum was computed over (0x59 preamble included) */
+    int32_t  reserved[2];
+} crr_exec_row;
+
+#define CRR_EXEC_CANCEL_REQUESTED  1u
+#define CRR_EXEC_RESET_POINTS_SET  2u   /* AutoResetPoints != nil */
+#define CRR_EXEC_CHECKSUM_VALID    4u
+
+/* persistence.ActivityInfo numeric image (112 B). */
+typedef struct crr_activity_row {
+    int64_t  schedule_id, version, scheduled_batch_id, scheduled_time;
+    int64_t  started_id, started_time;          /* started_time == CRR_ZERO_TIME until started */
+    int64_t  cancel_request_id;
+    int64_t  last_hb_timeout_vis_s;             /* LastHeartbeatTimeoutVisibilityInSeconds */
+    int32_t  sched_src, started_src;            /* ActivityID/TaskList/... from sched_src; RequestID from started_src */
+    int32_t  schedule_to_start, schedule_to_close, start_to_close, heartbeat;
+    int32_t  timer_task_status;
+    uint32_t key;                                /* interned ActivityID */
+    uint32_t flags;                              /* CRR_ROW_* */
+    int32_t  reserved[3];
+} crr_activity_row;
+
+/* persistence.TimerInfo numeric image (40 B). */
+typedef struct crr_timer_row {
+    int64_t  started_id, version, expiry_time;
+    int32_t  task_status;
+    uint32_t key;                                /* interned TimerID */
+    int32_t  src;                                /* step of TimerStarted */
+    uint32_t flags;
+} crr_timer_row;
+
+/* persistence.ChildExecutionInfo numeric image (48 B). CreateRequestID = injected uuid(src). */
+typedef struct crr_child_row {
+    int64_t  initiated_id, version, initiated_batch_id, started_id;
+    int32_t  src, started_src;
+    uint32_t flags;
+    int32_t  reserved;
+} crr_child_row;
+
+/* persistence.RequestCancelInfo / SignalInfo numeric image (32 B). Request IDs = injected uuid(src). */
+typedef struct crr_initiated_row {
+    int64_t  initiated_id, version, initiated_batch_id;
+    int32_t  src;
+    uint32_t flags;
+} crr_initiated_row;
+
+typedef struct crr_vh_item { int64_t event_id, version; } crr_vh_item;
+
+/* types.ResetPointInfo provenance (16 B): a previous point from the start event or a new point. */
+typedef struct crr_reset_point_row {
+    int32_t  src;        /* step of DecisionTaskCompleted (new) or of WorkflowExecutionStarted (prev) */
+    int32_t  prev_index; /* index into the start event's PrevAutoResetPoints, or -1 for a new point */
+    uint32_t key;        /* interned binary checksum */
+    uint32_t flags;      /* CRR_ROW_RESETTABLE */
+} crr_reset_point_row;
+
+#define CRR_ROW_LIVE             1u
+#define CRR_ROW_MAPPED           2u   /* activity: pendingActivityIDToEventID[ActivityID] == ScheduleID */
+#define CRR_ROW_CANCEL_REQUESTED 4u
+#define CRR_ROW_HAS_RETRY        8u
+#define CRR_ROW_RESETTABLE      16u
+
+typedef struct crr_outputs {
+    crr_exec_row*        exec;      /* [n_wf], indexed by workflow */
+    crr_activity_row*    act;       /* slot tables, rows addressed by crr_workflow bases */
+    crr_timer_row*       timer;
+    crr_child_row*       child;
+    crr_initiated_row*   rc;
+    crr_initiated_row*   sig;
+    crr_vh_item*         vh;
+    crr_reset_point_row* rp;
+} crr_outputs;
+
+/* ---- entry points ----------------------------------------------------------------------------- */
+/* All pointers in crr_inputs / crr_outputs are DEVICE pointers (HBM resident).  `stream` is a
+ * hipStream_t (NULL: default stream).  Returns 0 on successful launch, a negative value on an
+ * invalid argument, or the positive hipError_t of a failed launch.  Per-workflow outcomes are in
+ * crr_exec_row.status (first error aborts that workflow, state stays partially applied exactly as
+ * the Go code leaves it -- state_builder.go returns at the first error, there is no rollback).
+ *
+ * Replaces: StateBuilder.ApplyEvents for a whole batch of workflows
+ *           (state_builder.go:90-648, driven per batch by state_rebuilder.go:214-236 /
+ *            ndc/history_replicator.go:292,396,650), plus generateMutableStateChecksum
+ *           (checksum.go:36-43 via mutable_state_builder.go:4641-4651).
+ * CAN new-run histories (crr_workflow.flags & CRR_WF_FLAG_NEW_RUN) are replayed in a first
+ * launch, the rest in a second one, so a ContinuedAsNew event can observe its nested replay's
+ * outcome (state_builder.go:587-612). */
+int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream);
+
+/* Recompute checksums of already-replayed rows (the Load verify path,
+ * mutable_state_builder.go:334-348 -> checksum.go:45-54).  Writes checksums[n_wf]. */
+int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksums, void* stream);
+
+/* Select the HIP device for subsequent calls from this thread. */
+int crr_set_device(int device);
+
+/* Library / ABI version; struct sizes for binding-time layout checks. */
+int crr_abi_version(void);
+size_t crr_sizeof(int which);   /* 0 workflow, 1 exec row, 2 activity, 3 timer, 4 child, 5 initiated,
+                                   6 vh item, 7 reset point, 8 activity side, 9 start side */
+
+/* Host-side CRC32-IEEE (hash/crc32.ChecksumIEEE) used by the shim's standalone verify. */
+uint32_t crr_crc32_ieee(const uint8_t* data, size_t len);
+
+/* Last launch's kernel time in milliseconds measured with HIP events on `stream`
+ * (phase 0: new-run histories, phase 1: the rest).  Valid after the stream has synchronised. */
+float crr_last_kernel_ms(int phase);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CADENCE_REPLAY_H_ */

@@ -39,25 +39,6 @@ def parse():
     return p.parse_args()
 
 
-def digest(torch, exec_bytes, n_wf):
-    """Order-independent digest of the replayed shard: [events-ok, workflows-ok, statuses!=0, sum(crc),
-    xor-fold(crc), inconsistencies] as int64 (reduced across ranks by one RCCL all-reduce)."""
-    rows = exec_bytes[: n_wf * 192].view(torch.int32).view(n_wf, 48)
-    status = rows[:, 0]
-    crc = rows[:, 44].to(torch.int64) & 0xFFFFFFFF
-    ok = status == 0
-    okl = ok.to(torch.int64)
-    out = torch.stack([
-        ((rows[:, 8].to(torch.int64) - 1) * okl).sum(),   # events replayed (NextEventID - 1 per workflow)
-        okl.sum(),
-        n_wf - okl.sum(),
-        (crc * okl).sum(),
-        ((crc * 0x9E3779B1) & 0xFFFFFFFF).sum(),
-        rows[:, 2].to(torch.int64).sum(),
-    ])
-    return out
-
-
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,6 +47,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from cadence_amd import dist as cdist
     from cadence_amd import synth
     from cadence_amd.engine import ReplayEngine
     from cadence_amd.flatten import interleave
@@ -98,8 +80,8 @@ def main():
         eng.launch(db, stream)
         kernel_ms.append(None)
         if world > 1:
-            d = digest(torch, db.tensors["exec"], n_wf)
-            dist.all_reduce(d)
+            d = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
+            cdist.all_reduce_digest(torch, dist, d)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

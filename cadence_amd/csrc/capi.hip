@@ -7,7 +7,8 @@
 #include "cadence_replay.h"
 
 namespace crr {
-__global__ void replay_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
 }
 
@@ -82,7 +83,15 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
-    hipLaunchKernelGGL(crr::replay_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+    if (in->stride == 64) {
+      // fast path (LDS-indexed tables), then the general path for workflows it handed back
+      hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+      hipError_t err = hipGetLastError();
+      if (err != hipSuccess) return (int)err;
+      hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 1);
+    } else {
+      hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 0);
+    }
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return (int)err;
     if (timed) {

@@ -1,14 +1,19 @@
 // replay_kernel.hip -- CDNA4 (gfx950) batched mutable-state replay.
 //
-// One lane replays one workflow (the short-history bucket): every
-// workflow is an independent event-sourced state machine, so a wavefront advances 64 workflows
-// in lock step.  With the wave-interleaved input layout (stride 64) each per-step column load of a
-// wavefront is one contiguous 64-element run; the execution-info scalars, the version history's
-// last item and the table occupancy live in VGPRs; the pending activity / timer / child /
-// request-cancel / signal maps are per-workflow slot tables in HBM (interleaved the same way, so
-// lanes probing slot j touch one contiguous run), reused on delete so a workflow's footprint is its
-// peak concurrency.  The epilogue sorts the live rows by event ID (the order the checksum encodes)
-// and streams the thriftrw checksum payload through a slicing-by-8 CRC32 whose tables sit in LDS.
+// One lane replays one workflow: every workflow is an independent event-sourced state machine, so
+// a wavefront advances 64 workflows in lock step.
+//
+// Two table policies share one state-machine body (replay_body<P>):
+//   * LdsTables  (fast path, wave-interleaved layout): the pending activity / timer / child /
+//     request-cancel / signal maps and the reset-point keys are indexed in LDS ([slot][lane] SoA,
+//     bank-conflict free).  Every lookup, the per-batch timer epilogue and the checksum's sorted ID
+//     lists are served from LDS; the HBM rows of the output tables are written (never read) during
+//     replay and compacted once at the end.  Group-uniform bases live in SGPRs.  A workflow whose
+//     live set outgrows its LDS slots stops with CRR_INTERNAL_RETRY and is replayed again by
+//   * GlobalTables (any layout, unbounded): the same maps as slot tables in the HBM output rows.
+//
+// The column loads of step s+1 are issued before step s is processed (software pipeline).  The
+// checksum streams the thriftrw payload through a slicing-by-8 CRC32 whose tables sit in LDS.
 //
 // Control flow restates the Go path exactly as oracle/state_builder_ref.cpp does (citations there
 // and inline): service/history/execution/state_builder.go:90-648, mutable_state_builder.go,
@@ -20,6 +25,25 @@
 
 #include "cadence_replay.h"
 
+#ifndef CRR_LDS_ACT
+#define CRR_LDS_ACT 3
+#endif
+#ifndef CRR_LDS_TIMER
+#define CRR_LDS_TIMER 2
+#endif
+#ifndef CRR_LDS_CHILD
+#define CRR_LDS_CHILD 1
+#endif
+#ifndef CRR_LDS_RC
+#define CRR_LDS_RC 1
+#endif
+#ifndef CRR_LDS_SIG
+#define CRR_LDS_SIG 1
+#endif
+#ifndef CRR_LDS_RP
+#define CRR_LDS_RP 2
+#endif
+
 namespace crr {
 
 using i64 = int64_t;
@@ -28,14 +52,21 @@ using u32 = uint32_t;
 using u64 = uint64_t;
 
 constexpr i64 kSecond = 1000000000LL;
+constexpr int kBlock = 256;
+constexpr int CRR_INTERNAL_RETRY = 200;  // LDS slots exhausted: replay again with GlobalTables
 
-__device__ __forceinline__ i64 wadd(i64 a, i64 b) { return (i64)((u64)a + (u64)b); }
 __device__ __forceinline__ i64 add_seconds(i64 t, i64 s) { return (i64)((u64)t + (u64)s * (u64)kSecond); }
-__device__ __forceinline__ i64 unix_seconds(i64 ns) {
+__device__ __forceinline__ i64 unix_seconds(i64 ns) {  // time.Time.Unix(): floor
   i64 q = ns / kSecond;
   if ((ns % kSecond) < 0) --q;
   return q;
 }
+__device__ __forceinline__ i64 uniform64(i64 v) {
+  u32 lo = __builtin_amdgcn_readfirstlane((u32)(u64)v);
+  u32 hi = __builtin_amdgcn_readfirstlane((u32)((u64)v >> 32));
+  return (i64)(((u64)hi << 32) | lo);
+}
+__device__ __forceinline__ i32 uniform32(i32 v) { return (i32)__builtin_amdgcn_readfirstlane((u32)v); }
 
 // ---------------------------------------------------------------------------------------------------
 // CRC32-IEEE (hash/crc32.ChecksumIEEE, common/checksum/crc.go:46), slicing-by-8 over LDS tables.
@@ -76,9 +107,9 @@ struct Crc {
   __device__ __forceinline__ void be64(i64 v) { push(__builtin_bswap64((u64)v), 8); }
   // thrift binary WriteFieldBegin: type byte + big-endian i16 id
   __device__ __forceinline__ void field(u32 type, u32 id) { push(type | (((id >> 8) & 0xff) << 8) | ((id & 0xff) << 16), 3); }
-  __device__ __forceinline__ void list_i64_header(u32 id, u32 n) {  // field(TLIST,id) + (TI64, n)
+  __device__ __forceinline__ void list_header(u32 id, u32 elem, u32 n) {  // field(TLIST,id) + (elem type, n)
     field(15, id);
-    push(10u | ((u64)__builtin_bswap32(n) << 8), 5);
+    push(elem | ((u64)__builtin_bswap32(n) << 8), 5);
   }
   __device__ __forceinline__ u32 finish() {
     for (int i = 0; i < nbuf; ++i) {
@@ -110,7 +141,6 @@ __device__ void build_crc_tables(u32* T) {
 // ---------------------------------------------------------------------------------------------------
 // Per-lane replay state: the numeric image of WorkflowExecutionInfo plus engine bookkeeping.
 struct Lane {
-  // execution info (persistence.WorkflowExecutionInfo)
   i32 state, close_status;
   i64 next_event_id, last_first_event_id, last_event_task_id, last_processed_event, completion_event_batch_id;
   i64 decision_version, decision_schedule_id, decision_started_id, decision_attempt;
@@ -121,22 +151,18 @@ struct Lane {
   i32 start_src;
   u32 flags;                    // CRR_EXEC_CANCEL_REQUESTED | CRR_EXEC_RESET_POINTS_SET
   i64 current_version;
-  i64 now_ns;
-  // version history: last item in registers, earlier items in the vh table
   i64 vh_last_id, vh_last_ver;
   i32 vh_n;
   i32 token_src;
-  // slot-table occupancy: live counts and high-water marks
-  i32 n_act, hw_act, n_timer, hw_timer, n_child, hw_child, n_rc, hw_rc, n_sig, hw_sig, n_rp;
+  i32 n_act, n_timer, n_child, n_rc, n_sig, n_rp;
   i32 inconsistencies;
   i32 status, fail_step;
 };
 
-struct Ctx {
-  crr_inputs in;
+// Where this lane's output rows live in HBM: row(table, slot) = base + slot * stride.
+struct Geo {
   crr_outputs out;
-  i64 st;  // stride
-  // this workflow's slot-table bases / capacities
+  i64 st;
   i64 act_base, timer_base, child_base, rc_base, sig_base, vh_base, rp_base;
   i32 act_cap, timer_cap, child_cap, rc_cap, sig_cap, vh_cap, rp_cap;
   __device__ __forceinline__ crr_activity_row* act(i32 j) const { return out.act + act_base + (i64)j * st; }
@@ -148,8 +174,31 @@ struct Ctx {
   __device__ __forceinline__ crr_reset_point_row* rp(i32 j) const { return out.rp + rp_base + (i64)j * st; }
 };
 
+__device__ __forceinline__ void load_geo(Geo& G, const crr_workflow* wfp, const crr_outputs& out, i64 stride) {
+  G.out = out;
+  G.st = stride;
+  G.act_base = wfp->act_base; G.timer_base = wfp->timer_base; G.child_base = wfp->child_base;
+  G.rc_base = wfp->rc_base; G.sig_base = wfp->sig_base; G.vh_base = wfp->vh_base; G.rp_base = wfp->rp_base;
+  G.act_cap = wfp->act_cap; G.timer_cap = wfp->timer_cap; G.child_cap = wfp->child_cap; G.rc_cap = wfp->rc_cap;
+  G.sig_cap = wfp->sig_cap; G.vh_cap = wfp->vh_cap; G.rp_cap = wfp->rp_cap;
+}
+
+// Wave-interleaved layout: every base is group_base + lane and every capacity is the group's.
+// Moving the group-uniform part to SGPRs frees ~20 VGPRs per lane.
+__device__ __forceinline__ void uniformize_geo(Geo& G, i64 lane) {
+  G.act_base = uniform64(G.act_base - lane) + lane;
+  G.timer_base = uniform64(G.timer_base - lane) + lane;
+  G.child_base = uniform64(G.child_base - lane) + lane;
+  G.rc_base = uniform64(G.rc_base - lane) + lane;
+  G.sig_base = uniform64(G.sig_base - lane) + lane;
+  G.vh_base = uniform64(G.vh_base - lane) + lane;
+  G.rp_base = uniform64(G.rp_base - lane) + lane;
+  G.act_cap = uniform32(G.act_cap); G.timer_cap = uniform32(G.timer_cap); G.child_cap = uniform32(G.child_cap);
+  G.rc_cap = uniform32(G.rc_cap); G.sig_cap = uniform32(G.sig_cap); G.vh_cap = uniform32(G.vh_cap);
+  G.rp_cap = uniform32(G.rp_cap);
+}
+
 // UpdateWorkflowStateCloseStatus (common/persistence/workflowExecutionInfo.go:45-165).
-// Returns CRR_OK or the error code; on success the state is updated.
 __device__ __forceinline__ int update_state(Lane& L, int state, int cs) {
   bool ok;
   switch (L.state) {
@@ -204,146 +253,49 @@ __device__ __forceinline__ void update_decision(Lane& L, i64 ver, i64 sched, i64
 }
 
 // FailDecision(true) (:643-676) followed by ReplicateTransientDecisionTaskScheduled (:168-197)
-__device__ __forceinline__ void fail_decision_and_transient(Lane& L) {
+__device__ __forceinline__ void fail_decision_and_transient(Lane& L, i64 now_ns) {
   update_decision(L, CRR_EMPTY_VERSION, CRR_EMPTY_EVENT_ID, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, 0,
-                  L.decision_attempt + 1, 0, L.now_ns, 0);
-  // transient: !HasPendingDecision && DecisionAttempt != 0 -- always true right after FailDecision(true)
+                  L.decision_attempt + 1, 0, now_ns, 0);
   if (L.decision_schedule_id == CRR_EMPTY_EVENT_ID && L.decision_attempt != 0)
     update_decision(L, L.current_version, L.next_event_id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID,
-                    L.decision_start_to_close, L.decision_attempt, 0, L.now_ns, 0);
+                    L.decision_start_to_close, L.decision_attempt, 0, now_ns, 0);
 }
 
-// ---- slot-table primitives ---------------------------------------------------------------------------
-__device__ __forceinline__ i32 find_act_by_id(const Ctx& C, const Lane& L, i64 sched) {
-  for (i32 j = 0; j < L.hw_act; ++j) {
-    const crr_activity_row* r = C.act(j);
-    if ((r->flags & CRR_ROW_LIVE) && r->schedule_id == sched) return j;
-  }
-  return -1;
-}
-// live activity whose ActivityID mapping points at it (pendingActivityIDToEventID[key])
-__device__ __forceinline__ i32 find_act_mapped(const Ctx& C, const Lane& L, u32 key) {
-  for (i32 j = 0; j < L.hw_act; ++j) {
-    const crr_activity_row* r = C.act(j);
-    u32 f = r->flags;
-    if ((f & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && r->key == key) return j;
-  }
-  return -1;
-}
-template <class R>
-__device__ __forceinline__ i32 free_slot(R* (Ctx::*row)(i32) const, const Ctx& C, i32& hw, i32 cap) {
-  for (i32 j = 0; j < hw; ++j)
-    if (!((C.*row)(j)->flags & CRR_ROW_LIVE)) return j;
-  if (hw >= cap) return -1;
-  return hw++;
-}
-template <class R>
-__device__ __forceinline__ i32 find_initiated(R* (Ctx::*row)(i32) const, const Ctx& C, i32 hw, i64 id) {
-  for (i32 j = 0; j < hw; ++j) {
-    const R* r = (C.*row)(j);
-    if ((r->flags & CRR_ROW_LIVE) && r->initiated_id == id) return j;
-  }
-  return -1;
-}
-__device__ __forceinline__ i32 find_timer(const Ctx& C, const Lane& L, u32 key) {
-  for (i32 j = 0; j < L.hw_timer; ++j) {
-    const crr_timer_row* r = C.timer(j);
-    if ((r->flags & CRR_ROW_LIVE) && r->key == key) return j;
-  }
-  return -1;
-}
-
-// DeleteActivity (mutable_state_builder.go:1310-1339)
-__device__ __forceinline__ void delete_activity(const Ctx& C, Lane& L, i64 sched) {
-  i32 j = find_act_by_id(C, L, sched);
-  if (j < 0) { ++L.inconsistencies; return; }
-  crr_activity_row* r = C.act(j);
-  u32 f = r->flags;
-  u32 key = r->key;
-  r->flags = f & ~(CRR_ROW_LIVE | CRR_ROW_MAPPED);
-  --L.n_act;
-  if (f & CRR_ROW_MAPPED) return;  // delete(pendingActivityIDToEventID, ActivityID) removed our own mapping
-  i32 m = find_act_mapped(C, L, key);  // the mapping of this ActivityID points at a newer activity
-  if (m >= 0) C.act(m)->flags &= ~CRR_ROW_MAPPED;
-  else ++L.inconsistencies;
-}
-
-// ---- timer sequence epilogue (timer_sequence.go:127-199, :219-381, :461-493) ---------------------------
 __device__ __forceinline__ bool seq_less(i64 ta, i64 ea, i32 ya, i64 tb, i64 eb, i32 yb) {
   if (ta != tb) return ta < tb;
   if (ea != eb) return ea < eb;
   return ya < yb;
 }
-
-__device__ __forceinline__ void create_next_activity_timer(const Ctx& C, Lane& L) {
-  if (L.n_act == 0) return;
-  bool have = false;
-  i64 bt = 0, be = 0;
-  i32 by = 0, bj = -1;
-  bool bc = false;
-  for (i32 j = 0; j < L.hw_act; ++j) {
-    const crr_activity_row* r = C.act(j);
-    if (!(r->flags & CRR_ROW_LIVE)) continue;
-    const i64 sid = r->schedule_id;
-    if (sid == CRR_EMPTY_EVENT_ID) continue;
-    const i32 tts = r->timer_task_status;
-    const i64 sched_t = r->scheduled_time;
-    const i64 started = r->started_id;
-    // ScheduleToClose
-    {
-      i64 t = add_seconds(sched_t, r->schedule_to_close);
-      if (!have || seq_less(t, sid, CRR_TIMEOUT_SCHEDULE_TO_CLOSE, bt, be, by)) {
-        have = true; bt = t; be = sid; by = CRR_TIMEOUT_SCHEDULE_TO_CLOSE; bj = j; bc = (tts & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) != 0;
-      }
-    }
-    if (started == CRR_EMPTY_EVENT_ID) {
-      i64 t = add_seconds(sched_t, r->schedule_to_start);
-      if (seq_less(t, sid, CRR_TIMEOUT_SCHEDULE_TO_START, bt, be, by)) {
-        bt = t; be = sid; by = CRR_TIMEOUT_SCHEDULE_TO_START; bj = j; bc = (tts & CRR_TTS_CREATED_SCHEDULE_TO_START) != 0;
-      }
-    } else {
-      const i64 st = r->started_time;
-      i64 t = add_seconds(st, r->start_to_close);
-      if (seq_less(t, sid, CRR_TIMEOUT_START_TO_CLOSE, bt, be, by)) {
-        bt = t; be = sid; by = CRR_TIMEOUT_START_TO_CLOSE; bj = j; bc = (tts & CRR_TTS_CREATED_START_TO_CLOSE) != 0;
-      }
-      const i32 hb = r->heartbeat;
-      if (hb > 0) {  // LastHeartBeatUpdatedTime == StartedTime on the replay path
-        i64 th = add_seconds(st, hb);
-        if (seq_less(th, sid, CRR_TIMEOUT_HEARTBEAT, bt, be, by)) {
-          bt = th; be = sid; by = CRR_TIMEOUT_HEARTBEAT; bj = j; bc = (tts & CRR_TTS_CREATED_HEARTBEAT) != 0;
-        }
-      }
-    }
-  }
-  if (!have || bc) return;
-  crr_activity_row* r = C.act(bj);
-  const i32 mask = by == CRR_TIMEOUT_START_TO_CLOSE ? CRR_TTS_CREATED_START_TO_CLOSE
-                 : by == CRR_TIMEOUT_SCHEDULE_TO_START ? CRR_TTS_CREATED_SCHEDULE_TO_START
-                 : by == CRR_TIMEOUT_SCHEDULE_TO_CLOSE ? CRR_TTS_CREATED_SCHEDULE_TO_CLOSE
-                                                       : CRR_TTS_CREATED_HEARTBEAT;
-  r->timer_task_status |= mask;
-  if (by == CRR_TIMEOUT_HEARTBEAT) r->last_hb_timeout_vis_s = unix_seconds(bt);
+__device__ __forceinline__ u32 timer_mask(i32 type) {  // TimerTypeToTimerMask (timer_sequence.go:384-400)
+  return type == CRR_TIMEOUT_START_TO_CLOSE ? CRR_TTS_CREATED_START_TO_CLOSE
+       : type == CRR_TIMEOUT_SCHEDULE_TO_START ? CRR_TTS_CREATED_SCHEDULE_TO_START
+       : type == CRR_TIMEOUT_SCHEDULE_TO_CLOSE ? CRR_TTS_CREATED_SCHEDULE_TO_CLOSE
+                                               : CRR_TTS_CREATED_HEARTBEAT;
 }
 
-__device__ __forceinline__ void create_next_user_timer(const Ctx& C, Lane& L) {
-  if (L.n_timer == 0) return;
+// Candidate timers of one pending activity (timer_sequence.go:269-381) folded into a running min.
+struct BestTimer {
   bool have = false;
-  i64 bt = 0, be = 0;
-  i32 bj = -1;
-  for (i32 j = 0; j < L.hw_timer; ++j) {
-    const crr_timer_row* r = C.timer(j);
-    if (!(r->flags & CRR_ROW_LIVE)) continue;
-    i64 t = r->expiry_time, e = r->started_id;
-    if (!have || seq_less(t, e, 0, bt, be, 0)) { have = true; bt = t; be = e; bj = j; }
+  i64 t = 0, e = 0;
+  i32 y = 0, j = -1;
+  bool created = false;
+  __device__ __forceinline__ void offer(i64 tt, i64 ee, i32 yy, i32 jj, bool cc) {
+    if (!have || seq_less(tt, ee, yy, t, e, y)) { have = true; t = tt; e = ee; y = yy; j = jj; created = cc; }
   }
-  if (!have) return;
-  crr_timer_row* r = C.timer(bj);
-  if (r->task_status == CRR_TIMER_TASK_STATUS_CREATED) return;
-  r->task_status = CRR_TIMER_TASK_STATUS_CREATED;
+};
+__device__ __forceinline__ void activity_candidates(BestTimer& B, i32 j, i64 sid, i64 sched_t, bool started,
+                                                    i64 start_t, i32 s2s, i32 s2c, i32 st2c, i32 hb, u32 tts) {
+  if (sid == CRR_EMPTY_EVENT_ID) return;
+  B.offer(add_seconds(sched_t, s2c), sid, CRR_TIMEOUT_SCHEDULE_TO_CLOSE, j, (tts & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) != 0);
+  if (!started) {
+    B.offer(add_seconds(sched_t, s2s), sid, CRR_TIMEOUT_SCHEDULE_TO_START, j, (tts & CRR_TTS_CREATED_SCHEDULE_TO_START) != 0);
+  } else {
+    B.offer(add_seconds(start_t, st2c), sid, CRR_TIMEOUT_START_TO_CLOSE, j, (tts & CRR_TTS_CREATED_START_TO_CLOSE) != 0);
+    // LastHeartBeatUpdatedTime == StartedTime on the replay path (mutable_state_builder.go:2272-2273)
+    if (hb > 0) B.offer(add_seconds(start_t, hb), sid, CRR_TIMEOUT_HEARTBEAT, j, (tts & CRR_TTS_CREATED_HEARTBEAT) != 0);
+  }
 }
 
-// ---- end-of-replay compaction: live rows sorted by event ID into slots 0..n-1 ---------------------------
 template <class R, int WORDS>
 __device__ __forceinline__ void swap_rows(R* a, R* b) {
   u64* pa = reinterpret_cast<u64*>(a);
@@ -356,29 +308,529 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
   }
 }
 
-template <class R, class IdOf>
-__device__ __forceinline__ void compact_sort(R* (Ctx::*row)(i32) const, const Ctx& C, i32 hw, i32 n, IdOf id_of) {
-  for (i32 i = 0; i < n; ++i) {
-    i32 best = -1;
-    i64 bid = 0;
-    for (i32 j = i; j < hw; ++j) {
-      const R* r = (C.*row)(j);
-      if (!(r->flags & CRR_ROW_LIVE)) continue;
-      i64 id = id_of(r);
-      if (best < 0 || id < bid) { best = j; bid = id; }
-    }
-    if (best != i) swap_rows<R, sizeof(R) / 8>((C.*row)(i), (C.*row)(best));
-  }
-}
+// ===================================================================================================
+// GlobalTables: pending maps as slot tables in the HBM output rows (any layout, unbounded).
+// ===================================================================================================
+struct GlobalTables {
+  i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
 
+  template <class R>
+  __device__ __forceinline__ static i32 free_slot(R* (Geo::*row)(i32) const, const Geo& G, i32& hw, i32 cap) {
+    for (i32 j = 0; j < hw; ++j)
+      if (!((G.*row)(j)->flags & CRR_ROW_LIVE)) return j;
+    if (hw >= cap) return -1;
+    return hw++;
+  }
+  template <class R>
+  __device__ __forceinline__ static i32 find_initiated(R* (Geo::*row)(i32) const, const Geo& G, i32 hw, i64 id) {
+    for (i32 j = 0; j < hw; ++j) {
+      const R* r = (G.*row)(j);
+      if ((r->flags & CRR_ROW_LIVE) && r->initiated_id == id) return j;
+    }
+    return -1;
+  }
+  __device__ __forceinline__ i32 find_act_by_id(const Geo& G, i64 sched) const {
+    for (i32 j = 0; j < hw_act; ++j) {
+      const crr_activity_row* r = G.act(j);
+      if ((r->flags & CRR_ROW_LIVE) && r->schedule_id == sched) return j;
+    }
+    return -1;
+  }
+  __device__ __forceinline__ i32 find_act_mapped(const Geo& G, u32 key) const {
+    for (i32 j = 0; j < hw_act; ++j) {
+      const crr_activity_row* r = G.act(j);
+      if ((r->flags & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && r->key == key) return j;
+    }
+    return -1;
+  }
+  __device__ __forceinline__ i32 find_timer(const Geo& G, u32 key) const {
+    for (i32 j = 0; j < hw_timer; ++j) {
+      const crr_timer_row* r = G.timer(j);
+      if ((r->flags & CRR_ROW_LIVE) && r->key == key) return j;
+    }
+    return -1;
+  }
+
+  // ReplicateActivityTaskScheduledEvent (mutable_state_builder.go:2142-2197)
+  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
+    i32 m = find_act_mapped(G, row.key);  // pendingActivityIDToEventID[ActivityID] is overwritten
+    if (m >= 0) G.act(m)->flags &= ~CRR_ROW_MAPPED;
+    i32 j = free_slot<crr_activity_row>(&Geo::act, G, hw_act, G.act_cap);
+    if (j < 0) return CRR_ERR_CAPACITY;
+    *G.act(j) = row;
+    ++L.n_act;
+    return CRR_OK;
+  }
+  // ReplicateActivityTaskStartedEvent (:2254-2276)
+  __device__ __forceinline__ bool act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+    i32 j = find_act_by_id(G, sched);
+    if (j < 0) return false;
+    crr_activity_row* r = G.act(j);
+    r->version = ver;
+    r->started_id = id;
+    r->started_src = s;
+    r->started_time = ts;
+    return true;
+  }
+  // DeleteActivity (:1310-1339)
+  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
+    i32 j = find_act_by_id(G, sched);
+    if (j < 0) { ++L.inconsistencies; return; }
+    crr_activity_row* r = G.act(j);
+    u32 f = r->flags;
+    u32 key = r->key;
+    r->flags = f & ~(CRR_ROW_LIVE | CRR_ROW_MAPPED);
+    --L.n_act;
+    if (f & CRR_ROW_MAPPED) return;
+    i32 m = find_act_mapped(G, key);
+    if (m >= 0) G.act(m)->flags &= ~CRR_ROW_MAPPED;
+    else ++L.inconsistencies;
+  }
+  // ReplicateActivityTaskCancelRequestedEvent (:2444-2467)
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver) {
+    i32 j = find_act_mapped(G, key);
+    if (j < 0) return;
+    crr_activity_row* r = G.act(j);
+    r->version = ver;
+    r->flags |= CRR_ROW_CANCEL_REQUESTED;
+    r->cancel_request_id = id;
+  }
+  // ReplicateTimerStartedEvent (:3057-3081)
+  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
+    i32 j = find_timer(G, row.key);
+    if (j < 0) {
+      j = free_slot<crr_timer_row>(&Geo::timer, G, hw_timer, G.timer_cap);
+      if (j < 0) return CRR_ERR_CAPACITY;
+      ++L.n_timer;
+    }
+    *G.timer(j) = row;
+    return CRR_OK;
+  }
+  // DeleteUserTimer (:1390-1419)
+  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
+    i32 j = find_timer(G, key);
+    if (j < 0) { ++L.inconsistencies; return; }
+    G.timer(j)->flags = 0;
+    --L.n_timer;
+  }
+  // ReplicateStartChildWorkflowExecutionInitiatedEvent (:3417-3453)
+  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
+    i32 j = free_slot<crr_child_row>(&Geo::child, G, hw_child, G.child_cap);
+    if (j < 0) return CRR_ERR_CAPACITY;
+    *G.child(j) = row;
+    ++L.n_child;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+    i32 j = find_initiated<crr_child_row>(&Geo::child, G, hw_child, init);
+    if (j < 0) return false;
+    crr_child_row* r = G.child(j);
+    r->started_id = id;
+    r->started_src = s;
+    return true;
+  }
+  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
+    i32 j = find_initiated<crr_child_row>(&Geo::child, G, hw_child, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    G.child(j)->flags = 0;
+    --L.n_child;
+  }
+  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
+    i32 j = is_rc ? free_slot<crr_initiated_row>(&Geo::rc, G, hw_rc, G.rc_cap)
+                  : free_slot<crr_initiated_row>(&Geo::sig, G, hw_sig, G.sig_cap);
+    if (j < 0) return CRR_ERR_CAPACITY;
+    *(is_rc ? G.rc(j) : G.sig(j)) = row;
+    if (is_rc) ++L.n_rc; else ++L.n_sig;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
+    i32 j = is_rc ? find_initiated<crr_initiated_row>(&Geo::rc, G, hw_rc, init)
+                  : find_initiated<crr_initiated_row>(&Geo::sig, G, hw_sig, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    (is_rc ? G.rc(j) : G.sig(j))->flags = 0;
+    if (is_rc) --L.n_rc; else --L.n_sig;
+  }
+  // reset points: rows in HBM, append-only
+  __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    *G.rp(L.n_rp++) = row;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
+    for (i32 i = 0; i < L.n_rp; ++i)
+      if (G.rp(i)->key == key) return true;
+    return false;
+  }
+  // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+    if (L.n_act > 0) {
+      BestTimer B;
+      for (i32 j = 0; j < hw_act; ++j) {
+        const crr_activity_row* r = G.act(j);
+        if (!(r->flags & CRR_ROW_LIVE)) continue;
+        activity_candidates(B, j, r->schedule_id, r->scheduled_time, r->started_id != CRR_EMPTY_EVENT_ID,
+                            r->started_time, r->schedule_to_start, r->schedule_to_close, r->start_to_close,
+                            r->heartbeat, (u32)r->timer_task_status);
+      }
+      if (B.have && !B.created) {
+        crr_activity_row* r = G.act(B.j);
+        r->timer_task_status |= timer_mask(B.y);
+        if (B.y == CRR_TIMEOUT_HEARTBEAT) r->last_hb_timeout_vis_s = unix_seconds(B.t);
+      }
+    }
+    if (L.n_timer > 0) {
+      BestTimer B;
+      for (i32 j = 0; j < hw_timer; ++j) {
+        const crr_timer_row* r = G.timer(j);
+        if (!(r->flags & CRR_ROW_LIVE)) continue;
+        B.offer(r->expiry_time, r->started_id, 0, j, r->task_status == CRR_TIMER_TASK_STATUS_CREATED);
+      }
+      if (B.have && !B.created) G.timer(B.j)->task_status = CRR_TIMER_TASK_STATUS_CREATED;
+    }
+  }
+  template <class R, class IdOf>
+  __device__ __forceinline__ static void compact_sort(R* (Geo::*row)(i32) const, const Geo& G, i32 hw, i32 n, IdOf id_of) {
+    for (i32 i = 0; i < n; ++i) {
+      i32 best = -1;
+      i64 bid = 0;
+      for (i32 j = i; j < hw; ++j) {
+        const R* r = (G.*row)(j);
+        if (!(r->flags & CRR_ROW_LIVE)) continue;
+        i64 id = id_of(r);
+        if (best < 0 || id < bid) { best = j; bid = id; }
+      }
+      if (best != i) swap_rows<R, sizeof(R) / 8>((G.*row)(i), (G.*row)(best));
+    }
+  }
+  // live rows sorted by event ID into slots 0..n-1
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+    compact_sort<crr_activity_row>(&Geo::act, G, hw_act, L.n_act, [](const crr_activity_row* r) { return r->schedule_id; });
+    compact_sort<crr_timer_row>(&Geo::timer, G, hw_timer, L.n_timer, [](const crr_timer_row* r) { return r->started_id; });
+    compact_sort<crr_child_row>(&Geo::child, G, hw_child, L.n_child, [](const crr_child_row* r) { return r->initiated_id; });
+    compact_sort<crr_initiated_row>(&Geo::rc, G, hw_rc, L.n_rc, [](const crr_initiated_row* r) { return r->initiated_id; });
+    compact_sort<crr_initiated_row>(&Geo::sig, G, hw_sig, L.n_sig, [](const crr_initiated_row* r) { return r->initiated_id; });
+  }
+  // sorted IDs for the checksum (after finalize)
+  __device__ __forceinline__ i64 timer_id(const Geo& G, i32 i) const { return G.timer(i)->started_id; }
+  __device__ __forceinline__ i64 act_id(const Geo& G, i32 i) const { return G.act(i)->schedule_id; }
+  __device__ __forceinline__ i64 sig_id(const Geo& G, i32 i) const { return G.sig(i)->initiated_id; }
+  __device__ __forceinline__ i64 rc_id(const Geo& G, i32 i) const { return G.rc(i)->initiated_id; }
+  __device__ __forceinline__ i64 child_id(const Geo& G, i32 i) const { return G.child(i)->initiated_id; }
+};
+
+// ===================================================================================================
+// LdsTables: LDS index of the live pending entries; HBM rows written, not read, until finalize.
+// LDS arrays are [slot][256 lanes] so lane-parallel accesses hit consecutive banks.
+// ===================================================================================================
+constexpr int A_SLOTS = CRR_LDS_ACT, T_SLOTS = CRR_LDS_TIMER, C_SLOTS = CRR_LDS_CHILD, R_SLOTS = CRR_LDS_RC,
+              S_SLOTS = CRR_LDS_SIG, P_SLOTS = CRR_LDS_RP;
+// activity LDS flag bits (row bits + STARTED; TimerTaskStatus in bits 8..11)
+constexpr u32 LF_STARTED = 32u;
+constexpr int LF_TTS_SHIFT = 8;
+
+struct LdsArena {
+  i64 a_sid[A_SLOTS][kBlock];
+  i64 a_sched_t[A_SLOTS][kBlock];
+  i64 a_start_t[A_SLOTS][kBlock];
+  int4 a_to[A_SLOTS][kBlock];   // s2s, s2c, st2c, hb
+  u32 a_key[A_SLOTS][kBlock];
+  u32 a_fl[A_SLOTS][kBlock];
+  i64 t_sid[T_SLOTS][kBlock];
+  i64 t_exp[T_SLOTS][kBlock];
+  u32 t_key[T_SLOTS][kBlock];
+  u32 t_fl[T_SLOTS][kBlock];
+  i64 c_id[C_SLOTS][kBlock];
+  u32 c_fl[C_SLOTS][kBlock];
+  i64 r_id[R_SLOTS][kBlock];
+  u32 r_fl[R_SLOTS][kBlock];
+  i64 s_id[S_SLOTS][kBlock];
+  u32 s_fl[S_SLOTS][kBlock];
+  u32 p_key[P_SLOTS][kBlock];
+};
+
+struct LdsTables {
+  LdsArena* M;
+  int t;  // threadIdx.x
+
+  __device__ __forceinline__ void init(LdsArena* arena) {
+    M = arena;
+    t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < C_SLOTS; ++j) M->c_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < R_SLOTS; ++j) M->r_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < S_SLOTS; ++j) M->s_fl[j][t] = 0;
+  }
+
+  __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = A_SLOTS - 1; j >= 0; --j)
+      if ((M->a_fl[j][t] & CRR_ROW_LIVE) && M->a_sid[j][t] == sched) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = A_SLOTS - 1; j >= 0; --j) {
+      u32 f = M->a_fl[j][t];
+      if ((f & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && M->a_key[j][t] == key) hit = j;
+    }
+    return hit;
+  }
+
+  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
+    i32 m = find_act_mapped(row.key);
+    i32 j = -1;
+#pragma unroll
+    for (int k = A_SLOTS - 1; k >= 0; --k)
+      if (!(M->a_fl[k][t] & CRR_ROW_LIVE)) j = k;
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= G.act_cap) return CRR_ERR_CAPACITY;
+    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+    M->a_sid[j][t] = row.schedule_id;
+    M->a_sched_t[j][t] = row.scheduled_time;
+    M->a_start_t[j][t] = row.started_time;
+    M->a_to[j][t] = make_int4(row.schedule_to_start, row.schedule_to_close, row.start_to_close, row.heartbeat);
+    M->a_key[j][t] = row.key;
+    M->a_fl[j][t] = row.flags;
+    *G.act(j) = row;  // HBM row: written now, read only by finalize
+    ++L.n_act;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+    i32 j = find_act_by_id(sched);
+    if (j < 0) return false;
+    M->a_start_t[j][t] = ts;
+    M->a_fl[j][t] |= LF_STARTED;
+    crr_activity_row* r = G.act(j);
+    r->version = ver;
+    r->started_id = id;
+    r->started_src = s;
+    r->started_time = ts;
+    return true;
+  }
+  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
+    i32 j = find_act_by_id(sched);
+    if (j < 0) { ++L.inconsistencies; return; }
+    u32 f = M->a_fl[j][t];
+    u32 key = M->a_key[j][t];
+    M->a_fl[j][t] = 0;
+    --L.n_act;
+    if (f & CRR_ROW_MAPPED) return;
+    i32 m = find_act_mapped(key);
+    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+    else ++L.inconsistencies;
+  }
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver) {
+    i32 j = find_act_mapped(key);
+    if (j < 0) return;
+    M->a_fl[j][t] |= CRR_ROW_CANCEL_REQUESTED;
+    crr_activity_row* r = G.act(j);
+    r->version = ver;
+    r->cancel_request_id = id;
+  }
+
+  __device__ __forceinline__ i32 find_timer(u32 key) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = T_SLOTS - 1; j >= 0; --j)
+      if ((M->t_fl[j][t] & CRR_ROW_LIVE) && M->t_key[j][t] == key) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
+    i32 j = find_timer(row.key);
+    if (j < 0) {
+#pragma unroll
+      for (int k = T_SLOTS - 1; k >= 0; --k)
+        if (!(M->t_fl[k][t] & CRR_ROW_LIVE)) j = k;
+      if (j < 0) return CRR_INTERNAL_RETRY;
+      if (j >= G.timer_cap) return CRR_ERR_CAPACITY;
+      ++L.n_timer;
+    }
+    M->t_sid[j][t] = row.started_id;
+    M->t_exp[j][t] = row.expiry_time;
+    M->t_key[j][t] = row.key;
+    M->t_fl[j][t] = CRR_ROW_LIVE;  // bit 1 (value 2) below = TaskStatus created
+    *G.timer(j) = row;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
+    i32 j = find_timer(key);
+    if (j < 0) { ++L.inconsistencies; return; }
+    M->t_fl[j][t] = 0;
+    --L.n_timer;
+  }
+
+  template <int N>
+  __device__ __forceinline__ i32 find_init(const i64 (*ids)[kBlock], const u32 (*fl)[kBlock], i64 id) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j)
+      if ((fl[j][t] & CRR_ROW_LIVE) && ids[j][t] == id) hit = j;
+    return hit;
+  }
+  template <int N>
+  __device__ __forceinline__ i32 free_init(const u32 (*fl)[kBlock]) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j)
+      if (!(fl[j][t] & CRR_ROW_LIVE)) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
+    i32 j = free_init<C_SLOTS>(M->c_fl);
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= G.child_cap) return CRR_ERR_CAPACITY;
+    M->c_id[j][t] = row.initiated_id;
+    M->c_fl[j][t] = CRR_ROW_LIVE;
+    *G.child(j) = row;
+    ++L.n_child;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+    i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
+    if (j < 0) return false;
+    crr_child_row* r = G.child(j);
+    r->started_id = id;
+    r->started_src = s;
+    return true;
+  }
+  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
+    i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    M->c_fl[j][t] = 0;
+    --L.n_child;
+  }
+  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
+    i32 j = is_rc ? free_init<R_SLOTS>(M->r_fl) : free_init<S_SLOTS>(M->s_fl);
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= (is_rc ? G.rc_cap : G.sig_cap)) return CRR_ERR_CAPACITY;
+    if (is_rc) { M->r_id[j][t] = row.initiated_id; M->r_fl[j][t] = CRR_ROW_LIVE; *G.rc(j) = row; ++L.n_rc; }
+    else { M->s_id[j][t] = row.initiated_id; M->s_fl[j][t] = CRR_ROW_LIVE; *G.sig(j) = row; ++L.n_sig; }
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
+    i32 j = is_rc ? find_init<R_SLOTS>(M->r_id, M->r_fl, init) : find_init<S_SLOTS>(M->s_id, M->s_fl, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    if (is_rc) { M->r_fl[j][t] = 0; --L.n_rc; }
+    else { M->s_fl[j][t] = 0; --L.n_sig; }
+  }
+  __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+    if (L.n_rp >= P_SLOTS) return CRR_INTERNAL_RETRY;
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    M->p_key[L.n_rp][t] = row.key;
+    *G.rp(L.n_rp++) = row;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < P_SLOTS; ++i)
+      if (i < L.n_rp && M->p_key[i][t] == key) hit = true;
+    return hit;
+  }
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+    if (L.n_act > 0) {
+      BestTimer B;
+#pragma unroll
+      for (int j = 0; j < A_SLOTS; ++j) {
+        const u32 f = M->a_fl[j][t];
+        if (!(f & CRR_ROW_LIVE)) continue;
+        const int4 to = M->a_to[j][t];
+        activity_candidates(B, j, M->a_sid[j][t], M->a_sched_t[j][t], (f & LF_STARTED) != 0, M->a_start_t[j][t],
+                            to.x, to.y, to.z, to.w, f >> LF_TTS_SHIFT);
+      }
+      if (B.have && !B.created) {
+        M->a_fl[B.j][t] |= timer_mask(B.y) << LF_TTS_SHIFT;
+        if (B.y == CRR_TIMEOUT_HEARTBEAT) G.act(B.j)->last_hb_timeout_vis_s = unix_seconds(B.t);
+      }
+    }
+    if (L.n_timer > 0) {
+      BestTimer B;
+#pragma unroll
+      for (int j = 0; j < T_SLOTS; ++j) {
+        const u32 f = M->t_fl[j][t];
+        if (!(f & CRR_ROW_LIVE)) continue;
+        B.offer(M->t_exp[j][t], M->t_sid[j][t], 0, j, (f & 2u) != 0);
+      }
+      if (B.have && !B.created) M->t_fl[B.j][t] |= 2u;
+    }
+  }
+  // Write the LDS-held row fields, then sort live entries by event ID into slots 0..n-1 (LDS and HBM).
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+#pragma unroll
+    for (int j = 0; j < A_SLOTS; ++j) {
+      const u32 f = M->a_fl[j][t];
+      if (!(f & CRR_ROW_LIVE)) continue;
+      crr_activity_row* r = G.act(j);
+      r->timer_task_status = (i32)((f >> LF_TTS_SHIFT) & 0xF);
+      r->flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
+    }
+#pragma unroll
+    for (int j = 0; j < T_SLOTS; ++j) {
+      const u32 f = M->t_fl[j][t];
+      if (!(f & CRR_ROW_LIVE)) continue;
+      G.timer(j)->task_status = (f & 2u) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+    }
+    sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
+      swap_rows<crr_activity_row, sizeof(crr_activity_row) / 8>(G.act(i), G.act(b));
+    });
+    sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
+      swap_rows<crr_timer_row, sizeof(crr_timer_row) / 8>(G.timer(i), G.timer(b));
+    });
+    sort_slots<C_SLOTS>(M->c_id, M->c_fl, L.n_child, [&](int i, int b) {
+      swap_rows<crr_child_row, sizeof(crr_child_row) / 8>(G.child(i), G.child(b));
+    });
+    sort_slots<R_SLOTS>(M->r_id, M->r_fl, L.n_rc, [&](int i, int b) {
+      swap_rows<crr_initiated_row, sizeof(crr_initiated_row) / 8>(G.rc(i), G.rc(b));
+    });
+    sort_slots<S_SLOTS>(M->s_id, M->s_fl, L.n_sig, [&](int i, int b) {
+      swap_rows<crr_initiated_row, sizeof(crr_initiated_row) / 8>(G.sig(i), G.sig(b));
+    });
+  }
+  // selection sort of the live LDS slots by id; swaps the id/flag words in LDS and the HBM rows
+  template <int N, class SwapRows>
+  __device__ __forceinline__ void sort_slots(i64 (*ids)[kBlock], u32 (*fl)[kBlock], i32 n, SwapRows swap_rows_fn) {
+    for (i32 i = 0; i < n; ++i) {
+      i32 best = -1;
+      i64 bid = 0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        if (j < i || !(fl[j][t] & CRR_ROW_LIVE)) continue;
+        const i64 id = ids[j][t];
+        if (best < 0 || id < bid) { best = j; bid = id; }
+      }
+      if (best != i) {
+        swap_rows_fn(i, best);
+        i64 x = ids[i][t]; ids[i][t] = ids[best][t]; ids[best][t] = x;
+        u32 y = fl[i][t]; fl[i][t] = fl[best][t]; fl[best][t] = y;
+      }
+    }
+  }
+  __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return M->t_sid[i][t]; }
+  __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return M->a_sid[i][t]; }
+  __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return M->s_id[i][t]; }
+  __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return M->r_id[i][t]; }
+  __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return M->c_id[i][t]; }
+};
+
+// ---------------------------------------------------------------------------------------------------
 // generateMutableStateChecksum (checksum.go:36-114) -> GenerateCRC32 (crc.go:35-54) over
-// 0x59 + MutableStateChecksumPayload.Encode (.gen/go/checksum/checksum.go:539-821).  Reads the
-// numeric execution image R and the sorted live rows (slots 0..n-1) of this workflow.
-__device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const Ctx& C, const crr_workflow* wfp,
+// 0x59 + MutableStateChecksumPayload.Encode (.gen/go/checksum/checksum.go:539-821).
+template <class IDS>
+__device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids, const Geo& G, const crr_workflow* wfp,
                                            const uint8_t* arena, const u32* tables, u32* out_len) {
   Crc K;
   K.init(tables);
-  K.u8(0x59);                                                     // preambleVersion0
+  K.u8(0x59);                                                            // preambleVersion0
   K.field(2, 10); K.u8((R.flags & CRR_EXEC_CANCEL_REQUESTED) ? 1 : 0);   // CancelRequested
   K.field(6, 15); K.be16((u32)(uint16_t)(int16_t)R.state);              // State
   K.field(10, 23); K.be64(R.last_first_event_id);
@@ -389,24 +841,24 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const Ctx& C, 
   K.field(10, 36); K.be64(R.decision_version);
   K.field(10, 37); K.be64(R.decision_schedule_id);
   K.field(10, 38); K.be64(R.decision_started_id);
-  K.list_i64_header(45, (u32)R.n_timer);                          // PendingTimerStartedIDs
-  for (i32 i = 0; i < R.n_timer; ++i) K.be64(C.timer(i)->started_id);
-  K.list_i64_header(46, (u32)R.n_activity);                       // PendingActivityScheduledIDs
-  for (i32 i = 0; i < R.n_activity; ++i) K.be64(C.act(i)->schedule_id);
-  K.list_i64_header(47, (u32)R.n_signal);                         // PendingSignalInitiatedIDs
-  for (i32 i = 0; i < R.n_signal; ++i) K.be64(C.sig(i)->initiated_id);
-  K.list_i64_header(48, (u32)R.n_rc);                             // PendingReqCancelInitiatedIDs
-  for (i32 i = 0; i < R.n_rc; ++i) K.be64(C.rc(i)->initiated_id);
-  K.list_i64_header(49, (u32)R.n_child);                          // PendingChildInitiatedIDs
-  for (i32 i = 0; i < R.n_child; ++i) K.be64(C.child(i)->initiated_id);
-  K.field(11, 55); K.be32(0);                                     // StickyTaskListName ""
-  K.field(12, 56);                                                // VersionHistories (shared.go:91639)
-  K.field(8, 10); K.be32(0);                                      //   CurrentVersionHistoryIndex
-  K.field(15, 20); K.push(12u | ((u64)__builtin_bswap32(1u) << 8), 5);  // list<struct>, 1 history
+  K.list_header(45, 10, (u32)R.n_timer);                                 // PendingTimerStartedIDs
+  for (i32 i = 0; i < R.n_timer; ++i) K.be64(ids.timer_id(G, i));
+  K.list_header(46, 10, (u32)R.n_activity);                              // PendingActivityScheduledIDs
+  for (i32 i = 0; i < R.n_activity; ++i) K.be64(ids.act_id(G, i));
+  K.list_header(47, 10, (u32)R.n_signal);                                // PendingSignalInitiatedIDs
+  for (i32 i = 0; i < R.n_signal; ++i) K.be64(ids.sig_id(G, i));
+  K.list_header(48, 10, (u32)R.n_rc);                                    // PendingReqCancelInitiatedIDs
+  for (i32 i = 0; i < R.n_rc; ++i) K.be64(ids.rc_id(G, i));
+  K.list_header(49, 10, (u32)R.n_child);                                 // PendingChildInitiatedIDs
+  for (i32 i = 0; i < R.n_child; ++i) K.be64(ids.child_id(G, i));
+  K.field(11, 55); K.be32(0);                                            // StickyTaskListName ""
+  K.field(12, 56);                                                       // VersionHistories (shared.go:91639)
+  K.field(8, 10); K.be32(0);                                             //   CurrentVersionHistoryIndex
+  K.list_header(20, 12, 1u);                                             //   Histories: list<struct> of 1
   u32 toff = 0, tlen = 0;
   if (R.token_src == 1) { toff = wfp->start_token_off; tlen = wfp->start_token_len; }
   if (R.token_src == 2) { toff = wfp->final_token_off; tlen = wfp->final_token_len; }
-  K.field(11, 10); K.be32(tlen);                                  //   VersionHistory.BranchToken (shared.go:92043)
+  K.field(11, 10); K.be32(tlen);                                         //   VersionHistory.BranchToken (shared.go:92043)
   {
     const uint8_t* tp = arena + toff;
     u32 i = 0;
@@ -416,9 +868,9 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const Ctx& C, 
     }
     for (; i < tlen; ++i) K.u8(tp[i]);
   }
-  K.field(15, 20); K.push(12u | ((u64)__builtin_bswap32((u32)R.n_vh_items) << 8), 5);
-  for (i32 i = 0; i < R.n_vh_items; ++i) {                        //   VersionHistoryItem (shared.go:92375)
-    const crr_vh_item* it = C.vh(i);
+  K.list_header(20, 12, (u32)R.n_vh_items);
+  for (i32 i = 0; i < R.n_vh_items; ++i) {                               //   VersionHistoryItem (shared.go:92375)
+    const crr_vh_item* it = G.vh(i);
     K.field(10, 10); K.be64(it->event_id);
     K.field(10, 20); K.be64(it->version);
     K.u8(0);
@@ -430,29 +882,16 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const Ctx& C, 
   return K.finish();
 }
 
-// ---- the kernel ------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs out, int phase) {
-  __shared__ u32 crc_tables[8 * 256];
-  build_crc_tables(crc_tables);
+// ---------------------------------------------------------------------------------------------------
+struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
 
-  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= in.n_wf) return;
-  const crr_workflow* wfp = in.wf + w;
-  const i32 wflags = wfp->flags;
-  if (((wflags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
-
-  Ctx C;
-  C.in = in;
-  C.out = out;
-  C.st = in.stride;
-  C.act_base = wfp->act_base; C.timer_base = wfp->timer_base; C.child_base = wfp->child_base;
-  C.rc_base = wfp->rc_base; C.sig_base = wfp->sig_base; C.vh_base = wfp->vh_base; C.rp_base = wfp->rp_base;
-  C.act_cap = wfp->act_cap; C.timer_cap = wfp->timer_cap; C.child_cap = wfp->child_cap; C.rc_cap = wfp->rc_cap;
-  C.sig_cap = wfp->sig_cap; C.vh_cap = wfp->vh_cap; C.rp_cap = wfp->rp_cap;
-
-  const i64 ev_begin = wfp->ev_begin;
+template <class P>
+__device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
+                                            const Geo& G, P& T, i64 ev_begin, const u32* crc_tables) {
   const i32 n_ev = wfp->ev_count;
   const i32 empty_at = wfp->empty_batch_at;
+  const i64 st = in.stride;
+  const i64 now_ns = wfp->now_ns;
 
   // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
   Lane L;
@@ -465,10 +904,8 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
   L.decision_timeout = 0; L.decision_request_src = CRR_SRC_EMPTY_UUID;
   L.signal_count = 0; L.decision_start_to_close = 0; L.start_src = -1; L.flags = 0;
   L.current_version = wfp->init_version;
-  L.now_ns = wfp->now_ns;
   L.vh_last_id = 0; L.vh_last_ver = 0; L.vh_n = 0; L.token_src = 0;
-  L.n_act = L.hw_act = L.n_timer = L.hw_timer = L.n_child = L.hw_child = 0;
-  L.n_rc = L.hw_rc = L.n_sig = L.hw_sig = L.n_rp = 0;
+  L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = 0;
   L.inconsistencies = 0;
   L.status = CRR_OK; L.fail_step = -1;
 
@@ -483,13 +920,25 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
 
   i64 batch_first_id = 0;
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
+#define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
 
+  // Software pipeline: the 8 column loads of step s+1 are issued before step s is processed.
+  auto load_ev = [&](i32 step) {
+    Ev e;
+    const i64 ix = ev_begin + (i64)step * st;
+    e.et = col_type[ix]; e.id = col_id[ix]; e.ver = col_ver[ix]; e.ts = col_ts[ix];
+    e.task = col_task[ix]; e.ref = col_ref[ix]; e.key = col_key[ix]; e.aux = col_aux[ix];
+    return e;
+  };
+  Ev nx;
+  if (n_ev > 0) nx = load_ev(0);
   for (i32 s = 0; s < n_ev; ++s) {
     if (s == empty_at) FAIL(CRR_ERR_EMPTY_HISTORY, s);  // state_builder.go:98-100
-    const i64 ix = ev_begin + (i64)s * C.st;
-    const u32 et = col_type[ix];
-    const i64 id = col_id[ix];
-    const i64 ver = col_ver[ix];
+    const Ev ev = nx;
+    if (s + 1 < n_ev) nx = load_ev(s + 1);
+    const u32 et = ev.et;
+    const i64 id = ev.id;
+    const i64 ver = ev.ver;
     const i32 t = et & CRR_ETYPE_MASK;
     if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = id;  // firstEvent := history[0] (:101)
 
@@ -503,31 +952,30 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
     // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
     if (id < 0 || (ver < 0 && ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, s);
     if (L.vh_n == 0) {
-      if (C.vh_cap < 1) FAIL(CRR_ERR_CAPACITY, s);
+      if (G.vh_cap < 1) FAIL(CRR_ERR_CAPACITY, s);
       L.vh_last_id = id; L.vh_last_ver = ver; L.vh_n = 1;
     } else if (ver < L.vh_last_ver) {
       FAIL(CRR_ERR_VH_LOWER_VERSION, s);
     } else if (id <= L.vh_last_id) {
       FAIL(CRR_ERR_VH_EVENT_ID_NOT_INCREASING, s);
     } else if (ver > L.vh_last_ver) {
-      if (L.vh_n >= C.vh_cap) FAIL(CRR_ERR_CAPACITY, s);
-      crr_vh_item* it = C.vh(L.vh_n - 1);
+      if (L.vh_n >= G.vh_cap) FAIL(CRR_ERR_CAPACITY, s);
+      crr_vh_item* it = G.vh(L.vh_n - 1);
       it->event_id = L.vh_last_id;
       it->version = L.vh_last_ver;
       L.vh_last_id = id; L.vh_last_ver = ver; ++L.vh_n;
     } else {
       L.vh_last_id = id;
     }
-    L.last_event_task_id = col_task[ix];  // :129
+    L.last_event_task_id = ev.task;  // :129
 
     switch (t) {
       case CRR_EV_WORKFLOW_EXECUTION_STARTED: {  // :132-183 -> mutable_state_builder.go:1751-1829
-        const crr_start_side ss = in.start_side[col_aux[ix]];
+        const crr_start_side ss = in.start_side[ev.aux];
         if (ss.parent_domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         L.decision_start_to_close = ss.decision_start_to_close;
         L.start_src = s;
-        int e = update_state(L, CRR_STATE_CREATED, CRR_CLOSE_NONE);
-        if (e) FAIL(e, s);
+        CHECK(update_state(L, CRR_STATE_CREATED, CRR_CLOSE_NONE));
         L.last_processed_event = CRR_EMPTY_EVENT_ID;
         L.last_first_event_id = id;
         L.decision_version = CRR_EMPTY_VERSION;
@@ -536,15 +984,15 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
         L.decision_request_src = CRR_SRC_EMPTY_UUID;
         L.decision_timeout = 0;
         // AutoResetPoints = rolloverAutoResetPointsWithExpiringTime(PrevAutoResetPoints, ...) (:3343-3364)
-        L.n_rp = 0;
+        T.rp_reset(L);
         L.flags = (L.flags & ~CRR_EXEC_RESET_POINTS_SET) | (ss.prev_reset_count != -1 ? CRR_EXEC_RESET_POINTS_SET : 0u);
         for (i32 i = 0; i < ss.prev_reset_count; ++i) {
-          if (L.n_rp >= C.rp_cap) FAIL(CRR_ERR_CAPACITY, s);
-          crr_reset_point_row* rp = C.rp(L.n_rp++);
-          rp->src = s;
-          rp->prev_index = i;
-          rp->key = in.reset_keys[ss.prev_reset_key_off + i];
-          rp->flags = CRR_ROW_LIVE;
+          crr_reset_point_row rp;
+          rp.src = s;
+          rp.prev_index = i;
+          rp.key = in.reset_keys[ss.prev_reset_key_off + i];
+          rp.flags = CRR_ROW_LIVE;
+          CHECK(T.rp_push(L, G, rp));
         }
         // GenerateDelayedDecisionTasks (mutable_state_task_generator.go:242-281)
         if (ss.first_decision_backoff > 0 && ss.initiator != CRR_INITIATOR_NIL &&
@@ -554,197 +1002,135 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
         break;
       }
       case CRR_EV_DECISION_TASK_SCHEDULED: {  // :185-208 -> decision_task_manager.go:129-166
-        if (L.state != CRR_STATE_ZOMBIE) {
-          int e = update_state(L, CRR_STATE_RUNNING, CRR_CLOSE_NONE);
-          if (e) FAIL(e, s);
-        }
-        const i64 ts = col_ts[ix];
-        update_decision(L, ver, id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, col_aux[ix], col_ref[ix], 0, ts, ts);
+        if (L.state != CRR_STATE_ZOMBIE) CHECK(update_state(L, CRR_STATE_RUNNING, CRR_CLOSE_NONE));
+        update_decision(L, ver, id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, ev.aux, ev.ref, 0, ev.ts, ev.ts);
         break;
       }
       case CRR_EV_DECISION_TASK_STARTED: {  // :210-228 -> decision_task_manager.go:199-242
-        const i64 sched = col_ref[ix];
-        if (sched != L.decision_schedule_id) FAIL(CRR_ERR_DECISION_NOT_FOUND, s);
-        update_decision(L, ver, sched, id, s, L.decision_timeout, 0, col_ts[ix], L.decision_scheduled_ts,
+        if (ev.ref != L.decision_schedule_id) FAIL(CRR_ERR_DECISION_NOT_FOUND, s);
+        update_decision(L, ver, ev.ref, id, s, L.decision_timeout, 0, ev.ts, L.decision_scheduled_ts,
                         L.decision_orig_scheduled_ts);
         break;
       }
       case CRR_EV_DECISION_TASK_COMPLETED: {  // :230-235 -> decision_task_manager.go:244-249, :827-838
         update_decision(L, CRR_EMPTY_VERSION, CRR_EMPTY_EVENT_ID, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, 0, 0, 0, 0,
                         L.decision_orig_scheduled_ts);  // DeleteDecision
-        L.last_processed_event = col_ref[ix];
-        const u32 key = col_key[ix];
-        if (key != 0) {  // addBinaryCheckSumIfNotExists (mutable_state_builder.go:1911-1974)
-          bool exists = false;
-          for (i32 i = 0; i < L.n_rp; ++i)
-            if (C.rp(i)->key == key) { exists = true; break; }
-          if (!exists) {
-            if (L.n_rp >= C.rp_cap) FAIL(CRR_ERR_CAPACITY, s);
-            crr_reset_point_row* rp = C.rp(L.n_rp++);
-            rp->src = s;
-            rp->prev_index = -1;
-            rp->key = key;
-            const bool resettable = L.n_child == 0 && L.n_rc == 0 && L.n_sig == 0;  // CheckResettable (:1977-1994)
-            rp->flags = CRR_ROW_LIVE | (resettable ? CRR_ROW_RESETTABLE : 0u);
-            L.flags |= CRR_EXEC_RESET_POINTS_SET;
-          }
+        L.last_processed_event = ev.ref;
+        if (ev.key != 0 && !T.rp_has(L, G, ev.key)) {  // addBinaryCheckSumIfNotExists (:1911-1974)
+          crr_reset_point_row rp;
+          rp.src = s;
+          rp.prev_index = -1;
+          rp.key = ev.key;
+          const bool resettable = L.n_child == 0 && L.n_rc == 0 && L.n_sig == 0;  // CheckResettable (:1977-1994)
+          rp.flags = CRR_ROW_LIVE | (resettable ? CRR_ROW_RESETTABLE : 0u);
+          CHECK(T.rp_push(L, G, rp));
+          L.flags |= CRR_EXEC_RESET_POINTS_SET;
         }
         break;
       }
       case CRR_EV_DECISION_TASK_TIMED_OUT:  // :237-259 (StickyTaskList == "": incrementAttempt)
       case CRR_EV_DECISION_TASK_FAILED:     // :261-281
-        fail_decision_and_transient(L);
+        fail_decision_and_transient(L, now_ns);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
-        const crr_activity_side as = in.act_side[col_aux[ix]];
+        const crr_activity_side as = in.act_side[ev.aux];
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-        const u32 key = col_key[ix];
-        // pendingActivityIDToEventID[ActivityID] = ScheduleID: the previous mapping of this ID goes away
-        i32 m = find_act_mapped(C, L, key);
-        if (m >= 0) C.act(m)->flags &= ~CRR_ROW_MAPPED;
-        i32 j = free_slot<crr_activity_row>(&Ctx::act, C, L.hw_act, C.act_cap);
-        if (j < 0) FAIL(CRR_ERR_CAPACITY, s);
-        crr_activity_row* r = C.act(j);
-        r->schedule_id = id;
-        r->version = ver;
-        r->scheduled_batch_id = batch_first_id;
-        r->scheduled_time = col_ts[ix];
-        r->started_id = CRR_EMPTY_EVENT_ID;
-        r->started_time = CRR_ZERO_TIME;
-        r->cancel_request_id = CRR_EMPTY_EVENT_ID;
-        r->last_hb_timeout_vis_s = 0;
-        r->sched_src = s;
-        r->started_src = -1;
-        r->schedule_to_start = as.schedule_to_start;
-        r->schedule_to_close = as.schedule_to_close;
-        r->start_to_close = as.start_to_close;
-        r->heartbeat = as.heartbeat;
-        r->timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
-        r->key = key;
-        r->flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
-        ++L.n_act;
+        crr_activity_row row;
+        row.schedule_id = id;
+        row.version = ver;
+        row.scheduled_batch_id = batch_first_id;
+        row.scheduled_time = ev.ts;
+        row.started_id = CRR_EMPTY_EVENT_ID;
+        row.started_time = CRR_ZERO_TIME;
+        row.cancel_request_id = CRR_EMPTY_EVENT_ID;
+        row.last_hb_timeout_vis_s = 0;
+        row.sched_src = s;
+        row.started_src = -1;
+        row.schedule_to_start = as.schedule_to_start;
+        row.schedule_to_close = as.schedule_to_close;
+        row.start_to_close = as.start_to_close;
+        row.heartbeat = as.heartbeat;
+        row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+        row.key = ev.key;
+        row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
+        row.reserved[0] = row.reserved[1] = row.reserved[2] = 0;
+        CHECK(T.act_insert(L, G, row));
         break;
       }
-      case CRR_EV_ACTIVITY_TASK_STARTED: {  // :297-302 -> :2254-2276
-        i32 j = find_act_by_id(C, L, col_ref[ix]);
-        if (j < 0) FAIL(CRR_ERR_MISSING_ACTIVITY_INFO, s);
-        crr_activity_row* r = C.act(j);
-        r->version = ver;
-        r->started_id = id;
-        r->started_src = s;
-        r->started_time = col_ts[ix];
+      case CRR_EV_ACTIVITY_TASK_STARTED:  // :297-302 -> :2254-2276
+        if (!T.act_start(L, G, ev.ref, id, ver, s, ev.ts)) FAIL(CRR_ERR_MISSING_ACTIVITY_INFO, s);
         break;
-      }
       case CRR_EV_ACTIVITY_TASK_COMPLETED:
       case CRR_EV_ACTIVITY_TASK_FAILED:
       case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
-      case CRR_EV_ACTIVITY_TASK_CANCELED:  // :304-337 -> DeleteActivity
-        delete_activity(C, L, col_ref[ix]);
+      case CRR_EV_ACTIVITY_TASK_CANCELED:  // :304-337 -> DeleteActivity (:1310-1339)
+        T.act_delete(L, G, ev.ref);
         break;
-      case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED: {  // :325-330 -> :2444-2467
-        i32 j = find_act_mapped(C, L, col_key[ix]);
-        if (j >= 0) {
-          crr_activity_row* r = C.act(j);
-          r->version = ver;
-          r->flags |= CRR_ROW_CANCEL_REQUESTED;
-          r->cancel_request_id = id;
-        }
+      case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED:  // :325-330 -> :2444-2467
+        T.act_cancel(L, G, ev.key, id, ver);
         break;
-      }
       case CRR_EV_TIMER_STARTED: {  // :342-347 -> :3057-3081
-        const u32 key = col_key[ix];
-        i32 j = find_timer(C, L, key);  // pendingTimerInfoIDs[TimerID] = ti replaces a live timer
-        if (j < 0) {
-          j = free_slot<crr_timer_row>(&Ctx::timer, C, L.hw_timer, C.timer_cap);
-          if (j < 0) FAIL(CRR_ERR_CAPACITY, s);
-          ++L.n_timer;
-        }
-        crr_timer_row* r = C.timer(j);
-        r->started_id = id;
-        r->version = ver;
-        r->expiry_time = add_seconds(col_ts[ix], col_ref[ix]);
-        r->task_status = CRR_TIMER_TASK_STATUS_NONE;
-        r->key = key;
-        r->src = s;
-        r->flags = CRR_ROW_LIVE;
+        crr_timer_row row;
+        row.started_id = id;
+        row.version = ver;
+        row.expiry_time = add_seconds(ev.ts, ev.ref);
+        row.task_status = CRR_TIMER_TASK_STATUS_NONE;
+        row.key = ev.key;
+        row.src = s;
+        row.flags = CRR_ROW_LIVE;
+        CHECK(T.timer_start(L, G, row));
         break;
       }
       case CRR_EV_TIMER_FIRED:
-      case CRR_EV_TIMER_CANCELED: {  // :349-361 -> DeleteUserTimer (:1390-1419)
-        i32 j = find_timer(C, L, col_key[ix]);
-        if (j < 0) { ++L.inconsistencies; break; }
-        C.timer(j)->flags = 0;
-        --L.n_timer;
+      case CRR_EV_TIMER_CANCELED:  // :349-361 -> DeleteUserTimer (:1390-1419)
+        T.timer_delete(L, G, ev.key);
         break;
-      }
       case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: {  // :366-381 -> :3417-3453
-        if (col_aux[ix] == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-        i32 j = free_slot<crr_child_row>(&Ctx::child, C, L.hw_child, C.child_cap);
-        if (j < 0) FAIL(CRR_ERR_CAPACITY, s);
-        crr_child_row* r = C.child(j);
-        r->initiated_id = id;
-        r->version = ver;
-        r->initiated_batch_id = batch_first_id;
-        r->started_id = CRR_EMPTY_EVENT_ID;
-        r->src = s;
-        r->started_src = -1;
-        r->flags = CRR_ROW_LIVE;
-        ++L.n_child;
+        if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
+        crr_child_row row;
+        row.initiated_id = id;
+        row.version = ver;
+        row.initiated_batch_id = batch_first_id;
+        row.started_id = CRR_EMPTY_EVENT_ID;
+        row.src = s;
+        row.started_src = -1;
+        row.flags = CRR_ROW_LIVE;
+        row.reserved = 0;
+        CHECK(T.child_insert(L, G, row));
         break;
       }
-      case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED: {  // :390-395 -> :3485-3507
-        i32 j = find_initiated<crr_child_row>(&Ctx::child, C, L.hw_child, col_ref[ix]);
-        if (j < 0) FAIL(CRR_ERR_MISSING_CHILD_INFO, s);
-        crr_child_row* r = C.child(j);
-        r->started_id = id;
-        r->started_src = s;
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:  // :390-395 -> :3485-3507
+        if (!T.child_start(L, G, ev.ref, id, s)) FAIL(CRR_ERR_MISSING_CHILD_INFO, s);
         break;
-      }
       case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
-      case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED: {  // DeletePendingChildExecution (:1160-1178)
-        i32 j = find_initiated<crr_child_row>(&Ctx::child, C, L.hw_child, col_ref[ix]);
-        if (j < 0) { ++L.inconsistencies; break; }
-        C.child(j)->flags = 0;
-        --L.n_child;
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED:  // DeletePendingChildExecution (:1160-1178)
+        T.child_delete(L, G, ev.ref);
         break;
-      }
       case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
       case CRR_EV_SIGNAL_EXTERNAL_INITIATED: {  // :432-447 / :463-478 -> :2760-2779 / :2883-2905
-        const bool is_rc = t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED;
-        i32 j = is_rc ? free_slot<crr_initiated_row>(&Ctx::rc, C, L.hw_rc, C.rc_cap)
-                      : free_slot<crr_initiated_row>(&Ctx::sig, C, L.hw_sig, C.sig_cap);
-        if (j < 0) FAIL(CRR_ERR_CAPACITY, s);
-        crr_initiated_row* r = is_rc ? C.rc(j) : C.sig(j);
-        r->initiated_id = id;
-        r->version = ver;
-        r->initiated_batch_id = batch_first_id;
-        r->src = s;
-        r->flags = CRR_ROW_LIVE;
-        if (is_rc) ++L.n_rc; else ++L.n_sig;
+        crr_initiated_row row;
+        row.initiated_id = id;
+        row.version = ver;
+        row.initiated_batch_id = batch_first_id;
+        row.src = s;
+        row.flags = CRR_ROW_LIVE;
+        CHECK(T.init_insert(L, G, t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED, row));
         // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
-        if (col_aux[ix] == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
+        if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         break;
       }
       case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
-      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED: {  // DeletePendingRequestCancel (:1181-1199)
-        i32 j = find_initiated<crr_initiated_row>(&Ctx::rc, C, L.hw_rc, col_ref[ix]);
-        if (j < 0) { ++L.inconsistencies; break; }
-        C.rc(j)->flags = 0;
-        --L.n_rc;
+      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:  // DeletePendingRequestCancel (:1181-1199)
+        T.init_delete(L, G, true, ev.ref);
         break;
-      }
       case CRR_EV_SIGNAL_EXTERNAL_FAILED:
-      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED: {  // DeletePendingSignal (:1202-1220)
-        i32 j = find_initiated<crr_initiated_row>(&Ctx::sig, C, L.hw_sig, col_ref[ix]);
-        if (j < 0) { ++L.inconsistencies; break; }
-        C.sig(j)->flags = 0;
-        --L.n_sig;
+      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:  // DeletePendingSignal (:1202-1220)
+        T.init_delete(L, G, false, ev.ref);
         break;
-      }
       case CRR_EV_WORKFLOW_EXECUTION_SIGNALED:  // :497-502 -> :3260-3267
         L.signal_count = (i32)((u32)L.signal_count + 1u);
         break;
@@ -761,20 +1147,18 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
                      : t == CRR_EV_WORKFLOW_EXECUTION_TIMED_OUT ? CRR_CLOSE_TIMED_OUT
                      : t == CRR_EV_WORKFLOW_EXECUTION_CANCELED  ? CRR_CLOSE_CANCELED
                                                                 : CRR_CLOSE_TERMINATED;
-        int e = update_state(L, CRR_STATE_COMPLETED, cs);
-        if (e) FAIL(e, s);
+        CHECK(update_state(L, CRR_STATE_COMPLETED, cs));
         L.completion_event_batch_id = batch_first_id;
         break;
       }
       case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: {  // :587-627 -> :3366-3382
-        const i32 nr = col_aux[ix];
+        const i32 nr = ev.aux;
         if (nr >= 0) {
           if ((u32)nr >= in.n_wf) FAIL(CRR_ERR_NEW_RUN_MISSING, s);
-          const int nst = out.exec[nr].status;  // written by the phase-0 launch
+          const int nst = out.exec[nr].status;  // written by the phase-0 launches
           if (nst != CRR_OK) FAIL(nst, s);
         }
-        int e = update_state(L, CRR_STATE_COMPLETED, CRR_CLOSE_CONTINUED_AS_NEW);
-        if (e) FAIL(e, s);
+        CHECK(update_state(L, CRR_STATE_COMPLETED, CRR_CLOSE_CONTINUED_AS_NEW));
         L.completion_event_batch_id = batch_first_id;
         break;
       }
@@ -788,17 +1172,13 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
     }
 
     if (et & CRR_ETYPE_BATCH_LAST) {
-      // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
-      create_next_activity_timer(C, L);
-      create_next_user_timer(C, L);
-      // :642-643
-      L.last_first_event_id = batch_first_id;
+      T.epilogue(L, G);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
+      L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
   }
   if (empty_at == n_ev) FAIL(CRR_ERR_EMPTY_HISTORY, n_ev);
-  // rebuild finalisation (state_rebuilder.go:150-177)
-  if (wfp->final_token_len != 0xFFFFFFFFu) {
+  if (wfp->final_token_len != 0xFFFFFFFFu) {  // rebuild finalisation (state_rebuilder.go:150-177)
     L.token_src = 2;
     if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, n_ev);
     const i64 want_id = wfp->rebuild_last_event_id, want_ver = wfp->rebuild_last_event_version;
@@ -806,19 +1186,19 @@ __global__ void __launch_bounds__(256) replay_kernel(crr_inputs in, crr_outputs 
     if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
   }
 done_events:
+#undef CHECK
 #undef FAIL
 
-  // ---- write back: VH tail item, sorted live rows, checksum, execution row ----
+  if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
+    out.exec[w].status = CRR_INTERNAL_RETRY;
+    return;
+  }
   if (L.vh_n > 0) {
-    crr_vh_item* it = C.vh(L.vh_n - 1);
+    crr_vh_item* it = G.vh(L.vh_n - 1);
     it->event_id = L.vh_last_id;
     it->version = L.vh_last_ver;
   }
-  compact_sort<crr_activity_row>(&Ctx::act, C, L.hw_act, L.n_act, [](const crr_activity_row* r) { return r->schedule_id; });
-  compact_sort<crr_timer_row>(&Ctx::timer, C, L.hw_timer, L.n_timer, [](const crr_timer_row* r) { return r->started_id; });
-  compact_sort<crr_child_row>(&Ctx::child, C, L.hw_child, L.n_child, [](const crr_child_row* r) { return r->initiated_id; });
-  compact_sort<crr_initiated_row>(&Ctx::rc, C, L.hw_rc, L.n_rc, [](const crr_initiated_row* r) { return r->initiated_id; });
-  compact_sort<crr_initiated_row>(&Ctx::sig, C, L.hw_sig, L.n_sig, [](const crr_initiated_row* r) { return r->initiated_id; });
+  T.finalize(L, G);
 
   crr_exec_row R;
   R.status = L.status;
@@ -856,26 +1236,59 @@ done_events:
   R.payload_len = 0;
   R.reserved[0] = 0;
   R.reserved[1] = 0;
-  if (L.status == CRR_OK) R.checksum = payload_crc(R, C, wfp, in.arena, crc_tables, &R.payload_len);
+  if (L.status == CRR_OK) R.checksum = payload_crc(R, T, G, wfp, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
 }
 
+// ---- kernels ---------------------------------------------------------------------------------------
+// Fast path: wave-interleaved layout (stride 64), LDS-indexed tables.
+__global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
+  __shared__ u32 crc_tables[8 * 256];
+  __shared__ LdsArena arena;
+  build_crc_tables(crc_tables);
+  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= in.n_wf) return;
+  const crr_workflow* wfp = in.wf + w;
+  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  const i64 lane = threadIdx.x & 63;
+  Geo G;
+  load_geo(G, wfp, out, 64);
+  uniformize_geo(G, lane);
+  const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
+  LdsTables T;
+  T.init(&arena);
+  replay_body(in, out, w, wfp, G, T, ev_begin, crc_tables);
+}
+
+// General path: any layout; also replays workflows the fast path handed back (CRR_INTERNAL_RETRY).
+__global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only) {
+  __shared__ u32 crc_tables[8 * 256];
+  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
+  bool mine = w < in.n_wf && (((in.wf[w].flags & CRR_WF_FLAG_NEW_RUN) != 0) == (phase == 0));
+  if (retry_only && mine) mine = out.exec[w].status == CRR_INTERNAL_RETRY;
+  if (!__syncthreads_or(mine)) return;  // whole block has nothing to (re)play
+  build_crc_tables(crc_tables);
+  if (!mine) return;
+  const crr_workflow* wfp = in.wf + w;
+  Geo G;
+  load_geo(G, wfp, out, in.stride);
+  GlobalTables T;
+  replay_body(in, out, w, wfp, G, T, wfp->ev_begin, crc_tables);
+}
+
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).
-__global__ void __launch_bounds__(256) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {
+__global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {
   __shared__ u32 crc_tables[8 * 256];
   build_crc_tables(crc_tables);
   const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= in.n_wf) return;
   const crr_workflow* wfp = in.wf + w;
-  Ctx C;
-  C.in = in;
-  C.out = out;
-  C.st = in.stride;
-  C.act_base = wfp->act_base; C.timer_base = wfp->timer_base; C.child_base = wfp->child_base;
-  C.rc_base = wfp->rc_base; C.sig_base = wfp->sig_base; C.vh_base = wfp->vh_base; C.rp_base = wfp->rp_base;
+  Geo G;
+  load_geo(G, wfp, out, in.stride);
   const crr_exec_row R = out.exec[w];
+  GlobalTables ids;
   u32 len = 0;
-  checksums[w] = payload_crc(R, C, wfp, in.arena, crc_tables, &len);
+  checksums[w] = payload_crc(R, ids, G, wfp, in.arena, crc_tables, &len);
 }
 
 }  // namespace crr

@@ -17,7 +17,7 @@ from .flatten import HistoryBatch
 from .result import ReplayResult
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcadence_replay.so")
+LIB_PATH = os.environ.get("CRR_LIB_PATH") or os.path.join(_HERE, "libcadence_replay.so")
 _lib = None
 
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# parity tests on the default library, then kernel-only A/B timing of variant libraries
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd "$R"; mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/status.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for v in ${VARIANTS:-}; do
+  timeout -k 10 300 python tools/prof_kernel.py --lib build/variants/lib_$v.so --reps 7 ${PROF_ARGS:-} >> gpurun_out/ab.jsonl 2>> gpurun_out/ab.err
+  rc=$?; echo "variant $v rc=$rc" >> gpurun_out/status.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+exit 0

@@ -1,0 +1,111 @@
+"""Host-side logic without a GPU: C-ABI library exports, flattening, interleaving, digests."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from cadence_amd import abi, synth, synth_mixed
+from cadence_amd.flatten import flatten, interleave
+from cadence_amd.history import thrift_history_branch_token
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "cadence_amd", "libcadence_replay.so")
+
+
+def _declared_symbols():
+    txt = open(os.path.join(ROOT, "include", "cadence_replay.h")).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(crr_\w+)\s*\(", txt, re.M)))
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built (run __graft_entry__.build())")
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = ctypes.CDLL(LIB)
+    syms = _declared_symbols()
+    assert {"crr_replay", "crr_checksum", "crr_set_device", "crr_abi_version", "crr_sizeof",
+            "crr_crc32_ieee", "crr_last_kernel_ms"} <= set(syms)
+    for s in syms:
+        assert hasattr(lib, s), s
+    lib.crr_abi_version.restype = ctypes.c_int
+    assert lib.crr_abi_version() == abi.ABI_VERSION
+    abi.check_layout(lib)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_library_crc32_matches_zlib():
+    import zlib
+    from cadence_amd.engine import crc32
+    for data in (b"", b"123456789", bytes(range(256)) * 3):
+        assert crc32(data) == zlib.crc32(data)
+    assert crc32(b"123456789") == 0xCBF43926
+
+
+def test_engine_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from cadence_amd.engine import EngineUnavailable, ReplayEngine
+    with pytest.raises(EngineUnavailable):
+        ReplayEngine(0)
+
+
+def test_activity_chain_shape():
+    b = synth.activity_chain(100, 4, 1)
+    assert b.n_wf == 100 and b.n_events == 100 * 29
+    t = b.cols["etype"] & abi.ETYPE_MASK
+    assert (t[:29] == synth.activity_chain_template(4)[0]).all()
+    # batches: first/last flags pair up
+    first = (b.cols["etype"] & abi.BATCH_FIRST) != 0
+    last = (b.cols["etype"] & abi.BATCH_LAST) != 0
+    assert first.sum() == last.sum() == 100 * (3 + 4 * 4)
+    # branch tokens are the reference's thrift layout
+    tok = bytes(b.arena[:96])
+    run = tok[8:44].decode()
+    br = tok[51:87].decode()
+    assert tok == thrift_history_branch_token(run, br)
+
+
+def test_interleave_is_a_permutation():
+    hs = synth_mixed.mixed_histories(300, 5, multi_version=True)
+    b = flatten(hs)
+    ib = interleave(b)
+    assert ib.stride == 64
+    # every canonical event appears exactly once at its interleaved position
+    for w in range(b.n_wf):
+        p = int(np.nonzero(ib.perm == w)[0][0])
+        n = int(b.wf["ev_count"][w])
+        src = int(b.wf["ev_begin"][w]) + np.arange(n)
+        dst = int(ib.wf["ev_begin"][p]) + np.arange(n) * 64
+        for name, _ in abi.EVENT_COLUMNS:
+            if name == "aux":
+                continue
+            assert (b.cols[name][src] == ib.cols[name][dst]).all(), (w, name)
+    # group-uniform bases (the fast kernel reads them as SGPRs): base - lane constant per group
+    for f in ("ev_begin", "act_base", "timer_base", "child_base", "rc_base", "sig_base", "vh_base", "rp_base"):
+        v = ib.wf[f].astype(np.int64) - (np.arange(ib.n_wf) % 64)
+        g = np.arange(ib.n_wf) // 64
+        for gi in np.unique(g):
+            assert len(np.unique(v[g == gi])) == 1, f
+
+
+def test_flatten_capacities_bound_live_sets():
+    from oracle import oracle
+    hs = synth_mixed.mixed_histories(400, 9, multi_version=True, invalid_rate=0.1)
+    b = flatten(hs, known_domains={"domain-a", "domain-b", "parent-domain"})
+    r = oracle.replay(b, 2)
+    for name, _dt, _b, cap_f, n_f in abi.TABLES:
+        assert (r.exec[n_f] <= b.wf[cap_f]).all(), name
+    assert (r.exec["status"] != abi.Status.CAPACITY).all()
+
+
+def test_digest_numpy_matches_torch():
+    import torch
+    from cadence_amd import dist
+    rows = np.zeros(5, abi.EXEC_ROW)
+    rows["status"] = [0, 0, 3, 0, 0]
+    rows["checksum"] = [1, 0xFFFFFFFF, 7, 12345, 0x80000000]
+    rows["next_event_id"] = [30, 24, 5, 30, 2]
+    rows["inconsistencies"] = [0, 1, 0, 2, 0]
+    raw = torch.from_numpy(rows.view(np.uint8).copy())
+    assert (dist.digest_torch(torch, raw, 5).numpy() == dist.digest_numpy(rows)).all()

@@ -1,0 +1,56 @@
+"""Kernel-only driver for rocprofv3 / A-B timing: replays config 2 (1M x 29 events) a few times.
+
+    python tools/prof_kernel.py [--lib path/to/lib.so] [--wf N] [--k 4] [--reps R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--lib", default=None)
+    p.add_argument("--wf", type=int, default=1_000_000)
+    p.add_argument("--k", type=int, default=4)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--mixed", action="store_true", help="config-3-like mixed histories instead of chains")
+    a = p.parse_args()
+    if a.lib:
+        os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
+    import numpy as np
+    import torch
+    from cadence_amd import synth
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.flatten import interleave
+    eng = ReplayEngine(0)
+    if a.mixed:
+        from cadence_amd import synth_mixed
+        from cadence_amd.flatten import flatten
+        b = interleave(flatten(synth_mixed.mixed_histories(a.wf, 5), known_domains={"domain-a", "domain-b", "parent-domain"}))
+    else:
+        b = interleave(synth.activity_chain(a.wf, a.k, synth.SEED_C2, with_keys=False))
+    db = eng.upload(b)
+    eng.launch(db)
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(a.reps):
+        eng.launch(db)
+        torch.cuda.synchronize()
+        ms.append(eng.last_kernel_ms()[1])
+    res = eng.download(db)
+    alg = synth.algorithmic_bytes(b, res)
+    med = float(np.median(ms))
+    print(json.dumps({"lib": a.lib or "default", "workflows": b.n_wf, "events": b.n_events, "kernel_ms": ms,
+                      "median_ms": med, "events_per_s": b.n_events / (med * 1e-3),
+                      "alg_GBs": alg / (med * 1e-3) / 1e9, "alg_bytes": alg,
+                      "ok": int((res.exec["status"] == 0).sum()),
+                      "checksum_xor": int(np.bitwise_xor.reduce(res.exec["checksum"].astype(np.uint64)))}))
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,9 @@
 
 #include "cadence_replay.h"
 
+#ifndef CRR_WATERFALL
+#define CRR_WATERFALL 0
+#endif
 #ifndef CRR_LDS_ACT
 #define CRR_LDS_ACT 3
 #endif
@@ -969,7 +972,16 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     }
     L.last_event_task_id = ev.task;  // :129
 
+#if CRR_WATERFALL
+    // Waterfall dispatch: one pass per distinct event type present in the wavefront; the type is
+    // wave-uniform inside a pass, so the 42-way switch is a scalar jump, not an exec-mask tree.
+    for (;;) {
+    const i32 tu = uniform32(t);
+    if (t != tu) continue;
+    switch (tu) {
+#else
     switch (t) {
+#endif
       case CRR_EV_WORKFLOW_EXECUTION_STARTED: {  // :132-183 -> mutable_state_builder.go:1751-1829
         const crr_start_side ss = in.start_side[ev.aux];
         if (ss.parent_domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
@@ -1170,6 +1182,10 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       default:  // :629-630
         FAIL(CRR_ERR_UNKNOWN_EVENT_TYPE, s);
     }
+#if CRR_WATERFALL
+    break;
+    }
+#endif
 
     if (et & CRR_ETYPE_BATCH_LAST) {
       T.epilogue(L, G);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks

@@ -240,7 +240,10 @@ class CInputs(ctypes.Structure):
 
 
 class COutputs(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES]]
+    _fields_ = [(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES] + [("scratch",)]]
+
+
+SCRATCH_EXTRA_WORDS = 64
 
 
 def check_layout(lib):

@@ -15,6 +15,7 @@ __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checks
 namespace {
 
 constexpr int kBlock = 256;
+constexpr unsigned kRetryGrid = 512;
 
 struct Timing {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -46,6 +47,7 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!e.etype || !e.event_id || !e.version || !e.timestamp || !e.task_id || !e.ref || !e.key || !e.aux) return false;
   if (!in->act_side || !in->start_side || !in->reset_keys || !in->arena) return false;
   if (!out->act || !out->timer || !out->child || !out->rc || !out->sig || !out->vh || !out->rp) return false;
+  if (in->stride == 64 && !out->scratch) return false;
   return true;
 }
 
@@ -84,11 +86,14 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
     if (in->stride == 64) {
-      // fast path (LDS-indexed tables), then the general path for workflows it handed back
-      hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
-      hipError_t err = hipGetLastError();
+      // fast path (LDS-held tables), then the general path for the workflows it handed back
+      hipError_t err = hipMemsetAsync(out->scratch, 0, 64 * sizeof(uint32_t), s);
       if (err != hipSuccess) return (int)err;
-      hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 1);
+      hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+      err = hipGetLastError();
+      if (err != hipSuccess) return (int)err;
+      const unsigned retry_grid = grid < kRetryGrid ? grid : kRetryGrid;
+      hipLaunchKernelGGL(crr::replay_global_kernel, dim3(retry_grid), dim3(kBlock), 0, s, *in, *out, phase, 1);
     } else {
       hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 0);
     }

@@ -29,7 +29,7 @@
 #define CRR_WATERFALL 0
 #endif
 #ifndef CRR_LDS_ACT
-#define CRR_LDS_ACT 3
+#define CRR_LDS_ACT 2
 #endif
 #ifndef CRR_LDS_TIMER
 #define CRR_LDS_TIMER 2
@@ -57,6 +57,7 @@ using u64 = uint64_t;
 constexpr i64 kSecond = 1000000000LL;
 constexpr int kBlock = 256;
 constexpr int CRR_INTERNAL_RETRY = 200;  // LDS slots exhausted: replay again with GlobalTables
+constexpr u32 kScratchHeader = 64;       // scratch[0] = retry count, scratch[64 + i] = retry workflow
 
 __device__ __forceinline__ i64 add_seconds(i64 t, i64 s) { return (i64)((u64)t + (u64)s * (u64)kSecond); }
 __device__ __forceinline__ i64 unix_seconds(i64 ns) {  // time.Time.Unix(): floor
@@ -365,15 +366,15 @@ struct GlobalTables {
     return CRR_OK;
   }
   // ReplicateActivityTaskStartedEvent (:2254-2276)
-  __device__ __forceinline__ bool act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
     i32 j = find_act_by_id(G, sched);
-    if (j < 0) return false;
+    if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
     crr_activity_row* r = G.act(j);
     r->version = ver;
     r->started_id = id;
     r->started_src = s;
     r->started_time = ts;
-    return true;
+    return CRR_OK;
   }
   // DeleteActivity (:1310-1339)
   __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
@@ -390,7 +391,7 @@ struct GlobalTables {
     else ++L.inconsistencies;
   }
   // ReplicateActivityTaskCancelRequestedEvent (:2444-2467)
-  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver) {
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver, i32 /*s*/) {
     i32 j = find_act_mapped(G, key);
     if (j < 0) return;
     crr_activity_row* r = G.act(j);
@@ -424,13 +425,13 @@ struct GlobalTables {
     ++L.n_child;
     return CRR_OK;
   }
-  __device__ __forceinline__ bool child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
     i32 j = find_initiated<crr_child_row>(&Geo::child, G, hw_child, init);
-    if (j < 0) return false;
+    if (j < 0) return CRR_ERR_MISSING_CHILD_INFO;
     crr_child_row* r = G.child(j);
     r->started_id = id;
     r->started_src = s;
-    return true;
+    return CRR_OK;
   }
   __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
     i32 j = find_initiated<crr_child_row>(&Geo::child, G, hw_child, init);
@@ -523,42 +524,54 @@ struct GlobalTables {
 };
 
 // ===================================================================================================
-// LdsTables: LDS index of the live pending entries; HBM rows written, not read, until finalize.
-// LDS arrays are [slot][256 lanes] so lane-parallel accesses hit consecutive banks.
+// LdsTables: the live pending entries are held in LDS ([slot][lane] SoA, bank-conflict free);
+// HBM rows are not touched during replay.  At the end the live entries are sorted and their rows
+// are rebuilt from LDS plus the source events (version / IDs / batch of the event steps recorded
+// in LDS), so a workflow whose maps drain writes no pending rows at all.
 // ===================================================================================================
 constexpr int A_SLOTS = CRR_LDS_ACT, T_SLOTS = CRR_LDS_TIMER, C_SLOTS = CRR_LDS_CHILD, R_SLOTS = CRR_LDS_RC,
               S_SLOTS = CRR_LDS_SIG, P_SLOTS = CRR_LDS_RP;
-// activity LDS flag bits (row bits + STARTED; TimerTaskStatus in bits 8..11)
+// activity LDS flag bits: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + STARTED; TimerTaskStatus << 8
 constexpr u32 LF_STARTED = 32u;
 constexpr int LF_TTS_SHIFT = 8;
+constexpr u32 TF_CREATED = 2u;  // timer LDS flag: TaskStatus == TimerTaskStatusCreated
 
 struct LdsArena {
   i64 a_sid[A_SLOTS][kBlock];
   i64 a_sched_t[A_SLOTS][kBlock];
   i64 a_start_t[A_SLOTS][kBlock];
-  int4 a_to[A_SLOTS][kBlock];   // s2s, s2c, st2c, hb
+  int4 a_to[A_SLOTS][kBlock];    // s2s, s2c, st2c, hb
   u32 a_key[A_SLOTS][kBlock];
   u32 a_fl[A_SLOTS][kBlock];
+  int4 a_src[A_SLOTS][kBlock];   // sched step, started step, cancel-requested step, -
   i64 t_sid[T_SLOTS][kBlock];
   i64 t_exp[T_SLOTS][kBlock];
   u32 t_key[T_SLOTS][kBlock];
   u32 t_fl[T_SLOTS][kBlock];
+  i32 t_src[T_SLOTS][kBlock];
   i64 c_id[C_SLOTS][kBlock];
   u32 c_fl[C_SLOTS][kBlock];
+  int2 c_src[C_SLOTS][kBlock];   // initiated step, started step
   i64 r_id[R_SLOTS][kBlock];
   u32 r_fl[R_SLOTS][kBlock];
+  i32 r_src[R_SLOTS][kBlock];
   i64 s_id[S_SLOTS][kBlock];
   u32 s_fl[S_SLOTS][kBlock];
-  u32 p_key[P_SLOTS][kBlock];
+  i32 s_src[S_SLOTS][kBlock];
+  int4 p_row[P_SLOTS][kBlock];   // crr_reset_point_row
 };
 
 struct LdsTables {
   LdsArena* M;
   int t;  // threadIdx.x
+  const crr_inputs* in;
+  i64 ev_begin;
 
-  __device__ __forceinline__ void init(LdsArena* arena) {
+  __device__ __forceinline__ void init(LdsArena* arena, const crr_inputs* inputs, i64 begin) {
     M = arena;
     t = threadIdx.x;
+    in = inputs;
+    ev_begin = begin;
 #pragma unroll
     for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] = 0;
 #pragma unroll
@@ -569,6 +582,14 @@ struct LdsTables {
     for (int j = 0; j < R_SLOTS; ++j) M->r_fl[j][t] = 0;
 #pragma unroll
     for (int j = 0; j < S_SLOTS; ++j) M->s_fl[j][t] = 0;
+  }
+  // source-event column reads (finalize only)
+  __device__ __forceinline__ i64 ix(i32 step) const { return ev_begin + (i64)step * 64; }
+  __device__ __forceinline__ i64 ev_id(i32 step) const { return in->ev.event_id[ix(step)]; }
+  __device__ __forceinline__ i64 ev_ver(i32 step) const { return in->ev.version[ix(step)]; }
+  __device__ __forceinline__ i64 batch_first_id(i32 step) const {  // firstEvent.ID of the step's batch
+    while (step > 0 && !(in->ev.etype[ix(step)] & CRR_ETYPE_BATCH_FIRST)) --step;
+    return ev_id(step);
   }
 
   __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
@@ -599,25 +620,25 @@ struct LdsTables {
     if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
     M->a_sid[j][t] = row.schedule_id;
     M->a_sched_t[j][t] = row.scheduled_time;
-    M->a_start_t[j][t] = row.started_time;
+    M->a_start_t[j][t] = CRR_ZERO_TIME;
     M->a_to[j][t] = make_int4(row.schedule_to_start, row.schedule_to_close, row.start_to_close, row.heartbeat);
     M->a_key[j][t] = row.key;
     M->a_fl[j][t] = row.flags;
-    *G.act(j) = row;  // HBM row: written now, read only by finalize
+    M->a_src[j][t] = make_int4(row.sched_src, -1, -1, 0);
     ++L.n_act;
     return CRR_OK;
   }
-  __device__ __forceinline__ bool act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
     i32 j = find_act_by_id(sched);
-    if (j < 0) return false;
+    if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
+    const u32 f = M->a_fl[j][t];
+    // a restart after the heartbeat timer was created: LastHeartbeatTimeoutVisibilityInSeconds is no
+    // longer derivable from the latest StartedTime -> let the general path replay this workflow
+    if ((f & LF_STARTED) && (f & (CRR_TTS_CREATED_HEARTBEAT << LF_TTS_SHIFT))) return CRR_INTERNAL_RETRY;
     M->a_start_t[j][t] = ts;
-    M->a_fl[j][t] |= LF_STARTED;
-    crr_activity_row* r = G.act(j);
-    r->version = ver;
-    r->started_id = id;
-    r->started_src = s;
-    r->started_time = ts;
-    return true;
+    M->a_fl[j][t] = f | LF_STARTED;
+    M->a_src[j][t].y = s;
+    return CRR_OK;
   }
   __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
     i32 j = find_act_by_id(sched);
@@ -631,13 +652,11 @@ struct LdsTables {
     if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
     else ++L.inconsistencies;
   }
-  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver) {
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 /*id*/, i64 /*ver*/, i32 s) {
     i32 j = find_act_mapped(key);
     if (j < 0) return;
     M->a_fl[j][t] |= CRR_ROW_CANCEL_REQUESTED;
-    crr_activity_row* r = G.act(j);
-    r->version = ver;
-    r->cancel_request_id = id;
+    M->a_src[j][t].z = s;
   }
 
   __device__ __forceinline__ i32 find_timer(u32 key) const {
@@ -660,8 +679,8 @@ struct LdsTables {
     M->t_sid[j][t] = row.started_id;
     M->t_exp[j][t] = row.expiry_time;
     M->t_key[j][t] = row.key;
-    M->t_fl[j][t] = CRR_ROW_LIVE;  // bit 1 (value 2) below = TaskStatus created
-    *G.timer(j) = row;
+    M->t_fl[j][t] = CRR_ROW_LIVE;
+    M->t_src[j][t] = row.src;
     return CRR_OK;
   }
   __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
@@ -693,17 +712,15 @@ struct LdsTables {
     if (j >= G.child_cap) return CRR_ERR_CAPACITY;
     M->c_id[j][t] = row.initiated_id;
     M->c_fl[j][t] = CRR_ROW_LIVE;
-    *G.child(j) = row;
+    M->c_src[j][t] = make_int2(row.src, -1);
     ++L.n_child;
     return CRR_OK;
   }
-  __device__ __forceinline__ bool child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
     i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
-    if (j < 0) return false;
-    crr_child_row* r = G.child(j);
-    r->started_id = id;
-    r->started_src = s;
-    return true;
+    if (j < 0) return CRR_ERR_MISSING_CHILD_INFO;
+    M->c_src[j][t].y = s;
+    return CRR_OK;
   }
   __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
     i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
@@ -715,8 +732,8 @@ struct LdsTables {
     i32 j = is_rc ? free_init<R_SLOTS>(M->r_fl) : free_init<S_SLOTS>(M->s_fl);
     if (j < 0) return CRR_INTERNAL_RETRY;
     if (j >= (is_rc ? G.rc_cap : G.sig_cap)) return CRR_ERR_CAPACITY;
-    if (is_rc) { M->r_id[j][t] = row.initiated_id; M->r_fl[j][t] = CRR_ROW_LIVE; *G.rc(j) = row; ++L.n_rc; }
-    else { M->s_id[j][t] = row.initiated_id; M->s_fl[j][t] = CRR_ROW_LIVE; *G.sig(j) = row; ++L.n_sig; }
+    if (is_rc) { M->r_id[j][t] = row.initiated_id; M->r_fl[j][t] = CRR_ROW_LIVE; M->r_src[j][t] = row.src; ++L.n_rc; }
+    else { M->s_id[j][t] = row.initiated_id; M->s_fl[j][t] = CRR_ROW_LIVE; M->s_src[j][t] = row.src; ++L.n_sig; }
     return CRR_OK;
   }
   __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
@@ -729,15 +746,15 @@ struct LdsTables {
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
     if (L.n_rp >= P_SLOTS) return CRR_INTERNAL_RETRY;
     if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
-    M->p_key[L.n_rp][t] = row.key;
-    *G.rp(L.n_rp++) = row;
+    M->p_row[L.n_rp][t] = make_int4(row.src, row.prev_index, (i32)row.key, (i32)row.flags);
+    ++L.n_rp;
     return CRR_OK;
   }
   __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
     bool hit = false;
 #pragma unroll
     for (int i = 0; i < P_SLOTS; ++i)
-      if (i < L.n_rp && M->p_key[i][t] == key) hit = true;
+      if (i < L.n_rp && (u32)M->p_row[i][t].z == key) hit = true;
     return hit;
   }
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
@@ -751,10 +768,7 @@ struct LdsTables {
         activity_candidates(B, j, M->a_sid[j][t], M->a_sched_t[j][t], (f & LF_STARTED) != 0, M->a_start_t[j][t],
                             to.x, to.y, to.z, to.w, f >> LF_TTS_SHIFT);
       }
-      if (B.have && !B.created) {
-        M->a_fl[B.j][t] |= timer_mask(B.y) << LF_TTS_SHIFT;
-        if (B.y == CRR_TIMEOUT_HEARTBEAT) G.act(B.j)->last_hb_timeout_vis_s = unix_seconds(B.t);
-      }
+      if (B.have && !B.created) M->a_fl[B.j][t] |= timer_mask(B.y) << LF_TTS_SHIFT;
     }
     if (L.n_timer > 0) {
       BestTimer B;
@@ -762,46 +776,14 @@ struct LdsTables {
       for (int j = 0; j < T_SLOTS; ++j) {
         const u32 f = M->t_fl[j][t];
         if (!(f & CRR_ROW_LIVE)) continue;
-        B.offer(M->t_exp[j][t], M->t_sid[j][t], 0, j, (f & 2u) != 0);
+        B.offer(M->t_exp[j][t], M->t_sid[j][t], 0, j, (f & TF_CREATED) != 0);
       }
-      if (B.have && !B.created) M->t_fl[B.j][t] |= 2u;
+      if (B.have && !B.created) M->t_fl[B.j][t] |= TF_CREATED;
     }
   }
-  // Write the LDS-held row fields, then sort live entries by event ID into slots 0..n-1 (LDS and HBM).
-  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
-#pragma unroll
-    for (int j = 0; j < A_SLOTS; ++j) {
-      const u32 f = M->a_fl[j][t];
-      if (!(f & CRR_ROW_LIVE)) continue;
-      crr_activity_row* r = G.act(j);
-      r->timer_task_status = (i32)((f >> LF_TTS_SHIFT) & 0xF);
-      r->flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
-    }
-#pragma unroll
-    for (int j = 0; j < T_SLOTS; ++j) {
-      const u32 f = M->t_fl[j][t];
-      if (!(f & CRR_ROW_LIVE)) continue;
-      G.timer(j)->task_status = (f & 2u) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
-    }
-    sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
-      swap_rows<crr_activity_row, sizeof(crr_activity_row) / 8>(G.act(i), G.act(b));
-    });
-    sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
-      swap_rows<crr_timer_row, sizeof(crr_timer_row) / 8>(G.timer(i), G.timer(b));
-    });
-    sort_slots<C_SLOTS>(M->c_id, M->c_fl, L.n_child, [&](int i, int b) {
-      swap_rows<crr_child_row, sizeof(crr_child_row) / 8>(G.child(i), G.child(b));
-    });
-    sort_slots<R_SLOTS>(M->r_id, M->r_fl, L.n_rc, [&](int i, int b) {
-      swap_rows<crr_initiated_row, sizeof(crr_initiated_row) / 8>(G.rc(i), G.rc(b));
-    });
-    sort_slots<S_SLOTS>(M->s_id, M->s_fl, L.n_sig, [&](int i, int b) {
-      swap_rows<crr_initiated_row, sizeof(crr_initiated_row) / 8>(G.sig(i), G.sig(b));
-    });
-  }
-  // selection sort of the live LDS slots by id; swaps the id/flag words in LDS and the HBM rows
-  template <int N, class SwapRows>
-  __device__ __forceinline__ void sort_slots(i64 (*ids)[kBlock], u32 (*fl)[kBlock], i32 n, SwapRows swap_rows_fn) {
+
+  template <int N, class SwapFn>
+  __device__ __forceinline__ void sort_slots(i64 (*ids)[kBlock], u32 (*fl)[kBlock], i32 n, SwapFn swap_fn) {
     for (i32 i = 0; i < n; ++i) {
       i32 best = -1;
       i64 bid = 0;
@@ -812,10 +794,105 @@ struct LdsTables {
         if (best < 0 || id < bid) { best = j; bid = id; }
       }
       if (best != i) {
-        swap_rows_fn(i, best);
+        swap_fn(i, best);
         i64 x = ids[i][t]; ids[i][t] = ids[best][t]; ids[best][t] = x;
         u32 y = fl[i][t]; fl[i][t] = fl[best][t]; fl[best][t] = y;
       }
+    }
+  }
+  template <class V>
+  __device__ __forceinline__ static void swp(V& a, V& b) { V x = a; a = b; b = x; }
+
+  // Sort the live entries by event ID (LDS) and write their rows to HBM slots 0..n-1.
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+    sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
+      swp(M->a_sched_t[i][t], M->a_sched_t[b][t]); swp(M->a_start_t[i][t], M->a_start_t[b][t]);
+      swp(M->a_to[i][t], M->a_to[b][t]); swp(M->a_key[i][t], M->a_key[b][t]); swp(M->a_src[i][t], M->a_src[b][t]);
+    });
+    sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
+      swp(M->t_exp[i][t], M->t_exp[b][t]); swp(M->t_key[i][t], M->t_key[b][t]); swp(M->t_src[i][t], M->t_src[b][t]);
+    });
+    sort_slots<C_SLOTS>(M->c_id, M->c_fl, L.n_child, [&](int i, int b) { swp(M->c_src[i][t], M->c_src[b][t]); });
+    sort_slots<R_SLOTS>(M->r_id, M->r_fl, L.n_rc, [&](int i, int b) { swp(M->r_src[i][t], M->r_src[b][t]); });
+    sort_slots<S_SLOTS>(M->s_id, M->s_fl, L.n_sig, [&](int i, int b) { swp(M->s_src[i][t], M->s_src[b][t]); });
+
+    for (i32 i = 0; i < L.n_act; ++i) {  // ReplicateActivityTask{Scheduled,Started,CancelRequested} images
+      const u32 f = M->a_fl[i][t];
+      const int4 src = M->a_src[i][t];
+      const int4 to = M->a_to[i][t];
+      const u32 tts = (f >> LF_TTS_SHIFT) & 0xF;
+      const bool started = (f & LF_STARTED) != 0;
+      crr_activity_row r;
+      r.schedule_id = M->a_sid[i][t];
+      r.version = ev_ver(max(src.x, max(src.y, src.z)));   // last of Scheduled / Started / CancelRequested
+      r.scheduled_batch_id = batch_first_id(src.x);
+      r.scheduled_time = M->a_sched_t[i][t];
+      r.started_id = started ? ev_id(src.y) : CRR_EMPTY_EVENT_ID;
+      r.started_time = M->a_start_t[i][t];
+      r.cancel_request_id = (f & CRR_ROW_CANCEL_REQUESTED) ? ev_id(src.z) : CRR_EMPTY_EVENT_ID;
+      r.last_hb_timeout_vis_s = (tts & CRR_TTS_CREATED_HEARTBEAT) ? unix_seconds(add_seconds(r.started_time, to.w)) : 0;
+      r.sched_src = src.x;
+      r.started_src = started ? src.y : -1;
+      r.schedule_to_start = to.x; r.schedule_to_close = to.y; r.start_to_close = to.z; r.heartbeat = to.w;
+      r.timer_task_status = (i32)tts;
+      r.key = M->a_key[i][t];
+      r.flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
+      r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+      *G.act(i) = r;
+    }
+    for (i32 i = 0; i < L.n_timer; ++i) {  // ReplicateTimerStartedEvent image
+      const i32 src = M->t_src[i][t];
+      crr_timer_row r;
+      r.started_id = M->t_sid[i][t];
+      r.version = ev_ver(src);
+      r.expiry_time = M->t_exp[i][t];
+      r.task_status = (M->t_fl[i][t] & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+      r.key = M->t_key[i][t];
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.timer(i) = r;
+    }
+    for (i32 i = 0; i < L.n_child; ++i) {  // ReplicateStartChildWorkflowExecutionInitiatedEvent (+ Started)
+      const int2 src = M->c_src[i][t];
+      crr_child_row r;
+      r.initiated_id = M->c_id[i][t];
+      r.version = ev_ver(src.x);
+      r.initiated_batch_id = batch_first_id(src.x);
+      r.started_id = src.y >= 0 ? ev_id(src.y) : CRR_EMPTY_EVENT_ID;
+      r.src = src.x;
+      r.started_src = src.y;
+      r.flags = CRR_ROW_LIVE;
+      r.reserved = 0;
+      *G.child(i) = r;
+    }
+    for (i32 i = 0; i < L.n_rc; ++i) {
+      const i32 src = M->r_src[i][t];
+      crr_initiated_row r;
+      r.initiated_id = M->r_id[i][t];
+      r.version = ev_ver(src);
+      r.initiated_batch_id = batch_first_id(src);
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.rc(i) = r;
+    }
+    for (i32 i = 0; i < L.n_sig; ++i) {
+      const i32 src = M->s_src[i][t];
+      crr_initiated_row r;
+      r.initiated_id = M->s_id[i][t];
+      r.version = ev_ver(src);
+      r.initiated_batch_id = batch_first_id(src);
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.sig(i) = r;
+    }
+    for (i32 i = 0; i < L.n_rp; ++i) {
+      const int4 p = M->p_row[i][t];
+      crr_reset_point_row r;
+      r.src = p.x;
+      r.prev_index = p.y;
+      r.key = (u32)p.z;
+      r.flags = (u32)p.w;
+      *G.rp(i) = r;
     }
   }
   __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return M->t_sid[i][t]; }
@@ -1070,7 +1147,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         break;
       }
       case CRR_EV_ACTIVITY_TASK_STARTED:  // :297-302 -> :2254-2276
-        if (!T.act_start(L, G, ev.ref, id, ver, s, ev.ts)) FAIL(CRR_ERR_MISSING_ACTIVITY_INFO, s);
+        CHECK(T.act_start(L, G, ev.ref, id, ver, s, ev.ts));
         break;
       case CRR_EV_ACTIVITY_TASK_COMPLETED:
       case CRR_EV_ACTIVITY_TASK_FAILED:
@@ -1079,7 +1156,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         T.act_delete(L, G, ev.ref);
         break;
       case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED:  // :325-330 -> :2444-2467
-        T.act_cancel(L, G, ev.key, id, ver);
+        T.act_cancel(L, G, ev.key, id, ver, s);
         break;
       case CRR_EV_TIMER_STARTED: {  // :342-347 -> :3057-3081
         crr_timer_row row;
@@ -1112,7 +1189,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         break;
       }
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:  // :390-395 -> :3485-3507
-        if (!T.child_start(L, G, ev.ref, id, s)) FAIL(CRR_ERR_MISSING_CHILD_INFO, s);
+        CHECK(T.child_start(L, G, ev.ref, id, s));
         break;
       case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
@@ -1207,6 +1284,8 @@ done_events:
 
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
     out.exec[w].status = CRR_INTERNAL_RETRY;
+    const u32 k = atomicAdd(out.scratch, 1u);
+    out.scratch[kScratchHeader + k] = w;
     return;
   }
   if (L.vh_n > 0) {
@@ -1257,7 +1336,7 @@ done_events:
 }
 
 // ---- kernels ---------------------------------------------------------------------------------------
-// Fast path: wave-interleaved layout (stride 64), LDS-indexed tables.
+// Fast path: wave-interleaved layout (stride 64), LDS-held tables.
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
   __shared__ u32 crc_tables[8 * 256];
   __shared__ LdsArena arena;
@@ -1272,24 +1351,32 @@ __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_o
   uniformize_geo(G, lane);
   const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
   LdsTables T;
-  T.init(&arena);
+  T.init(&arena, &in, ev_begin);
   replay_body(in, out, w, wfp, G, T, ev_begin, crc_tables);
 }
 
-// General path: any layout; also replays workflows the fast path handed back (CRR_INTERNAL_RETRY).
+// General path over HBM slot tables (any layout).  retry_only: replay the workflows the fast path
+// handed back (scratch list), grid-striding so the launch is cheap when there are none.
 __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only) {
   __shared__ u32 crc_tables[8 * 256];
-  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
-  bool mine = w < in.n_wf && (((in.wf[w].flags & CRR_WF_FLAG_NEW_RUN) != 0) == (phase == 0));
-  if (retry_only && mine) mine = out.exec[w].status == CRR_INTERNAL_RETRY;
-  if (!__syncthreads_or(mine)) return;  // whole block has nothing to (re)play
+  u32 n_items = in.n_wf;
+  if (retry_only) {
+    n_items = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n_items == 0) return;  // uniform across the grid
+  } else if (blockIdx.x * blockDim.x >= n_items) {
+    return;
+  }
   build_crc_tables(crc_tables);
-  if (!mine) return;
-  const crr_workflow* wfp = in.wf + w;
-  Geo G;
-  load_geo(G, wfp, out, in.stride);
-  GlobalTables T;
-  replay_body(in, out, w, wfp, G, T, wfp->ev_begin, crc_tables);
+  const u32 stride = gridDim.x * blockDim.x;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
+    const u32 w = retry_only ? out.scratch[kScratchHeader + i] : i;
+    const crr_workflow* wfp = in.wf + w;
+    if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) continue;
+    Geo G;
+    load_geo(G, wfp, out, in.stride);
+    GlobalTables T;
+    replay_body(in, out, w, wfp, G, T, wfp->ev_begin, crc_tables);
+  }
 }
 
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).

@@ -121,6 +121,8 @@ class ReplayEngine:
             rows = max(batch.table_rows.get(name, 0), 1)
             T["out_" + name] = torch.zeros(rows * dt.itemsize, dtype=torch.uint8, device=dev)
             setattr(co, name, T["out_" + name].data_ptr())
+        T["scratch"] = torch.zeros(batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)
+        co.scratch = T["scratch"].data_ptr()
         return DeviceBatch(batch, T, ci, co, self.device)
 
     # -- launch ------------------------------------------------------------------------------------

@@ -346,6 +346,7 @@ typedef struct crr_outputs {
     crr_initiated_row*   sig;
     crr_vh_item*         vh;
     crr_reset_point_row* rp;
+    uint32_t*            scratch;   /* engine scratch: >= n_wf + 64 words, contents undefined */
 } crr_outputs;
 
 /* ---- entry points ----------------------------------------------------------------------------- */

@@ -84,6 +84,7 @@ def _outputs(res: ReplayResult):
     co.exec = res.exec.ctypes.data if res.exec.size else np.zeros(1, abi.EXEC_ROW).ctypes.data
     for name, *_ in abi.TABLES:
         setattr(co, name, res.tables[name].ctypes.data)
+    co.scratch = None
     return co
 
 

@@ -147,6 +147,7 @@ ROW_RESETTABLE = 16
 
 WF_FLAG_NEW_RUN = 1
 IN_HAS_NEW_RUN = 1
+IN_LDS_SMALL = 2
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([

@@ -8,6 +8,7 @@
 
 namespace crr {
 __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
 }
@@ -89,7 +90,10 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       // fast path (LDS-held tables), then the general path for the workflows it handed back
       hipError_t err = hipMemsetAsync(out->scratch, 0, 64 * sizeof(uint32_t), s);
       if (err != hipSuccess) return (int)err;
-      hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+      if (in->flags & CRR_IN_LDS_SMALL)
+        hipLaunchKernelGGL(crr::replay_lds_small_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+      else
+        hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
       err = hipGetLastError();
       if (err != hipSuccess) return (int)err;
       const unsigned retry_grid = grid < kRetryGrid ? grid : kRetryGrid;

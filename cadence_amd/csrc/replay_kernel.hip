@@ -529,14 +529,25 @@ struct GlobalTables {
 // are rebuilt from LDS plus the source events (version / IDs / batch of the event steps recorded
 // in LDS), so a workflow whose maps drain writes no pending rows at all.
 // ===================================================================================================
-constexpr int A_SLOTS = CRR_LDS_ACT, T_SLOTS = CRR_LDS_TIMER, C_SLOTS = CRR_LDS_CHILD, R_SLOTS = CRR_LDS_RC,
-              S_SLOTS = CRR_LDS_SIG, P_SLOTS = CRR_LDS_RP;
+// LDS slot tiers: workflows whose live sets fit the small tier run at 3 blocks/CU (48 KB LDS/block),
+// the large tier at 2 blocks/CU (76.8 KB); anything larger falls back to GlobalTables.
+template <int A, int T, int C, int R, int S, int P>
+struct Tier {
+  static constexpr int A_SLOTS = A, T_SLOTS = T, C_SLOTS = C, R_SLOTS = R, S_SLOTS = S, P_SLOTS = P;
+};
+using SmallTier = Tier<1, 1, 1, 1, 1, 1>;
+using LargeTier = Tier<CRR_LDS_ACT, CRR_LDS_TIMER, CRR_LDS_CHILD, CRR_LDS_RC, CRR_LDS_SIG, CRR_LDS_RP>;
+#define CRR_TIER_SLOTS                                                                      \
+  static constexpr int A_SLOTS = TIER::A_SLOTS, T_SLOTS = TIER::T_SLOTS, C_SLOTS = TIER::C_SLOTS, \
+                       R_SLOTS = TIER::R_SLOTS, S_SLOTS = TIER::S_SLOTS, P_SLOTS = TIER::P_SLOTS;
 // activity LDS flag bits: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + STARTED; TimerTaskStatus << 8
 constexpr u32 LF_STARTED = 32u;
 constexpr int LF_TTS_SHIFT = 8;
 constexpr u32 TF_CREATED = 2u;  // timer LDS flag: TaskStatus == TimerTaskStatusCreated
 
+template <class TIER>
 struct LdsArena {
+  CRR_TIER_SLOTS
   i64 a_sid[A_SLOTS][kBlock];
   i64 a_sched_t[A_SLOTS][kBlock];
   i64 a_start_t[A_SLOTS][kBlock];
@@ -561,13 +572,16 @@ struct LdsArena {
   int4 p_row[P_SLOTS][kBlock];   // crr_reset_point_row
 };
 
+template <class TIER>
 struct LdsTables {
-  LdsArena* M;
+  CRR_TIER_SLOTS
+  using Arena = LdsArena<TIER>;
+  Arena* M;
   int t;  // threadIdx.x
   const crr_inputs* in;
   i64 ev_begin;
 
-  __device__ __forceinline__ void init(LdsArena* arena, const crr_inputs* inputs, i64 begin) {
+  __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin) {
     M = arena;
     t = threadIdx.x;
     in = inputs;
@@ -1337,9 +1351,10 @@ done_events:
 
 // ---- kernels ---------------------------------------------------------------------------------------
 // Fast path: wave-interleaved layout (stride 64), LDS-held tables.
-__global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
+template <class TIER>
+__device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase) {
   __shared__ u32 crc_tables[8 * 256];
-  __shared__ LdsArena arena;
+  __shared__ LdsArena<TIER> arena;
   build_crc_tables(crc_tables);
   const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= in.n_wf) return;
@@ -1350,9 +1365,15 @@ __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_o
   load_geo(G, wfp, out, 64);
   uniformize_geo(G, lane);
   const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
-  LdsTables T;
+  LdsTables<TIER> T;
   T.init(&arena, &in, ev_begin);
   replay_body(in, out, w, wfp, G, T, ev_begin, crc_tables);
+}
+__global__ void __launch_bounds__(kBlock, 3) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
+  replay_lds<SmallTier>(in, out, phase);
+}
+__global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
+  replay_lds<LargeTier>(in, out, phase);
 }
 
 // General path over HBM slot tables (any layout).  retry_only: replay the workflows the fast path

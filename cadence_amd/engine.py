@@ -13,7 +13,7 @@ from typing import Dict, Optional
 import numpy as np
 
 from . import abi
-from .flatten import HistoryBatch
+from .flatten import HistoryBatch, fits_small_tier
 from .result import ReplayResult
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -113,7 +113,9 @@ class ReplayEngine:
         ci.n_wf = batch.n_wf
         ci.stride = batch.stride
         has_new_run = bool((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()) if batch.n_wf else False
-        ci.flags = abi.IN_HAS_NEW_RUN if has_new_run else 0
+        ci.flags = (abi.IN_HAS_NEW_RUN if has_new_run else 0)
+        if batch.stride == 64 and fits_small_tier(batch):
+            ci.flags |= abi.IN_LDS_SMALL
         co = abi.COutputs()
         T["exec"] = torch.zeros(max(batch.n_wf, 1) * abi.EXEC_ROW.itemsize, dtype=torch.uint8, device=dev)
         co.exec = T["exec"].data_ptr()

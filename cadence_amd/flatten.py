@@ -352,3 +352,74 @@ def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, 
         idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * batch.stride
         out[name] = tables[name][idx]
     return out
+
+
+SMALL_TIER = {"act": 1, "timer": 1, "child": 1, "rc": 1, "sig": 1, "rp": 1}
+
+
+def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
+    """Approximate peak live-set size per workflow and map (running inserts - deletes; reset points:
+    distinct non-empty binary checksums + previous points).  Used only to pick the LDS tier: a
+    workflow that outgrows its tier is replayed by the general path, so this affects speed only."""
+    n = batch.n_wf
+    cnt = batch.wf["ev_count"].astype(np.int64)
+    if batch.stride == 1:
+        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + \
+            (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+    else:
+        step = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + step * batch.stride
+    t = (batch.cols["etype"][idx] & abi.ETYPE_MASK).astype(np.int64)
+    wf_of = np.repeat(np.arange(n), cnt)
+    out = {}
+    rules = {
+        "act": ([ET.ActivityTaskScheduled], [ET.ActivityTaskCompleted, ET.ActivityTaskFailed, ET.ActivityTaskTimedOut,
+                                            ET.ActivityTaskCanceled]),
+        "timer": ([ET.TimerStarted], [ET.TimerFired, ET.TimerCanceled]),
+        "child": ([ET.StartChildWorkflowExecutionInitiated],
+                  [ET.StartChildWorkflowExecutionFailed, ET.ChildWorkflowExecutionCompleted,
+                   ET.ChildWorkflowExecutionFailed, ET.ChildWorkflowExecutionCanceled,
+                   ET.ChildWorkflowExecutionTimedOut, ET.ChildWorkflowExecutionTerminated]),
+        "rc": ([ET.RequestCancelExternalWorkflowExecutionInitiated],
+               [ET.RequestCancelExternalWorkflowExecutionFailed, ET.ExternalWorkflowExecutionCancelRequested]),
+        "sig": ([ET.SignalExternalWorkflowExecutionInitiated],
+                [ET.SignalExternalWorkflowExecutionFailed, ET.ExternalWorkflowExecutionSignaled]),
+    }
+    starts = np.cumsum(cnt) - cnt
+    nz = cnt > 0
+    for name, (ins, dels) in rules.items():
+        lut = np.zeros(64, np.int8)
+        lut[[int(x) for x in ins]] = 1
+        lut[[int(x) for x in dels]] = -1
+        d = lut[t]
+        if d.size == 0 or not d.any():
+            out[name] = np.zeros(n, np.int64)
+            continue
+        cs = np.cumsum(d, dtype=np.int64)
+        base = np.where(starts > 0, cs[np.maximum(starts - 1, 0)], 0)
+        rel = cs - np.repeat(base, cnt)
+        mx = np.zeros(n, np.int64)
+        mx[nz] = np.maximum.reduceat(rel, starts[nz])
+        out[name] = np.maximum(mx, 0)
+    # reset points: non-empty binary checksums that differ from the workflow's previous one (an upper
+    # bound of the distinct count) + points carried over by the start event
+    dtc_pos = np.nonzero((t == ET.DecisionTaskCompleted) & (batch.cols["key"][idx] != 0))[0]
+    rp = np.zeros(n, np.int64)
+    if dtc_pos.size:
+        keys = batch.cols["key"][idx[dtc_pos]]
+        wfs = wf_of[dtc_pos]
+        new_key = np.ones(dtc_pos.size, bool)
+        new_key[1:] = (keys[1:] != keys[:-1]) | (wfs[1:] != wfs[:-1])
+        rp = np.bincount(wfs[new_key], minlength=n).astype(np.int64)
+    prev = np.zeros(n, np.int64)
+    st = t == ET.WorkflowExecutionStarted
+    if st.any():
+        pc = batch.start_side["prev_reset_count"][batch.cols["aux"][idx][st]].astype(np.int64)
+        np.maximum.at(prev, wf_of[st], np.maximum(pc, 0))
+    out["rp"] = rp + prev
+    return out
+
+
+def fits_small_tier(batch: HistoryBatch) -> bool:
+    b = live_set_bounds(batch)
+    return all(bool((b[k] <= v).all()) for k, v in SMALL_TIER.items())

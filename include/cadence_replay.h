@@ -254,6 +254,9 @@ typedef struct crr_inputs {
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
+#define CRR_IN_LDS_SMALL   2u   /* hint: live sets are small (<= 1 pending entry per map): use the
+                                   3-blocks/CU LDS tier; workflows that outgrow it are replayed by
+                                   the general path, so the hint affects speed only */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (192 B). */

@@ -36,6 +36,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads for the CPU baseline (0: os cpu share)")
     p.add_argument("--cpu-sample", type=int, default=1_000_000, help="workflows in the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=2.0,
+                   help="minimum wall seconds of CPU-baseline replay (x threads = CPU seconds; 2 s x 16 = 32)")
     return p.parse_args()
 
 
@@ -156,13 +158,18 @@ def cpu_baseline(args, gpu_res, gpu_batch, k):
     n = min(args.cpu_sample, args.workflows)
     threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
     sample = synth.activity_chain(n, k, synth.SEED_C2, with_keys=True)
-    t0 = time.perf_counter()
-    res = oracle.replay(sample, threads)
-    dt = time.perf_counter() - t0
-    out = {"value": sample.n_events / dt, "unit": "events/s", "cores": threads, "kind": "port",
-           "sample": f"{n} config-2 workflows ({sample.n_events} events), seed SEED_C2, "
+    # repeat whole passes over the sample until >= cpu_seconds of wall time (bounded CPU work)
+    passes, dt, res = 0, 0.0, None
+    while passes == 0 or dt < args.cpu_seconds:
+        t0 = time.perf_counter()
+        r = oracle.replay(sample, threads)
+        dt += time.perf_counter() - t0
+        res = res if res is not None else r
+        passes += 1
+    out = {"value": sample.n_events * passes / dt, "unit": "events/s", "cores": threads, "kind": "port",
+           "sample": f"{passes} pass(es) over {n} config-2 workflows ({sample.n_events} events), seed SEED_C2, "
                      f"{threads} std::thread workers, CPU restatement of Go stateBuilder (reference not runnable)",
-           "wall_s": dt}
+           "wall_s": dt, "cpu_seconds_approx": dt * threads}
     if n == args.workflows:
         d = diff_results(gpu_batch, gpu_res, sample, res)
         out["gpu_parity_bit_exact"] = not d

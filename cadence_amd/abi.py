@@ -148,6 +148,7 @@ ROW_RESETTABLE = 16
 WF_FLAG_NEW_RUN = 1
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
+IN_WAVE_TAIL = 4
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([
@@ -237,7 +238,7 @@ class CInputs(ctypes.Structure):
     _fields_ = [("ev", CEvents), ("act_side", ctypes.c_void_p), ("start_side", ctypes.c_void_p),
                 ("reset_keys", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("wf", ctypes.c_void_p),
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("wave_begin", ctypes.c_uint32)]
 
 
 class COutputs(ctypes.Structure):

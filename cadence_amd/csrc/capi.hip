@@ -7,9 +7,11 @@
 #include "cadence_replay.h"
 
 namespace crr {
-__global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
-__global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
+template <bool WAVE_TAIL> __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
+template <bool WAVE_TAIL> __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
+__global__ void replay_wave_big_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void replay_wave_hbm_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
 }
 
@@ -17,6 +19,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr unsigned kRetryGrid = 512;
+constexpr unsigned kBigGrid = 1024;   // 2 blocks (waves) per CU x 256 CUs, twice over
 
 struct Timing {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -49,6 +52,9 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!in->act_side || !in->start_side || !in->reset_keys || !in->arena) return false;
   if (!out->act || !out->timer || !out->child || !out->rc || !out->sig || !out->vh || !out->rp) return false;
   if (in->stride == 64 && !out->scratch) return false;
+  if (in->flags & CRR_IN_WAVE_TAIL) {
+    if (in->stride != 64 || in->wave_begin > in->n_wf) return false;
+  }
   return true;
 }
 
@@ -82,22 +88,34 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool timed = ensure_events();
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
+  // fast-path grid: one block per 4 long (wave-tail) workflows, then one per 256 lane workflows
+  const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
+  const unsigned lds_grid = (in->n_wf - n_lane + kBlock / 64 - 1) / (kBlock / 64) + (n_lane + kBlock - 1) / kBlock;
   g_timing.valid[0] = g_timing.valid[1] = false;
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
     if (in->stride == 64) {
       // fast path (LDS-held tables), then the general path for the workflows it handed back
-      hipError_t err = hipMemsetAsync(out->scratch, 0, 64 * sizeof(uint32_t), s);
+      hipError_t err = hipMemsetAsync(out->scratch, 0, 2 * sizeof(uint32_t), s);
       if (err != hipSuccess) return (int)err;
-      if (in->flags & CRR_IN_LDS_SMALL)
-        hipLaunchKernelGGL(crr::replay_lds_small_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+      const bool tail = n_lane < in->n_wf;
+      const bool small = (in->flags & CRR_IN_LDS_SMALL) != 0;
+      if (small && tail)
+        hipLaunchKernelGGL(crr::replay_lds_small_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
+      else if (small)
+        hipLaunchKernelGGL(crr::replay_lds_small_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
+      else if (tail)
+        hipLaunchKernelGGL(crr::replay_lds_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
       else
-        hipLaunchKernelGGL(crr::replay_lds_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase);
+        hipLaunchKernelGGL(crr::replay_lds_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
       err = hipGetLastError();
       if (err != hipSuccess) return (int)err;
-      const unsigned retry_grid = grid < kRetryGrid ? grid : kRetryGrid;
-      hipLaunchKernelGGL(crr::replay_global_kernel, dim3(retry_grid), dim3(kBlock), 0, s, *in, *out, phase, 1);
+      // the workflows it handed back: one wavefront each, big LDS arena, then HBM rows
+      const unsigned big_grid = in->n_wf < kBigGrid ? in->n_wf : kBigGrid;
+      hipLaunchKernelGGL(crr::replay_wave_big_kernel, dim3(big_grid), dim3(64), 0, s, *in, *out, phase);
+      const unsigned hbm_grid = (in->n_wf + 3) / 4 < kRetryGrid ? (in->n_wf + 3) / 4 : kRetryGrid;
+      hipLaunchKernelGGL(crr::replay_wave_hbm_kernel, dim3(hbm_grid), dim3(kBlock), 0, s, *in, *out, phase);
     } else {
       hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 0);
     }

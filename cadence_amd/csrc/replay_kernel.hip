@@ -57,7 +57,12 @@ using u64 = uint64_t;
 constexpr i64 kSecond = 1000000000LL;
 constexpr int kBlock = 256;
 constexpr int CRR_INTERNAL_RETRY = 200;  // LDS slots exhausted: replay again with GlobalTables
-constexpr u32 kScratchHeader = 64;       // scratch[0] = retry count, scratch[64 + i] = retry workflow
+constexpr u32 kScratchHeader = 64;       // scratch[0], [1] = retry list counts; lists follow the header
+// Retry lists: list 0 (fast path -> big-arena wavefront pass) at scratch[64 + k], list 1 (big arena ->
+// HBM-row wavefront pass) at scratch[64 + n_wf + k]; scratch holds >= 2 * n_wf + 64 words.
+__device__ __forceinline__ u32 retry_slot(const crr_inputs& in, int list, u32 k) {
+  return kScratchHeader + (list ? in.n_wf : 0u) + k;
+}
 
 __device__ __forceinline__ i64 add_seconds(i64 t, i64 s) { return (i64)((u64)t + (u64)s * (u64)kSecond); }
 __device__ __forceinline__ i64 unix_seconds(i64 ns) {  // time.Time.Unix(): floor
@@ -521,6 +526,7 @@ struct GlobalTables {
   __device__ __forceinline__ i64 sig_id(const Geo& G, i32 i) const { return G.sig(i)->initiated_id; }
   __device__ __forceinline__ i64 rc_id(const Geo& G, i32 i) const { return G.rc(i)->initiated_id; }
   __device__ __forceinline__ i64 child_id(const Geo& G, i32 i) const { return G.child(i)->initiated_id; }
+  __device__ __forceinline__ void retry_push(const crr_inputs&, const crr_outputs&, u32) const {}  // never retries
 };
 
 // ===================================================================================================
@@ -914,6 +920,466 @@ struct LdsTables {
   __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return M->s_id[i][t]; }
   __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return M->r_id[i][t]; }
   __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return M->c_id[i][t]; }
+
+  // Hand a workflow back to the general path: one atomic per wavefront (ballot + mbcnt prefix
+  // count compacts the retrying lanes into the scratch list).
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) const {
+    const u64 m = __builtin_amdgcn_ballot_w64(true);
+    const u32 lane = threadIdx.x & 63;
+    const u32 leader = (u32)__builtin_ctzll(m);
+    const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+    u32 base = 0;
+    if (lane == leader) base = atomicAdd(out.scratch, (u32)__builtin_popcountll(m));
+    base = (u32)__shfl((int)base, (int)leader, 64);
+    out.scratch[retry_slot(in, 0, base + below)] = w;
+  }
+};
+
+// ===================================================================================================
+// WaveTables: one wavefront replays one long history (length bucketing).  The
+// state machine runs wave-uniform (scalar registers); the pending maps are full rows that the 64
+// lanes search in parallel (one ballot per 64 slots), the per-batch timer candidates are built in
+// parallel (shuffle argmin) and the live rows are ordered in parallel at the end.  Row storage:
+//   * LdsRows: a per-wave LDS arena (fast path, fused into the lane kernel's launch); a live set
+//     that outgrows it stops with CRR_INTERNAL_RETRY and is replayed again with
+//   * HbmRows: the workflow's own output rows in HBM (bounded only by the host's capacities).
+// ===================================================================================================
+template <int NA, int NT, int NC, int NR, int NS, int NP>
+struct WaveArena {
+  static constexpr int A = NA, T = NT, C = NC, R = NR, S = NS, P = NP;
+  crr_activity_row act[NA];
+  crr_timer_row timer[NT];
+  crr_child_row child[NC];
+  crr_initiated_row rc[NR];
+  crr_initiated_row sig[NS];
+  crr_reset_point_row rp[NP];
+  i64 ids[NA + NT + NC + NR + NS];  // sorted IDs for the checksum lists (after finalize)
+};
+constexpr int kWavesPerBlock = kBlock / 64;
+
+__device__ __forceinline__ void wave_sync_lds() {  // this wave's LDS writes -> visible to all its lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void wave_sync_global() {  // ... and its global-memory writes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <class ARENA, int LIST>
+struct LdsRows {
+  static constexpr bool kLds = true;
+  static constexpr int kList = LIST;  // scratch list a workflow that outgrows the arena is handed to
+  static constexpr i32 A = ARENA::A, T = ARENA::T, C = ARENA::C, R = ARENA::R, S = ARENA::S, P = ARENA::P;
+  ARENA* M;
+  __device__ __forceinline__ crr_activity_row& act(i32 j) const { return M->act[j]; }
+  __device__ __forceinline__ crr_timer_row& timer(i32 j) const { return M->timer[j]; }
+  __device__ __forceinline__ crr_child_row& child(i32 j) const { return M->child[j]; }
+  __device__ __forceinline__ crr_initiated_row& rc(i32 j) const { return M->rc[j]; }
+  __device__ __forceinline__ crr_initiated_row& sig(i32 j) const { return M->sig[j]; }
+  __device__ __forceinline__ crr_reset_point_row& rp(i32 j) const { return M->rp[j]; }
+};
+struct HbmRows {
+  static constexpr bool kLds = false;
+  static constexpr int kList = -1;    // never outgrown
+  static constexpr i32 A = 0x3fffffff, T = A, C = A, R = A, S = A, P = A;
+  Geo G;
+  __device__ __forceinline__ crr_activity_row& act(i32 j) const { return *G.act(j); }
+  __device__ __forceinline__ crr_timer_row& timer(i32 j) const { return *G.timer(j); }
+  __device__ __forceinline__ crr_child_row& child(i32 j) const { return *G.child(j); }
+  __device__ __forceinline__ crr_initiated_row& rc(i32 j) const { return *G.rc(j); }
+  __device__ __forceinline__ crr_initiated_row& sig(i32 j) const { return *G.sig(j); }
+  __device__ __forceinline__ crr_reset_point_row& rp(i32 j) const { return *G.rp(j); }
+};
+
+template <class ST>
+struct WaveTables {
+  ST S;
+  i32 lane;
+  i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
+
+  __device__ __forceinline__ void init() { lane = (i32)(threadIdx.x & 63); }
+
+  // HbmRows ownership: slot j is only ever written and searched by lane j % 64, so every HBM read
+  // follows that lane's own writes (single work-item ordering, no fences); a uniform read of a
+  // row field takes the owner lane's value.  LDS rows are shared by the whole wave.
+  __device__ __forceinline__ bool own(i32 j) const { return ST::kLds || lane == (j & 63); }
+  __device__ __forceinline__ u32 bcast(i32 j, u32 v) const {
+    if constexpr (ST::kLds) return v;
+    else return __builtin_amdgcn_readlane(v, j & 63);
+  }
+
+  // first slot j < hw with pred(row j) (uniform), -1 if none
+  template <class Row, class F>
+  __device__ __forceinline__ i32 find(Row row, i32 hw, F pred) const {
+    for (i32 b = 0; b < hw; b += 64) {
+      const i32 j = b + lane;
+      const u64 m = __builtin_amdgcn_ballot_w64(j < hw && pred(row(j)));
+      if (m) return b + (i32)__builtin_ctzll(m);
+    }
+    return -1;
+  }
+  // lowest free slot (GlobalTables::free_slot semantics); CAPACITY when `cap` rows are live,
+  // INTERNAL_RETRY when the row storage is full first.  Returns the slot or a negative status.
+  template <class Row>
+  __device__ __forceinline__ i32 take(Row row, i32& hw, i32 store_cap, i32 cap) const {
+    i32 j = find(row, hw, [](const auto& r) { return !(r.flags & CRR_ROW_LIVE); });
+    if (j < 0) j = hw;
+    if (j >= cap) return -CRR_ERR_CAPACITY;
+    if (j >= store_cap) return -CRR_INTERNAL_RETRY;
+    if (j == hw) ++hw;
+    return j;
+  }
+  __device__ __forceinline__ auto A_() const { return [this](i32 j) -> crr_activity_row& { return S.act(j); }; }
+  __device__ __forceinline__ auto T_() const { return [this](i32 j) -> crr_timer_row& { return S.timer(j); }; }
+  __device__ __forceinline__ auto C_() const { return [this](i32 j) -> crr_child_row& { return S.child(j); }; }
+  __device__ __forceinline__ auto R_() const { return [this](i32 j) -> crr_initiated_row& { return S.rc(j); }; }
+  __device__ __forceinline__ auto S_() const { return [this](i32 j) -> crr_initiated_row& { return S.sig(j); }; }
+  __device__ __forceinline__ auto P_() const { return [this](i32 j) -> crr_reset_point_row& { return S.rp(j); }; }
+
+  __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
+    return find(A_(), hw_act, [&](const crr_activity_row& r) { return (r.flags & CRR_ROW_LIVE) && r.schedule_id == sched; });
+  }
+  __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
+    return find(A_(), hw_act, [&](const crr_activity_row& r) {
+      return (r.flags & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && r.key == key;
+    });
+  }
+  __device__ __forceinline__ i32 find_timer(u32 key) const {
+    return find(T_(), hw_timer, [&](const crr_timer_row& r) { return (r.flags & CRR_ROW_LIVE) && r.key == key; });
+  }
+  template <class Row>
+  __device__ __forceinline__ i32 find_initiated(Row row, i32 hw, i64 id) const {
+    return find(row, hw, [&](const auto& r) { return (r.flags & CRR_ROW_LIVE) && r.initiated_id == id; });
+  }
+
+  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
+    const i32 m = find_act_mapped(row.key);
+    const i32 j = take(A_(), hw_act, ST::A, G.act_cap);
+    if (j < 0) return -j;
+    if (m >= 0 && own(m)) S.act(m).flags &= ~CRR_ROW_MAPPED;
+    if (own(j)) S.act(j) = row;
+    ++L.n_act;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
+    if (own(j)) {
+      crr_activity_row& r = S.act(j);
+      r.version = ver;
+      r.started_id = id;
+      r.started_src = s;
+      r.started_time = ts;
+    }
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) { ++L.inconsistencies; return; }
+    const u32 f = bcast(j, S.act(j).flags);
+    const u32 key = bcast(j, S.act(j).key);
+    if (own(j)) S.act(j).flags = f & ~(CRR_ROW_LIVE | CRR_ROW_MAPPED);
+    --L.n_act;
+    if (f & CRR_ROW_MAPPED) return;
+    const i32 m = find_act_mapped(key);
+    if (m >= 0) { if (own(m)) S.act(m).flags &= ~CRR_ROW_MAPPED; }
+    else ++L.inconsistencies;
+  }
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver, i32 /*s*/) {
+    const i32 j = find_act_mapped(key);
+    if (j < 0) return;
+    if (own(j)) {
+      crr_activity_row& r = S.act(j);
+      r.version = ver;
+      r.flags |= CRR_ROW_CANCEL_REQUESTED;
+      r.cancel_request_id = id;
+    }
+  }
+  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
+    i32 j = find_timer(row.key);
+    if (j < 0) {
+      j = take(T_(), hw_timer, ST::T, G.timer_cap);
+      if (j < 0) return -j;
+      ++L.n_timer;
+    }
+    if (own(j)) S.timer(j) = row;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
+    const i32 j = find_timer(key);
+    if (j < 0) { ++L.inconsistencies; return; }
+    if (own(j)) S.timer(j).flags = 0;
+    --L.n_timer;
+  }
+  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
+    const i32 j = take(C_(), hw_child, ST::C, G.child_cap);
+    if (j < 0) return -j;
+    if (own(j)) S.child(j) = row;
+    ++L.n_child;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+    const i32 j = find_initiated(C_(), hw_child, init);
+    if (j < 0) return CRR_ERR_MISSING_CHILD_INFO;
+    if (own(j)) {
+      S.child(j).started_id = id;
+      S.child(j).started_src = s;
+    }
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
+    const i32 j = find_initiated(C_(), hw_child, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    if (own(j)) S.child(j).flags = 0;
+    --L.n_child;
+  }
+  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
+    const i32 j = is_rc ? take(R_(), hw_rc, ST::R, G.rc_cap) : take(S_(), hw_sig, ST::S, G.sig_cap);
+    if (j < 0) return -j;
+    if (own(j)) {
+      if (is_rc) S.rc(j) = row;
+      else S.sig(j) = row;
+    }
+    if (is_rc) ++L.n_rc; else ++L.n_sig;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
+    const i32 j = is_rc ? find_initiated(R_(), hw_rc, init) : find_initiated(S_(), hw_sig, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    if (own(j)) {
+      if (is_rc) S.rc(j).flags = 0;
+      else S.sig(j).flags = 0;
+    }
+    if (is_rc) --L.n_rc; else --L.n_sig;
+  }
+  __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    if (L.n_rp >= ST::P) return CRR_INTERNAL_RETRY;
+    if (own(L.n_rp)) S.rp(L.n_rp) = row;
+    ++L.n_rp;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
+    return find(P_(), L.n_rp, [&](const crr_reset_point_row& r) { return r.key == key; }) >= 0;
+  }
+
+  // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type))
+  __device__ __forceinline__ static void wave_min(BestTimer& B) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      BestTimer o;
+      o.have = __shfl_xor((int)B.have, off, 64) != 0;
+      o.t = __shfl_xor((long long)B.t, off, 64);
+      o.e = __shfl_xor((long long)B.e, off, 64);
+      o.y = __shfl_xor(B.y, off, 64);
+      o.j = __shfl_xor(B.j, off, 64);
+      o.created = __shfl_xor((int)B.created, off, 64) != 0;
+      if (o.have && (!B.have || seq_less(o.t, o.e, o.y, B.t, B.e, B.y))) B = o;
+    }
+    B.have = uniform32(B.have) != 0;
+    B.t = uniform64(B.t);
+    B.e = uniform64(B.e);
+    B.y = uniform32(B.y);
+    B.j = uniform32(B.j);
+    B.created = uniform32(B.created) != 0;
+  }
+  // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+    if (L.n_act > 0) {
+      BestTimer B;
+      for (i32 j = lane; j < hw_act; j += 64) {
+        const crr_activity_row& r = S.act(j);
+        if (!(r.flags & CRR_ROW_LIVE)) continue;
+        activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
+                            r.schedule_to_start, r.schedule_to_close, r.start_to_close, r.heartbeat,
+                            (u32)r.timer_task_status);
+      }
+      wave_min(B);
+      if (B.have && !B.created && own(B.j)) {
+        crr_activity_row& r = S.act(B.j);
+        r.timer_task_status |= timer_mask(B.y);
+        if (B.y == CRR_TIMEOUT_HEARTBEAT) r.last_hb_timeout_vis_s = unix_seconds(B.t);
+      }
+    }
+    if (L.n_timer > 0) {
+      BestTimer B;
+      for (i32 j = lane; j < hw_timer; j += 64) {
+        const crr_timer_row& r = S.timer(j);
+        if (!(r.flags & CRR_ROW_LIVE)) continue;
+        B.offer(r.expiry_time, r.started_id, 0, j, r.task_status == CRR_TIMER_TASK_STATUS_CREATED);
+      }
+      wave_min(B);
+      if (B.have && !B.created && own(B.j)) S.timer(B.j).task_status = CRR_TIMER_TASK_STATUS_CREATED;
+    }
+  }
+
+  // LdsRows: live rows -> HBM slots 0..n-1 in event-ID order (rank = number of smaller live IDs);
+  // the sorted IDs -> ids[] for the checksum lists
+  template <class R, class Row, class IdOf>
+  __device__ __forceinline__ void scatter(Row row, i32 hw, i64* ids, R* (Geo::*dst)(i32) const, const Geo& G,
+                                          IdOf id_of) const {
+    for (i32 j = lane; j < hw; j += 64) {
+      const R& r = row(j);
+      if (!(r.flags & CRR_ROW_LIVE)) continue;
+      const i64 id = id_of(r);
+      i32 rank = 0;
+      for (i32 k = 0; k < hw; ++k) rank += ((row(k).flags & CRR_ROW_LIVE) && id_of(row(k)) < id) ? 1 : 0;
+      *(G.*dst)(rank) = r;
+      ids[rank] = id;
+    }
+  }
+  // HbmRows: in-place selection sort of the live rows into slots 0..n-1 (parallel argmin per slot,
+  // rows swapped one 8-byte word per lane)
+  template <class R, class Row, class IdOf>
+  __device__ __forceinline__ void sort_in_place(Row row, i32 hw, i32 n, IdOf id_of) const {
+    for (i32 i = 0; i < n; ++i) {
+      wave_sync_global();
+      i64 best_id = 0;
+      i32 best = -1;
+      for (i32 j = i + lane; j < hw; j += 64) {
+        const R& r = row(j);
+        if (!(r.flags & CRR_ROW_LIVE)) continue;
+        const i64 id = id_of(r);
+        if (best < 0 || id < best_id) { best = j; best_id = id; }
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const i32 ob = __shfl_xor(best, off, 64);
+        const i64 oid = __shfl_xor((long long)best_id, off, 64);
+        if (ob >= 0 && (best < 0 || oid < best_id)) { best = ob; best_id = oid; }
+      }
+      best = uniform32(best);
+      if (best != i) {
+        u64* pa = reinterpret_cast<u64*>(&row(i));
+        u64* pb = reinterpret_cast<u64*>(&row(best));
+        constexpr int W = (int)(sizeof(R) / 8);
+        if (lane < W) {
+          const u64 x = pa[lane];
+          const u64 y = pb[lane];
+          pa[lane] = y;
+          pb[lane] = x;
+        }
+      }
+    }
+    wave_sync_global();
+  }
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+    if constexpr (ST::kLds) {
+      i64* ids = S.M->ids;
+      constexpr i32 oT = ST::A, oC = oT + ST::T, oR = oC + ST::C, oS = oR + ST::R;
+      scatter<crr_activity_row>(A_(), hw_act, ids, &Geo::act, G, [](const crr_activity_row& r) { return r.schedule_id; });
+      scatter<crr_timer_row>(T_(), hw_timer, ids + oT, &Geo::timer, G, [](const crr_timer_row& r) { return r.started_id; });
+      scatter<crr_child_row>(C_(), hw_child, ids + oC, &Geo::child, G, [](const crr_child_row& r) { return r.initiated_id; });
+      scatter<crr_initiated_row>(R_(), hw_rc, ids + oR, &Geo::rc, G, [](const crr_initiated_row& r) { return r.initiated_id; });
+      scatter<crr_initiated_row>(S_(), hw_sig, ids + oS, &Geo::sig, G, [](const crr_initiated_row& r) { return r.initiated_id; });
+      for (i32 i = lane; i < L.n_rp; i += 64) *G.rp(i) = S.rp(i);
+      wave_sync_lds();
+    } else {
+      sort_in_place<crr_activity_row>(A_(), hw_act, L.n_act, [](const crr_activity_row& r) { return r.schedule_id; });
+      sort_in_place<crr_timer_row>(T_(), hw_timer, L.n_timer, [](const crr_timer_row& r) { return r.started_id; });
+      sort_in_place<crr_child_row>(C_(), hw_child, L.n_child, [](const crr_child_row& r) { return r.initiated_id; });
+      sort_in_place<crr_initiated_row>(R_(), hw_rc, L.n_rc, [](const crr_initiated_row& r) { return r.initiated_id; });
+      sort_in_place<crr_initiated_row>(S_(), hw_sig, L.n_sig, [](const crr_initiated_row& r) { return r.initiated_id; });
+    }
+  }
+  __device__ __forceinline__ i64 act_id(const Geo& G, i32 i) const {
+    if constexpr (ST::kLds) return S.M->ids[i]; else return G.act(i)->schedule_id;
+  }
+  __device__ __forceinline__ i64 timer_id(const Geo& G, i32 i) const {
+    if constexpr (ST::kLds) return S.M->ids[ST::A + i]; else return G.timer(i)->started_id;
+  }
+  __device__ __forceinline__ i64 child_id(const Geo& G, i32 i) const {
+    if constexpr (ST::kLds) return S.M->ids[ST::A + ST::T + i]; else return G.child(i)->initiated_id;
+  }
+  __device__ __forceinline__ i64 rc_id(const Geo& G, i32 i) const {
+    if constexpr (ST::kLds) return S.M->ids[ST::A + ST::T + ST::C + i]; else return G.rc(i)->initiated_id;
+  }
+  __device__ __forceinline__ i64 sig_id(const Geo& G, i32 i) const {
+    if constexpr (ST::kLds) return S.M->ids[ST::A + ST::T + ST::C + ST::R + i]; else return G.sig(i)->initiated_id;
+  }
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) const {
+    if constexpr (ST::kList >= 0) {
+      if (lane == 0) {
+        const u32 k = atomicAdd(out.scratch + ST::kList, 1u);
+        out.scratch[retry_slot(in, ST::kList, k)] = w;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------------
+// Event sources.  LaneSource: one workflow per lane, the 8 column loads of step s+1 are issued before
+// step s is processed.  WaveSource: one workflow per wavefront, 64 consecutive events are loaded per
+// column in one coalesced instruction (one event per lane, the next chunk one chunk ahead) and step s
+// is read out of lane s % 64 into scalar registers.
+struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
+
+struct LaneSource {
+  const crr_events& E;
+  i64 begin, st;
+  i32 n;
+  Ev nx;
+  __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count) : E(e), begin(b), st(stride), n(count) {}
+  __device__ __forceinline__ Ev load(i32 step) const {
+    Ev e;
+    const i64 ix = begin + (i64)step * st;
+    e.et = E.etype[ix]; e.id = E.event_id[ix]; e.ver = E.version[ix]; e.ts = E.timestamp[ix];
+    e.task = E.task_id[ix]; e.ref = E.ref[ix]; e.key = E.key[ix]; e.aux = E.aux[ix];
+    return e;
+  }
+  __device__ __forceinline__ void start() { if (n > 0) nx = load(0); }
+  __device__ __forceinline__ Ev next(i32 s) {
+    const Ev e = nx;
+    if (s + 1 < n) nx = load(s + 1);
+    return e;
+  }
+};
+
+struct WaveSource {
+  const crr_events& E;
+  i64 begin, st;
+  i32 n, lane;
+  Ev cur, nxt;
+  __device__ __forceinline__ WaveSource(const crr_events& e, i64 b, i64 stride, i32 count)
+      : E(e), begin(b), st(stride), n(count) {
+    lane = (i32)(threadIdx.x & 63);
+  }
+  __device__ __forceinline__ Ev load_chunk(i32 c) const {
+    Ev e;
+    const i32 s = c * 64 + lane;
+    const i64 ix = begin + (i64)(s < n ? s : 0) * st;
+    e.et = E.etype[ix]; e.id = E.event_id[ix]; e.ver = E.version[ix]; e.ts = E.timestamp[ix];
+    e.task = E.task_id[ix]; e.ref = E.ref[ix]; e.key = E.key[ix]; e.aux = E.aux[ix];
+    return e;
+  }
+  __device__ __forceinline__ static i64 rl64(i64 v, i32 l) {
+    const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
+    const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
+    return (i64)(((u64)hi << 32) | lo);
+  }
+  __device__ __forceinline__ void start() {
+    if (n > 0) cur = load_chunk(0);
+    if (n > 64) nxt = load_chunk(1);
+  }
+  __device__ __forceinline__ Ev next(i32 s) {
+    const i32 l = s & 63;
+    if (l == 0 && s > 0) {
+      cur = nxt;
+      const i32 c = (s >> 6) + 1;
+      if (c * 64 < n) nxt = load_chunk(c);
+    }
+    Ev e;
+    e.et = __builtin_amdgcn_readlane(cur.et, l);
+    e.id = rl64(cur.id, l); e.ver = rl64(cur.ver, l); e.ts = rl64(cur.ts, l);
+    e.task = rl64(cur.task, l); e.ref = rl64(cur.ref, l);
+    e.key = __builtin_amdgcn_readlane(cur.key, l);
+    e.aux = (i32)__builtin_amdgcn_readlane((u32)cur.aux, l);
+    return e;
+  }
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -977,14 +1443,11 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
 }
 
 // ---------------------------------------------------------------------------------------------------
-struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
-
-template <class P>
+template <class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
-                                            const Geo& G, P& T, i64 ev_begin, const u32* crc_tables) {
+                                            const Geo& G, P& T, SRC& src, const u32* crc_tables) {
   const i32 n_ev = wfp->ev_count;
   const i32 empty_at = wfp->empty_batch_at;
-  const i64 st = in.stride;
   const i64 now_ns = wfp->now_ns;
 
   // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
@@ -1003,33 +1466,14 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   L.inconsistencies = 0;
   L.status = CRR_OK; L.fail_step = -1;
 
-  const uint8_t* __restrict__ col_type = in.ev.etype;
-  const int64_t* __restrict__ col_id = in.ev.event_id;
-  const int64_t* __restrict__ col_ver = in.ev.version;
-  const int64_t* __restrict__ col_ts = in.ev.timestamp;
-  const int64_t* __restrict__ col_task = in.ev.task_id;
-  const int64_t* __restrict__ col_ref = in.ev.ref;
-  const uint32_t* __restrict__ col_key = in.ev.key;
-  const int32_t* __restrict__ col_aux = in.ev.aux;
-
   i64 batch_first_id = 0;
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
 
-  // Software pipeline: the 8 column loads of step s+1 are issued before step s is processed.
-  auto load_ev = [&](i32 step) {
-    Ev e;
-    const i64 ix = ev_begin + (i64)step * st;
-    e.et = col_type[ix]; e.id = col_id[ix]; e.ver = col_ver[ix]; e.ts = col_ts[ix];
-    e.task = col_task[ix]; e.ref = col_ref[ix]; e.key = col_key[ix]; e.aux = col_aux[ix];
-    return e;
-  };
-  Ev nx;
-  if (n_ev > 0) nx = load_ev(0);
+  src.start();
   for (i32 s = 0; s < n_ev; ++s) {
     if (s == empty_at) FAIL(CRR_ERR_EMPTY_HISTORY, s);  // state_builder.go:98-100
-    const Ev ev = nx;
-    if (s + 1 < n_ev) nx = load_ev(s + 1);
+    const Ev ev = src.next(s);
     const u32 et = ev.et;
     const i64 id = ev.id;
     const i64 ver = ev.ver;
@@ -1298,8 +1742,7 @@ done_events:
 
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
     out.exec[w].status = CRR_INTERNAL_RETRY;
-    const u32 k = atomicAdd(out.scratch, 1u);
-    out.scratch[kScratchHeader + k] = w;
+    T.retry_push(in, out, w);
     return;
   }
   if (L.vh_n > 0) {
@@ -1350,14 +1793,53 @@ done_events:
 }
 
 // ---- kernels ---------------------------------------------------------------------------------------
-// Fast path: wave-interleaved layout (stride 64), LDS-held tables.
+// Workflows [0, n_lane) use the batch stride (wave-interleaved: lane per workflow); workflows
+// [wave_begin, n_wf) of a CRR_IN_WAVE_TAIL batch are contiguous (stride 1), one per wavefront.
+__device__ __forceinline__ u32 lane_count(const crr_inputs& in) {
+  return (in.flags & CRR_IN_WAVE_TAIL) ? in.wave_begin : in.n_wf;
+}
+__device__ __forceinline__ i64 wf_stride(const crr_inputs& in, u32 w) {
+  return ((in.flags & CRR_IN_WAVE_TAIL) && w >= in.wave_begin) ? 1 : (i64)in.stride;
+}
+
+// LDS arena of a block: the lane-per-workflow [slot][lane] tables or 4 per-wave row arenas.
+template <class TIER> struct WaveTier;
+template <> struct WaveTier<SmallTier> { using Arena = WaveArena<40, 32, 16, 8, 8, 24>; };
+template <> struct WaveTier<LargeTier> { using Arena = WaveArena<64, 48, 24, 16, 16, 32>; };
 template <class TIER>
+union BlockArena {
+  LdsArena<TIER> lane;
+  typename WaveTier<TIER>::Arena wave[kWavesPerBlock];
+};
+
+// Fast path (stride 64): blocks [0, wave_blocks) replay the long-history tail one workflow per
+// wavefront (dispatched first, they run longest), the remaining blocks replay lane per workflow.
+template <class TIER, bool WAVE_TAIL>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase) {
+  static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
+                "per-wave arenas must fit in the lane arena");
   __shared__ u32 crc_tables[8 * 256];
-  __shared__ LdsArena<TIER> arena;
+  __shared__ BlockArena<TIER> arena;
   build_crc_tables(crc_tables);
-  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= in.n_wf) return;
+  const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
+  const u32 wave_blocks = WAVE_TAIL ? (in.n_wf - n_lane + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+  if (WAVE_TAIL && blockIdx.x < wave_blocks) {
+    const u32 wv = (u32)uniform32((i32)(threadIdx.x >> 6));
+    const u32 w = n_lane + blockIdx.x * kWavesPerBlock + wv;
+    if (w >= in.n_wf) return;
+    const crr_workflow* wfp = in.wf + w;
+    if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+    Geo G;
+    load_geo(G, wfp, out, 1);
+    WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 0>> T;
+    T.S.M = &arena.wave[wv];
+    T.init();
+    WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
+    replay_body(in, out, w, wfp, G, T, S, crc_tables);
+    return;
+  }
+  const u32 w = (blockIdx.x - wave_blocks) * blockDim.x + threadIdx.x;
+  if (w >= n_lane) return;
   const crr_workflow* wfp = in.wf + w;
   if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   const i64 lane = threadIdx.x & 63;
@@ -1366,15 +1848,22 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   uniformize_geo(G, lane);
   const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
   LdsTables<TIER> T;
-  T.init(&arena, &in, ev_begin);
-  replay_body(in, out, w, wfp, G, T, ev_begin, crc_tables);
+  T.init(&arena.lane, &in, ev_begin);
+  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count);
+  replay_body(in, out, w, wfp, G, T, S, crc_tables);
 }
+template <bool WAVE_TAIL>
 __global__ void __launch_bounds__(kBlock, 3) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<SmallTier>(in, out, phase);
+  replay_lds<SmallTier, WAVE_TAIL>(in, out, phase);
 }
+template <bool WAVE_TAIL>
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<LargeTier>(in, out, phase);
+  replay_lds<LargeTier, WAVE_TAIL>(in, out, phase);
 }
+template __global__ void replay_lds_small_kernel<false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<true>(crr_inputs, crr_outputs, int);
 
 // General path over HBM slot tables (any layout).  retry_only: replay the workflows the fast path
 // handed back (scratch list), grid-striding so the launch is cheap when there are none.
@@ -1393,10 +1882,57 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
     const u32 w = retry_only ? out.scratch[kScratchHeader + i] : i;
     const crr_workflow* wfp = in.wf + w;
     if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) continue;
+    const i64 st = wf_stride(in, w);
     Geo G;
-    load_geo(G, wfp, out, in.stride);
+    load_geo(G, wfp, out, st);
     GlobalTables T;
-    replay_body(in, out, w, wfp, G, T, wfp->ev_begin, crc_tables);
+    LaneSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
+    replay_body(in, out, w, wfp, G, T, S, crc_tables);
+  }
+}
+
+// Retry passes, one wavefront per workflow (lane or tail workflows alike; per-workflow stride):
+//   list 0 -> replay_wave_big_kernel: one wave per block with a 57 KB LDS row arena (2 blocks/CU);
+//   list 1 -> replay_wave_hbm_kernel: tables in the workflow's HBM rows (no size limit).
+// Both grid-stride over their list; an empty list costs one load per block.
+using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
+template <class ST>
+__device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
+                                                 WaveTables<ST>& T, const u32* crc_tables) {
+  const crr_workflow* wfp = in.wf + w;
+  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  const i64 st = wf_stride(in, w);
+  Geo G;
+  load_geo(G, wfp, out, st);
+  if constexpr (!ST::kLds) T.S.G = G;
+  T.init();
+  T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
+  WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
+  replay_body(in, out, w, wfp, G, T, S, crc_tables);
+}
+__global__ void __launch_bounds__(64) replay_wave_big_kernel(crr_inputs in, crr_outputs out, int phase) {
+  __shared__ u32 crc_tables[8 * 256];
+  __shared__ BigArena arena;
+  const u32 n_items = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n_items == 0) return;
+  build_crc_tables(crc_tables);
+  for (u32 i = blockIdx.x; i < n_items; i += gridDim.x) {
+    const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 0, i)]);
+    WaveTables<LdsRows<BigArena, 1>> T;
+    T.S.M = &arena;
+    replay_wave_item(in, out, phase, w, T, crc_tables);
+  }
+}
+__global__ void __launch_bounds__(kBlock) replay_wave_hbm_kernel(crr_inputs in, crr_outputs out, int phase) {
+  __shared__ u32 crc_tables[8 * 256];
+  const u32 n_items = __hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n_items == 0) return;
+  build_crc_tables(crc_tables);
+  const u32 wv = (u32)uniform32((i32)(threadIdx.x >> 6));
+  for (u32 i = blockIdx.x * kWavesPerBlock + wv; i < n_items; i += gridDim.x * kWavesPerBlock) {
+    const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
+    WaveTables<HbmRows> T;
+    replay_wave_item(in, out, phase, w, T, crc_tables);
   }
 }
 
@@ -1408,7 +1944,7 @@ __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_out
   if (w >= in.n_wf) return;
   const crr_workflow* wfp = in.wf + w;
   Geo G;
-  load_geo(G, wfp, out, in.stride);
+  load_geo(G, wfp, out, wf_stride(in, w));
   const crr_exec_row R = out.exec[w];
   GlobalTables ids;
   u32 len = 0;

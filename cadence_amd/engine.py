@@ -113,7 +113,8 @@ class ReplayEngine:
         ci.n_wf = batch.n_wf
         ci.stride = batch.stride
         has_new_run = bool((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()) if batch.n_wf else False
-        ci.flags = (abi.IN_HAS_NEW_RUN if has_new_run else 0)
+        ci.flags = (abi.IN_HAS_NEW_RUN if has_new_run else 0) | batch.c_flags()
+        ci.wave_begin = batch.wave_begin or 0
         if batch.stride == 64 and fits_small_tier(batch):
             ci.flags |= abi.IN_LDS_SMALL
         co = abi.COutputs()
@@ -123,7 +124,7 @@ class ReplayEngine:
             rows = max(batch.table_rows.get(name, 0), 1)
             T["out_" + name] = torch.zeros(rows * dt.itemsize, dtype=torch.uint8, device=dev)
             setattr(co, name, T["out_" + name].data_ptr())
-        T["scratch"] = torch.zeros(batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)
+        T["scratch"] = torch.zeros(2 * batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)
         co.scratch = T["scratch"].data_ptr()
         return DeviceBatch(batch, T, ci, co, self.device)
 

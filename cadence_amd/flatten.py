@@ -40,6 +40,19 @@ class HistoryBatch:
     perm: Optional[np.ndarray] = None
     # sizes of the slot tables (rows)
     table_rows: Dict[str, int] = dataclasses.field(default_factory=dict)
+    # length bucketing: workflows [wave_begin, n_wf) are long histories, contiguous (stride 1),
+    # replayed one per wavefront (CRR_IN_WAVE_TAIL); None: every workflow uses `stride`
+    wave_begin: Optional[int] = None
+
+    def wf_strides(self) -> np.ndarray:
+        """Column / row stride of every workflow."""
+        st = np.full(self.n_wf, self.stride, np.int64)
+        if self.wave_begin is not None:
+            st[self.wave_begin:] = 1
+        return st
+
+    def c_flags(self) -> int:
+        return abi.IN_WAVE_TAIL if self.wave_begin is not None else 0
 
     @property
     def n_wf(self) -> int:
@@ -273,38 +286,60 @@ def assign_canonical_tables(batch: HistoryBatch, caps: Dict[str, np.ndarray]):
         batch.table_rows[name] = int(c.sum()) if c.size else 0
 
 
-def interleave(batch: HistoryBatch, wave: int = WAVE) -> HistoryBatch:
-    """Permute a canonical batch into the wave-interleaved device layout.
+LONG_HISTORY = 256   # lane per workflow up to ~256 events, a wavefront per workflow above
+
+
+def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[int] = LONG_HISTORY) -> HistoryBatch:
+    """Permute a canonical batch into the device layout.
 
     Workflows are sorted by event count (descending; ties by index) and packed 64 per group.
     Group g occupies ``group_len[g] * 64`` event slots; lanes shorter than the group's longest
-    workflow see CRR_EV_PAD slots.  CAN ``aux`` references are remapped to device positions.
+    workflow see CRR_EV_PAD slots.  With ``long_threshold`` (length bucketing), workflows longer
+    than it form a tail after the groups: contiguous events and rows (stride 1), one wavefront
+    each on the device (``long_threshold=None``: every workflow lane per workflow).  CAN ``aux``
+    references are remapped to device positions.
     """
     assert batch.stride == 1
     n = batch.n_wf
     counts = batch.wf["ev_count"].astype(np.int64)
-    perm = np.lexsort((np.arange(n), -counts)).astype(np.int64)     # device pos -> canonical wf
+    order = np.lexsort((np.arange(n), -counts)).astype(np.int64)
+    if long_threshold is not None:
+        is_long = counts[order] > long_threshold
+        perm = np.concatenate([order[~is_long], order[is_long]])   # device pos -> canonical wf
+        n_lane = int((~is_long).sum())
+    else:
+        perm = order
+        n_lane = n
     inv = np.empty(n, np.int64)
     inv[perm] = np.arange(n)
-    n_groups = (n + wave - 1) // wave
+    n_groups = (n_lane + wave - 1) // wave
     pos = np.arange(n_groups * wave)
     lane = pos % wave
     group = pos // wave
-    valid = pos < n
     cnt_sorted = np.zeros(n_groups * wave, np.int64)
-    cnt_sorted[:n] = counts[perm]
+    cnt_sorted[:n_lane] = counts[perm[:n_lane]]
     glen = cnt_sorted.reshape(n_groups, wave).max(axis=1)
     gbase = np.zeros(n_groups, np.int64)
     if n_groups:
         gbase[1:] = np.cumsum(glen * wave)[:-1]
-    total_slots = int((glen * wave).sum())
+    lane_slots = int((glen * wave).sum())
+    tail_cnt = counts[perm[n_lane:]]
+    tail_begin = lane_slots + np.concatenate([[0], np.cumsum(tail_cnt)[:-1]]).astype(np.int64)
+    total_slots = lane_slots + int(tail_cnt.sum())
+
+    dev_begin = np.empty(n, np.int64)
+    dev_begin[:n_lane] = gbase[group[:n_lane]] + lane[:n_lane]
+    dev_begin[n_lane:] = tail_begin
+    dev_stride = np.full(n, wave, np.int64)
+    dev_stride[n_lane:] = 1
 
     # event permutation
+    cperm = counts[perm]
     src_begin = batch.wf["ev_begin"][perm].astype(np.int64)
-    wf_pos = np.repeat(np.arange(n), counts[perm])
-    step = np.arange(wf_pos.size) - np.repeat(np.cumsum(counts[perm]) - counts[perm], counts[perm])
+    wf_pos = np.repeat(np.arange(n), cperm)
+    step = np.arange(wf_pos.size) - np.repeat(np.cumsum(cperm) - cperm, cperm)
     src_idx = src_begin[wf_pos] + step
-    dst_idx = gbase[group[wf_pos]] + step * wave + lane[wf_pos]
+    dst_idx = dev_begin[wf_pos] + step * dev_stride[wf_pos]
     cols = {}
     for name, t in abi.EVENT_COLUMNS:
         c = np.zeros(total_slots, dtype=t)
@@ -325,20 +360,24 @@ def interleave(batch: HistoryBatch, wave: int = WAVE) -> HistoryBatch:
         key_len[dst_idx] = batch.key_len[src_idx]
 
     wf = batch.wf[perm].copy()
-    wf["ev_begin"] = gbase[group[:n]] + lane[:n]
+    wf["ev_begin"] = dev_begin
     out = HistoryBatch(cols=cols, act_side=batch.act_side, start_side=batch.start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
-                       key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm)
+                       key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
+                       wave_begin=n_lane if long_threshold is not None else None)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)
-        cap[:n] = wf[cap_f]
+        cap[:n_lane] = wf[cap_f][:n_lane]
         gcap = cap.reshape(n_groups, wave).max(axis=1)
         tbase = np.zeros(n_groups, np.int64)
         if n_groups:
             tbase[1:] = np.cumsum(gcap * wave)[:-1]
-        wf[base_f] = tbase[group[:n]] + lane[:n]
-        wf[cap_f] = gcap[group[:n]]
-        out.table_rows[name] = int((gcap * wave).sum())
+        lane_rows = int((gcap * wave).sum())
+        tcap = np.maximum(wf[cap_f][n_lane:].astype(np.int64), 0)
+        wf[base_f][:n_lane] = tbase[group[:n_lane]] + lane[:n_lane]
+        wf[cap_f][:n_lane] = gcap[group[:n_lane]]
+        wf[base_f][n_lane:] = lane_rows + np.concatenate([[0], np.cumsum(tcap)[:-1]]).astype(np.int64)
+        out.table_rows[name] = lane_rows + int(tcap.sum())
     return out
 
 
@@ -349,7 +388,7 @@ def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, 
     for name, _dt, base_f, _cap_f, n_f in abi.TABLES:
         n = int(exec_rows[w][n_f])
         n = min(n, int(r[_cap_f]))
-        idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * batch.stride
+        idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * int(batch.wf_strides()[w])
         out[name] = tables[name][idx]
     return out
 
@@ -363,12 +402,8 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
     workflow that outgrows its tier is replayed by the general path, so this affects speed only."""
     n = batch.n_wf
     cnt = batch.wf["ev_count"].astype(np.int64)
-    if batch.stride == 1:
-        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + \
-            (np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
-    else:
-        step = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
-        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + step * batch.stride
+    step = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + step * np.repeat(batch.wf_strides(), cnt)
     t = (batch.cols["etype"][idx] & abi.ETYPE_MASK).astype(np.int64)
     wf_of = np.repeat(np.arange(n), cnt)
     out = {}
@@ -420,6 +455,15 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
     return out
 
 
+# per-wave LDS arenas of the wave-per-workflow tail (replay_kernel.hip WaveTier<SmallTier>)
+WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp": 24}
+
+
 def fits_small_tier(batch: HistoryBatch) -> bool:
+    """Whether the 3-blocks/CU LDS tier holds every workflow's live sets (lane part: 1 entry per
+    map; wave tail: the small per-wave arena)."""
     b = live_set_bounds(batch)
-    return all(bool((b[k] <= v).all()) for k, v in SMALL_TIER.items())
+    nl = batch.n_wf if batch.wave_begin is None else batch.wave_begin
+    lane_ok = all(bool((b[k][:nl] <= v).all()) for k, v in SMALL_TIER.items())
+    tail_ok = all(bool((b[k][nl:] <= v).all()) for k, v in WAVE_SMALL_TIER.items())
+    return lane_ok and tail_ok

@@ -20,7 +20,7 @@ class ReplayResult:
         out = {}
         for name, _dt, base_f, cap_f, n_f in abi.TABLES:
             n = min(int(self.exec[w][n_f]), int(r[cap_f]))
-            idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * batch.stride
+            idx = int(r[base_f]) + np.arange(n, dtype=np.int64) * int(batch.wf_strides()[w])
             out[name] = self.tables[name][idx]
         return out
 
@@ -45,7 +45,7 @@ def gather_live(batch: HistoryBatch, res: ReplayResult) -> Dict[str, np.ndarray]
             continue
         wf_idx = np.repeat(np.arange(batch.n_wf), n)
         slot = np.arange(tot) - np.repeat(np.cumsum(n) - n, n)
-        idx = batch.wf[base_f].astype(np.int64)[wf_idx] + slot * batch.stride
+        idx = batch.wf[base_f].astype(np.int64)[wf_idx] + slot * batch.wf_strides()[wf_idx]
         out[name] = res.tables[name][idx]
     return out
 
@@ -112,6 +112,6 @@ def _live_canonical(batch: HistoryBatch, res: ReplayResult):
             continue
         wf_idx = np.repeat(order, n)
         slot = np.arange(tot) - np.repeat(np.cumsum(n) - n, n)
-        idx = batch.wf[base_f].astype(np.int64)[wf_idx] + slot * batch.stride
+        idx = batch.wf[base_f].astype(np.int64)[wf_idx] + slot * batch.wf_strides()[wf_idx]
         out[name] = res.tables[name][idx]
     return out

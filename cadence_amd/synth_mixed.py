@@ -43,6 +43,10 @@ class _Walk:
         self.sigs = set()
         self.closed = False
         self.attempt = 0
+        self.caps = None         # optional concurrency caps {"act", "timer", "child", "rc", "sig"}
+
+    def full(self, what: str, live) -> bool:
+        return self.caps is not None and len(live) >= self.caps[what]
 
     def ev(self, t, **attrs) -> HistoryEvent:
         self.eid += 1
@@ -91,7 +95,9 @@ class _Walk:
         out = []
         for _ in range(self.rng.choice([0, 1, 1, 2, 3])):
             kind = self.rng.random()
-            if kind < 0.40:
+            if kind < 0.40 and self.full("act", self.acts):
+                e = self.ev(ET.MarkerRecorded)
+            elif kind < 0.40:
                 dup = self.acts and self.rng.random() < 0.05
                 aid = self.rng.choice(list(self.acts)) if dup else str(self.act_seq)
                 self.act_seq += 1
@@ -103,18 +109,26 @@ class _Walk:
                             retry_policy=({"expiration_interval_in_seconds": self.rng.randint(0, 600)}
                                           if self.rng.random() < 0.3 else None))
                 self.acts[aid] = [e.id, False]
+            elif kind < 0.60 and self.full("timer", self.timers):
+                e = self.ev(ET.MarkerRecorded)
             elif kind < 0.60:
                 dup = self.timers and self.rng.random() < 0.1
                 tid = self.rng.choice(list(self.timers)) if dup else f"t{self.timer_seq}"
                 self.timer_seq += 1
                 e = self.ev(ET.TimerStarted, timer_id=tid, start_to_fire_timeout_seconds=self.rng.randint(1, 100000))
                 self.timers[tid] = e.id
+            elif kind < 0.67 and self.full("child", self.children):
+                e = self.ev(ET.MarkerRecorded)
             elif kind < 0.67:
                 e = self.ev(ET.StartChildWorkflowExecutionInitiated, domain=self.domain())
                 self.children[e.id] = False
+            elif kind < 0.72 and self.full("rc", self.rcs):
+                e = self.ev(ET.MarkerRecorded)
             elif kind < 0.72:
                 e = self.ev(ET.RequestCancelExternalWorkflowExecutionInitiated, domain=self.domain())
                 self.rcs.add(e.id)
+            elif kind < 0.77 and self.full("sig", self.sigs):
+                e = self.ev(ET.MarkerRecorded)
             elif kind < 0.77:
                 e = self.ev(ET.SignalExternalWorkflowExecutionInitiated, domain=self.domain())
                 self.sigs.add(e.id)
@@ -189,8 +203,9 @@ class _Walk:
 
 
 def random_workflow(rng: random.Random, w: int, target_len: int, multi_version=False, invalid=False,
-                    domains=("domain-a", "domain-b", "unknown-domain")) -> WorkflowHistory:
+                    domains=("domain-a", "domain-b", "unknown-domain"), force_close=None, caps=None) -> WorkflowHistory:
     k = _Walk(rng, w, multi_version, list(domains))
+    k.caps = caps
     prev = None
     if rng.random() < 0.1:
         prev = [f"bin-{rng.randint(0, 3)}" for _ in range(rng.randint(0, 3))]
@@ -236,6 +251,14 @@ def random_workflow(rng: random.Random, w: int, target_len: int, multi_version=F
             ext.append(k.sched_decision())
         k.emit(ext)
     # close
+    if force_close is not None and not k.closed:
+        if k.dec_started is None:
+            if k.dec_sched is None:
+                k.emit([k.sched_decision()])
+            k.emit([k.start_decision()])
+        k.emit([k.ev(ET.DecisionTaskCompleted, scheduled_event_id=k.dec_sched, started_event_id=k.dec_started,
+                     binary_checksum=binsum), k.ev(force_close)])
+        k.closed = True
     if not k.closed:
         r = rng.random()
         if k.dec_started is not None and r < 0.6:
@@ -325,3 +348,60 @@ def _attach_new_runs(rng: random.Random, hs: List[WorkflowHistory], rate: float)
             nr.batches[0][1].version = nr.batches[0][0].version - 1 if nr.batches[0][0].version > 0 else -5
         last.attrs["new_run"] = len(hs)
         hs.append(nr)
+
+
+def zipf_lengths(rng: random.Random, n: int, alpha: float = 1.2, min_len: int = 10, max_len: int = 50_000):
+    """History lengths ~ min_len * Zipf(alpha), truncated to max_len."""
+    out = []
+    for _ in range(n):
+        u = rng.random()
+        # inverse CDF of the continuous Pareto(alpha - 1) tail as a Zipf stand-in
+        k = (1.0 - u) ** (-1.0 / (alpha - 1.0)) if alpha > 1.0 else 1.0 / max(1.0 - u, 1e-12)
+        out.append(int(min(max_len, max(min_len, min_len * k))))
+    return out
+
+
+LONG_TAIL_CAPS = {"act": 32, "timer": 16, "child": 8, "rc": 4, "sig": 4}
+
+
+def long_tail_histories(n: int, seed: int, alpha: float = 1.2, min_len: int = 10, max_len: int = 50_000,
+                        run_cap: int = 10_000, multi_version=False, invalid_rate=0.0,
+                        caps=LONG_TAIL_CAPS) -> List[WorkflowHistory]:
+    """Config 4: n logical workflows with Zipf-distributed total lengths, continued-as-new every
+    <= run_cap events.  Every run is its own history (replayed independently); a run closed by
+    ContinuedAsNew carries the next run's first batch as its new-run history (state_builder.go:587-627).
+    ``caps`` bounds the concurrently pending activities / timers / children / external requests
+    (a long-running workflow keeps a bounded working set; None: unbounded random walk)."""
+    rng = random.Random(seed)
+    out: List[WorkflowHistory] = []
+    links = []
+    w = 0
+    for total in zipf_lengths(rng, n, alpha, min_len, max_len):
+        runs = []
+        left = total
+        while True:
+            this = min(left, run_cap)
+            left -= this
+            more = left > 0
+            h = random_workflow(rng, w, this, multi_version=multi_version,
+                                invalid=(not more) and rng.random() < invalid_rate, domains=("domain-a", "domain-b"),
+                                caps=caps,
+                                force_close=ET.WorkflowExecutionContinuedAsNew if more else None)
+            w += 1
+            runs.append(h)
+            last = h.batches[-1][-1] if h.batches and h.batches[-1] else None
+            if not more or last is None or last.event_type != ET.WorkflowExecutionContinuedAsNew:
+                break
+        for a, b in zip(runs, runs[1:]):
+            links.append((len(out) + runs.index(a), len(out) + runs.index(b)))
+        out.extend(runs)
+    for ia, ib in links:   # the next run's first batch is the CAN event's new-run history
+        a, b = out[ia], out[ib]
+        last = a.batches[-1][-1]
+        nr = WorkflowHistory(batches=[[HistoryEvent(e.event_type, e.id, e.version, e.timestamp, e.task_id,
+                                                    dict(e.attrs)) for e in b.batches[0]]],
+                             domain_failover_version=b.domain_failover_version, workflow_id=a.workflow_id,
+                             run_id=b.run_id, branch_id=det_uuid("nrbranch", ib), now_ns=a.now_ns, is_new_run=True)
+        last.attrs["new_run"] = len(out)
+        out.append(nr)
+    return out

@@ -250,13 +250,17 @@ typedef struct crr_inputs {
     uint32_t                 n_wf;
     uint32_t                 stride;       /* 1 (canonical) or 64 (wave-interleaved) */
     uint32_t                 flags;        /* CRR_IN_* */
-    uint32_t                 reserved;
+    uint32_t                 wave_begin;   /* CRR_IN_WAVE_TAIL: workflows [wave_begin, n_wf) are long
+                                              histories laid out contiguously (stride 1), replayed one
+                                              per wavefront; [0, wave_begin) use `stride` */
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
 #define CRR_IN_LDS_SMALL   2u   /* hint: live sets are small (<= 1 pending entry per map): use the
                                    3-blocks/CU LDS tier; workflows that outgrow it are replayed by
                                    the general path, so the hint affects speed only */
+#define CRR_IN_WAVE_TAIL   4u   /* length bucketing (stride-64 batches only): workflows
+                                   [wave_begin, n_wf) are replayed one per wavefront */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (192 B). */
@@ -349,7 +353,7 @@ typedef struct crr_outputs {
     crr_initiated_row*   sig;
     crr_vh_item*         vh;
     crr_reset_point_row* rp;
-    uint32_t*            scratch;   /* engine scratch: >= n_wf + 64 words, contents undefined */
+    uint32_t*            scratch;   /* engine scratch: >= 2 * n_wf + 64 words, contents undefined */
 } crr_outputs;
 
 /* ---- entry points ----------------------------------------------------------------------------- */

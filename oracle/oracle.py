@@ -70,6 +70,8 @@ class _HostInputs:
             setattr(ci, field, a.ctypes.data)
         ci.n_wf = batch.n_wf
         ci.stride = batch.stride
+        ci.flags = batch.c_flags()
+        ci.wave_begin = batch.wave_begin or 0
         self.c = ci
         self.key_off = np.ascontiguousarray(batch.key_off, dtype=np.uint32)
         self.key_len = np.ascontiguousarray(batch.key_len, dtype=np.uint32)

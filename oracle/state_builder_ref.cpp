@@ -55,11 +55,16 @@ struct KeyStrings {  // per-event key strings (ActivityID / TimerID / BinaryChec
   const char* arena;
 };
 
+// per-workflow column/row stride: the long-history tail of a CRR_IN_WAVE_TAIL batch is contiguous
+inline i64 stride_of(const crr_inputs* in, const crr_workflow* wf) {
+  return ((in->flags & CRR_IN_WAVE_TAIL) && (uint32_t)(wf - in->wf) >= in->wave_begin) ? 1 : (i64)in->stride;
+}
+
 struct WfView {
   const crr_inputs* in;
   const crr_workflow* wf;
   const KeyStrings* ks;
-  i64 idx(int step) const { return wf->ev_begin + (i64)step * in->stride; }
+  i64 idx(int step) const { return wf->ev_begin + (i64)step * stride_of(in, wf); }
   int type(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_MASK; }
   bool first(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_BATCH_FIRST; }
   bool last(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_BATCH_LAST; }
@@ -923,7 +928,7 @@ uint32_t crc32_ieee_bitwise(const uint8_t* p, size_t n) {
 void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const Outcome& oc,
                  const crr_outputs* out) {
   const crr_workflow* wf = &in->wf[w];
-  const i64 st = in->stride;
+  const i64 st = stride_of(in, wf);
   crr_exec_row& r = out->exec[w];
   std::memset(&r, 0, sizeof(r));
   const ExecutionInfo& x = ms.exec;

@@ -71,7 +71,41 @@ def test_mixed_single_version(engine):
 
 def test_long_histories(engine):
     hs = synth_mixed.mixed_histories(200, 13, mean_len=600, multi_version=True, invalid_rate=0.1)
-    check(engine, interleave(flatten(hs, known_domains=KNOWN)))
+    b = flatten(hs, known_domains=KNOWN)
+    check(engine, interleave(b, long_threshold=None))   # lane per workflow
+    ib = interleave(b)                                    # length-bucketed: a wavefront per long history
+    assert ib.wave_begin < b.n_wf
+    check(engine, ib)
+
+
+def test_wave_per_workflow_all_event_types(engine):
+    """Every workflow of the mixed set replayed one per wavefront (LDS row arenas)."""
+    hs = synth_mixed.mixed_histories(3000, 21, multi_version=True, invalid_rate=0.25, can_rate=0.5)
+    ib = interleave(flatten(hs, known_domains=KNOWN), long_threshold=0)
+    assert ib.wave_begin == 0
+    got = check(engine, ib)
+    assert len(set(int(s) for s in got.exec["status"])) >= 8
+
+
+def test_long_tail_continue_as_new(engine):
+    """Config 4 shape: Zipf lengths, continue-as-new chains.  Unbounded random walks: live sets
+    outgrow both LDS arenas, so those workflows go through the HBM-row wavefront pass."""
+    hs = synth_mixed.long_tail_histories(300, 7, max_len=5000, run_cap=2000, multi_version=True, invalid_rate=0.1,
+                                         caps=None)
+    b = flatten(hs, known_domains=KNOWN)
+    ib = interleave(b)
+    got = check(engine, ib)
+    assert (got.exec["status"] == 0).sum() > 0.9 * b.n_wf
+    assert got.exec["n_activity"].max() > 64                # beyond the LDS arena
+    assert (b.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()
+
+
+def test_long_tail_bounded_working_set(engine):
+    """Config 4 with bounded pending sets (the per-wave LDS arenas), lanes + wavefronts mixed."""
+    hs = synth_mixed.long_tail_histories(400, 8, max_len=6000, run_cap=2500, multi_version=True, invalid_rate=0.1)
+    b = flatten(hs, known_domains=KNOWN)
+    for th in (None, 256, 64):
+        check(engine, interleave(b, long_threshold=th))
 
 
 def test_archival_fixture(engine):

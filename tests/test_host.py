@@ -89,6 +89,33 @@ def test_interleave_is_a_permutation():
             assert len(np.unique(v[g == gi])) == 1, f
 
 
+def test_interleave_wave_tail_layout():
+    """Length bucketing: histories longer than the threshold follow the lane groups, contiguous
+    (stride 1) in events and rows; row ranges of all workflows are disjoint."""
+    hs = synth_mixed.mixed_histories(300, 6, mean_len=60)
+    b = flatten(hs)
+    ib = interleave(b, long_threshold=60)
+    nl = ib.wave_begin
+    cnt = ib.wf["ev_count"]
+    assert 0 < nl < ib.n_wf
+    assert (cnt[:nl] <= 60).all() and (cnt[nl:] > 60).all()
+    assert (np.diff(cnt[nl:]) <= 0).all()                          # longest first
+    st = ib.wf_strides()
+    assert (st[:nl] == 64).all() and (st[nl:] == 1).all()
+    for w in range(nl, ib.n_wf):
+        c = int(ib.perm[w])
+        n = int(b.wf["ev_count"][c])
+        src = int(b.wf["ev_begin"][c]) + np.arange(n)
+        dst = int(ib.wf["ev_begin"][w]) + np.arange(n)
+        assert (b.cols["event_id"][src] == ib.cols["event_id"][dst]).all()
+    for name, _dt, base_f, cap_f, _n in abi.TABLES:
+        used = np.zeros(ib.table_rows[name] + 1, np.int32)
+        for w in range(ib.n_wf):
+            idx = int(ib.wf[base_f][w]) + np.arange(int(ib.wf[cap_f][w])) * int(st[w])
+            used[idx] += 1
+        assert used.max() <= 1, name
+
+
 def test_flatten_capacities_bound_live_sets():
     from oracle import oracle
     hs = synth_mixed.mixed_histories(400, 9, multi_version=True, invalid_rate=0.1)

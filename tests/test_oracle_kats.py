@@ -298,5 +298,7 @@ def test_canonical_vs_interleaved_layout_identical():
     from cadence_amd import synth_mixed
     hs = synth_mixed.mixed_histories(500, 3, multi_version=True, invalid_rate=0.2, can_rate=0.5)
     b = flatten(hs, known_domains={"domain-a", "domain-b", "parent-domain"})
-    ib = interleave(b)
-    assert not diff_results(b, oracle.replay(b, 2), ib, oracle.replay(ib, 2))
+    want = oracle.replay(b, 2)
+    for th in (None, 0, 40):   # all lanes, all wave tail, mixed
+        ib = interleave(b, long_threshold=th)
+        assert not diff_results(b, want, ib, oracle.replay(ib, 2)), th

@@ -1,0 +1,70 @@
+"""Config-4 probe: long-tail histories (Zipf lengths, continue-as-new chains) replayed with and
+without length bucketing; kernel time per layout and cross-layout bit-exactness.
+
+    python tools/prof_longtail.py [--n 400] [--max-len 50000] [--run-cap 10000] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=int, default=400, help="logical workflows (before CAN splitting)")
+    p.add_argument("--max-len", type=int, default=50_000)
+    p.add_argument("--run-cap", type=int, default=10_000)
+    p.add_argument("--seed", type=int, default=0xCAD00004)
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--thresholds", default="none,256,64")
+    p.add_argument("--unbounded", action="store_true", help="unbounded pending sets (random walk)")
+    a = p.parse_args()
+    import numpy as np
+    import torch
+    from cadence_amd import synth_mixed
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.flatten import flatten, interleave
+    from cadence_amd.result import diff_results
+
+    t0 = time.time()
+    kw = {"caps": None} if a.unbounded else {}
+    hs = synth_mixed.long_tail_histories(a.n, a.seed, max_len=a.max_len, run_cap=a.run_cap, **kw)
+    b = flatten(hs, known_domains={"domain-a", "domain-b", "parent-domain"})
+    gen_s = time.time() - t0
+    cnt = b.wf["ev_count"]
+    eng = ReplayEngine(0)
+    ref = None
+    for th in a.thresholds.split(","):
+        thv = None if th == "none" else int(th)
+        ib = interleave(b, long_threshold=thv)
+        db = eng.upload(ib)
+        eng.launch(db)
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(a.reps):
+            eng.launch(db)
+            torch.cuda.synchronize()
+            k = eng.last_kernel_ms()
+            ms.append(sum(x for x in k if x > 0))
+        res = eng.download(db)
+        retries = [int(x) for x in db.tensors["scratch"][:2].cpu().tolist()]
+        same = None
+        if ref is None:
+            ref = (ib, res)
+        else:
+            same = not diff_results(ref[0], ref[1], ib, res)
+        med = float(np.median(ms))
+        print(json.dumps({"threshold": th, "unbounded": a.unbounded, "workflows": b.n_wf, "events": int(cnt.sum()), "max_len": int(cnt.max()),
+                          "wave_tail": int(b.n_wf - (ib.wave_begin if ib.wave_begin is not None else b.n_wf)),
+                          "kernel_ms": ms, "median_ms": med, "events_per_s": float(cnt.sum()) / (med * 1e-3),
+                          "ok": int((res.exec["status"] == 0).sum()), "same_as_first": same,
+                          "retries_lane_wave": retries, "phase_ms": k,
+                          "gen_s": gen_s}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -73,14 +73,13 @@ def main():
         eng.launch(db, stream)
     torch.cuda.synchronize()
 
-    kernel_ms = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.timing_begin()          # per-launch HIP events around the dominant kernel, on the launch stream
     t_start = time.perf_counter()
     for _ in range(args.steps):
         eng.launch(db, stream)
-        kernel_ms.append(None)
         if world > 1:
             d = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
             cdist.all_reduce_digest(torch, dist, d)
@@ -88,12 +87,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    # per-launch kernel time with HIP events on the launch stream
-    ms = []
-    for _ in range(min(args.steps, 5)):
-        eng.launch(db, stream)
-        torch.cuda.synchronize()
-        ms.append(eng.last_kernel_ms()[1])
+    ms = eng.timing_read()
+    if len(ms) != args.steps:
+        raise RuntimeError(f"timed {len(ms)} kernel launches, expected {args.steps}")
     kernel_avg_ms = float(np.mean(ms))
 
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -102,6 +98,10 @@ def main():
     elapsed_max = float(t.item())
 
     res = eng.download(db)
+    from cadence_amd import abi
+    tier = "replay_lds_small_kernel" if db.c_in.flags & abi.IN_LDS_SMALL else "replay_lds_kernel"
+    tail = bool(db.c_in.flags & abi.IN_WAVE_TAIL) and db.c_in.wave_begin < db.n_wf
+    kernel_name = tier + ("<true>" if tail else "<false>")
     ok = bool((res.exec["status"] == 0).all())
     alg_bytes = synth.algorithmic_bytes(batch, res)
     achieved_gbs = alg_bytes / (kernel_avg_ms * 1e-3) / 1e9
@@ -130,7 +130,8 @@ def main():
         "all_ok": ok,
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": kernel_avg_ms, "algorithmic_bytes_per_launch": alg_bytes},
+                     "kernel": kernel_name, "kernel_ms": kernel_avg_ms,
+                     "algorithmic_bytes_per_launch": alg_bytes},
         "setup_s": gen_s,
     }
     if os.path.exists(PROFILE_TRAFFIC):

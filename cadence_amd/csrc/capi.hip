@@ -22,11 +22,23 @@ constexpr unsigned kRetryGrid = 512;
 constexpr unsigned kBigGrid = 1024;   // 2 blocks (waves) per CU x 256 CUs, twice over
 
 struct Timing {
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  bool valid[2] = {false, false};
+  // [0,1] phase 0, [2,3] phase 1, [4,5] the phase-1 fast-path kernel alone
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool valid[3] = {false, false, false};
   int device = -1;
 };
 thread_local Timing g_timing;
+
+// Per-launch record of the phase-1 fast-path kernel over a measured region (crr_timing_begin ..
+// crr_timing_read), without synchronising between launches: a ring of event pairs.
+constexpr int kRing = 512;
+struct TimingRing {
+  hipEvent_t ev[2 * kRing] = {};
+  int n = 0;          // launches recorded since crr_timing_begin
+  bool on = false;
+  int device = -1;
+};
+thread_local TimingRing g_ring;
 
 bool ensure_events() {
   int dev = 0;
@@ -91,7 +103,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   // fast-path grid: one block per 4 long (wave-tail) workflows, then one per 256 lane workflows
   const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
   const unsigned lds_grid = (in->n_wf - n_lane + kBlock / 64 - 1) / (kBlock / 64) + (n_lane + kBlock - 1) / kBlock;
-  g_timing.valid[0] = g_timing.valid[1] = false;
+  g_timing.valid[0] = g_timing.valid[1] = g_timing.valid[2] = false;
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
@@ -101,6 +113,9 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (err != hipSuccess) return (int)err;
       const bool tail = n_lane < in->n_wf;
       const bool small = (in->flags & CRR_IN_LDS_SMALL) != 0;
+      if (timed && phase == 1) (void)hipEventRecord(g_timing.ev[4], s);
+      const bool ring = phase == 1 && g_ring.on && g_ring.n < kRing;
+      if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n], s);
       if (small && tail)
         hipLaunchKernelGGL(crr::replay_lds_small_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
       else if (small)
@@ -111,6 +126,11 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         hipLaunchKernelGGL(crr::replay_lds_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
       err = hipGetLastError();
       if (err != hipSuccess) return (int)err;
+      if (timed && phase == 1) {
+        (void)hipEventRecord(g_timing.ev[5], s);
+        g_timing.valid[2] = true;
+      }
+      if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n++ + 1], s);
       // the workflows it handed back: one wavefront each, big LDS arena, then HBM rows
       const unsigned big_grid = in->n_wf < kBigGrid ? in->n_wf : kBigGrid;
       hipLaunchKernelGGL(crr::replay_wave_big_kernel, dim3(big_grid), dim3(64), 0, s, *in, *out, phase);
@@ -138,24 +158,53 @@ int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksu
   return (int)hipGetLastError();
 }
 
-float crr_last_kernel_ms(int phase) {
-  if (phase < 0 || phase > 1 || !g_timing.valid[phase]) return -1.0f;
+float crr_last_kernel_ms(int which) {
+  if (which < 0 || which > 2 || !g_timing.valid[which]) return -1.0f;
   float ms = -1.0f;
-  if (hipEventElapsedTime(&ms, g_timing.ev[2 * phase], g_timing.ev[2 * phase + 1]) != hipSuccess) return -1.0f;
+  if (hipEventElapsedTime(&ms, g_timing.ev[2 * which], g_timing.ev[2 * which + 1]) != hipSuccess) return -1.0f;
   return ms;
 }
 
-uint32_t crr_crc32_ieee(const uint8_t* data, size_t len) {
-  static uint32_t table[256];
-  static bool init = false;
-  if (!init) {
-    for (uint32_t i = 0; i < 256; ++i) {
-      uint32_t c = i;
-      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
-      table[i] = c;
+int crr_timing_begin(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (g_ring.device != dev) {
+    for (auto& e : g_ring.ev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
     }
-    init = true;
+    for (auto& e : g_ring.ev)
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+    g_ring.device = dev;
   }
+  g_ring.n = 0;
+  g_ring.on = true;
+  return 0;
+}
+
+int crr_timing_read(float* ms, int cap) {
+  g_ring.on = false;
+  int n = g_ring.n < cap ? g_ring.n : cap;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(g_ring.ev[2 * i + 1]) != hipSuccess) return -1;
+    if (hipEventElapsedTime(&ms[i], g_ring.ev[2 * i], g_ring.ev[2 * i + 1]) != hipSuccess) return -1;
+  }
+  return n;
+}
+
+uint32_t crr_crc32_ieee(const uint8_t* data, size_t len) {
+  struct Table {
+    uint32_t t[256];
+    Table() {
+      for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+        t[i] = c;
+      }
+    }
+  };
+  static const Table tab;  // thread-safe static init
+  const uint32_t* table = tab.t;
   uint32_t c = 0xFFFFFFFFu;
   for (size_t i = 0; i < len; ++i) c = table[(c ^ data[i]) & 0xff] ^ (c >> 8);
   return ~c;

@@ -44,6 +44,9 @@ def lib():
         L.crr_crc32_ieee.restype = ctypes.c_uint32
         L.crr_last_kernel_ms.argtypes = [ctypes.c_int]
         L.crr_last_kernel_ms.restype = ctypes.c_float
+        L.crr_timing_begin.restype = ctypes.c_int
+        L.crr_timing_read.argtypes = [vp, ctypes.c_int]
+        L.crr_timing_read.restype = ctypes.c_int
         if L.crr_abi_version() != abi.ABI_VERSION:
             raise EngineUnavailable("ABI version mismatch")
         abi.check_layout(L)
@@ -138,7 +141,21 @@ class ReplayEngine:
             raise RuntimeError(f"crr_replay failed: {rc}")
 
     def last_kernel_ms(self):
-        return [self.lib.crr_last_kernel_ms(0), self.lib.crr_last_kernel_ms(1)]
+        """[phase 0, phase 1 (all kernels), phase-1 fast-path kernel alone] in ms (-1: not run)."""
+        return [self.lib.crr_last_kernel_ms(i) for i in range(3)]
+
+    def timing_begin(self):
+        """Start recording the fast-path kernel of every launch (HIP events on the launch stream)."""
+        if self.lib.crr_timing_begin() != 0:
+            raise RuntimeError("crr_timing_begin failed")
+
+    def timing_read(self):
+        """End the measured region; per-launch fast-path kernel durations in ms."""
+        buf = (ctypes.c_float * 512)()
+        n = self.lib.crr_timing_read(buf, 512)
+        if n < 0:
+            raise RuntimeError("crr_timing_read failed")
+        return list(buf[:n])
 
     def checksum(self, db: DeviceBatch, stream=None) -> np.ndarray:
         """Recompute checksums of the replayed rows on the device (Load verify path)."""

@@ -388,8 +388,16 @@ size_t crr_sizeof(int which);   /* 0 workflow, 1 exec row, 2 activity, 3 timer, 
 uint32_t crr_crc32_ieee(const uint8_t* data, size_t len);
 
 /* Last launch's kernel time in milliseconds measured with HIP events on `stream`
- * (phase 0: new-run histories, phase 1: the rest).  Valid after the stream has synchronised. */
-float crr_last_kernel_ms(int phase);
+ * (0: phase 0, new-run histories; 1: phase 1, the rest, all of its kernels; 2: the phase-1
+ * fast-path (lane/wave LDS) kernel alone).  Valid after the stream has synchronised; -1 if absent. */
+float crr_last_kernel_ms(int which);
+
+/* Measured region for benchmarks: after crr_timing_begin, every crr_replay on this thread records
+ * its phase-1 fast-path kernel with its own HIP event pair on the launch stream (up to 512 launches,
+ * no synchronisation between launches).  crr_timing_read ends the region, waits for the events and
+ * writes up to `cap` per-launch durations (ms); returns how many, or -1 on a HIP error. */
+int crr_timing_begin(void);
+int crr_timing_read(float* ms, int cap);
 
 #ifdef __cplusplus
 }

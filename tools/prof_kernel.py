@@ -19,7 +19,12 @@ def main():
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--mixed", action="store_true", help="config-3-like mixed histories instead of chains")
+    p.add_argument("--calib", action="store_true", help="first stream known byte counts (tools/calib.py)")
     a = p.parse_args()
+    if a.calib:   # in-process (never spawn or exec from a process the profiler has put on the GPU)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import calib
+        calib.run(1024, 2)
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
     import numpy as np

@@ -25,8 +25,11 @@
 
 #include "cadence_replay.h"
 
-#ifndef CRR_WATERFALL
-#define CRR_WATERFALL 0
+// Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
+// checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
+// record loads, bit 16 the start side record loads.
+#ifndef CRR_EXP
+#define CRR_EXP 0
 #endif
 #ifndef CRR_LDS_ACT
 #define CRR_LDS_ACT 2
@@ -1318,25 +1321,66 @@ struct WaveTables {
 // is read out of lane s % 64 into scalar registers.
 struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
 
+// Lane per workflow: step k of this lane's workflow is column element begin + k * st.
+// Loads are typed: the event type of step s+1 is fetched one step ahead of its columns, so only the
+// columns that type's transition reads are fetched (per-lane predicated loads; a wavefront whose
+// lanes all skip a column issues nothing for it).  TaskID is read once, for the last applied event.
+namespace need {  // event types whose transition reads the column (apply_event below)
+constexpr u64 bit(int t) { return 1ull << t; }
+constexpr u64 kTs = bit(CRR_EV_DECISION_TASK_SCHEDULED) | bit(CRR_EV_DECISION_TASK_STARTED) |
+                    bit(CRR_EV_ACTIVITY_TASK_SCHEDULED) | bit(CRR_EV_ACTIVITY_TASK_STARTED) | bit(CRR_EV_TIMER_STARTED);
+constexpr u64 kRef = bit(CRR_EV_DECISION_TASK_SCHEDULED) | bit(CRR_EV_DECISION_TASK_STARTED) |
+                     bit(CRR_EV_DECISION_TASK_COMPLETED) | bit(CRR_EV_ACTIVITY_TASK_STARTED) |
+                     bit(CRR_EV_ACTIVITY_TASK_COMPLETED) | bit(CRR_EV_ACTIVITY_TASK_FAILED) |
+                     bit(CRR_EV_ACTIVITY_TASK_TIMED_OUT) | bit(CRR_EV_ACTIVITY_TASK_CANCELED) | bit(CRR_EV_TIMER_STARTED) |
+                     bit(CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED) | bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED) |
+                     bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED) | bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED) |
+                     bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED) | bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT) |
+                     bit(CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED) | bit(CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED) |
+                     bit(CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED) | bit(CRR_EV_SIGNAL_EXTERNAL_FAILED) |
+                     bit(CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED);
+constexpr u64 kKey = bit(CRR_EV_DECISION_TASK_COMPLETED) | bit(CRR_EV_ACTIVITY_TASK_SCHEDULED) |
+                     bit(CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED) | bit(CRR_EV_TIMER_STARTED) | bit(CRR_EV_TIMER_FIRED) |
+                     bit(CRR_EV_TIMER_CANCELED);
+constexpr u64 kAux = bit(CRR_EV_WORKFLOW_EXECUTION_STARTED) | bit(CRR_EV_DECISION_TASK_SCHEDULED) |
+                     bit(CRR_EV_ACTIVITY_TASK_SCHEDULED) | bit(CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED) |
+                     bit(CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW) |
+                     bit(CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED) | bit(CRR_EV_SIGNAL_EXTERNAL_INITIATED);
+__device__ __forceinline__ bool has(u64 mask, u32 et) { return (mask >> (et & CRR_ETYPE_MASK)) & 1ull; }
+}  // namespace need
+
 struct LaneSource {
   const crr_events& E;
   i64 begin, st;
   i32 n;
-  Ev nx;
+  Ev nx;      // step s+1 (type and the columns it needs), in flight during step s
+  u32 et_nx;  // type byte of step s+2, in flight during step s
   __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count) : E(e), begin(b), st(stride), n(count) {}
-  __device__ __forceinline__ Ev load(i32 step) const {
+  __device__ __forceinline__ i64 ix(i32 step) const { return begin + (i64)step * st; }
+  __device__ __forceinline__ Ev load(i32 step, u32 et) const {
     Ev e;
-    const i64 ix = begin + (i64)step * st;
-    e.et = E.etype[ix]; e.id = E.event_id[ix]; e.ver = E.version[ix]; e.ts = E.timestamp[ix];
-    e.task = E.task_id[ix]; e.ref = E.ref[ix]; e.key = E.key[ix]; e.aux = E.aux[ix];
+    const i64 i = ix(step);
+    e.et = et;
+    e.id = E.event_id[i];
+    e.ver = E.version[i];
+    e.ts = need::has(need::kTs, et) ? E.timestamp[i] : 0;
+    e.ref = need::has(need::kRef, et) ? E.ref[i] : 0;
+    e.key = need::has(need::kKey, et) ? E.key[i] : 0u;
+    e.aux = need::has(need::kAux, et) ? E.aux[i] : 0;
+    e.task = 0;
     return e;
   }
-  __device__ __forceinline__ void start() { if (n > 0) nx = load(0); }
+  __device__ __forceinline__ void start() {
+    if (n > 0) nx = load(0, E.etype[ix(0)]);
+    if (n > 1) et_nx = E.etype[ix(1)];
+  }
   __device__ __forceinline__ Ev next(i32 s) {
     const Ev e = nx;
-    if (s + 1 < n) nx = load(s + 1);
+    if (s + 1 < n) nx = load(s + 1, et_nx);
+    if (s + 2 < n) et_nx = E.etype[ix(s + 2)];
     return e;
   }
+  __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[ix(step)]; }
 };
 
 struct WaveSource {
@@ -1356,6 +1400,7 @@ struct WaveSource {
     e.task = E.task_id[ix]; e.ref = E.ref[ix]; e.key = E.key[ix]; e.aux = E.aux[ix];
     return e;
   }
+  __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[begin + (i64)step * st]; }
   __device__ __forceinline__ static i64 rl64(i64 v, i32 l) {
     const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
     const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
@@ -1443,82 +1488,23 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
 }
 
 // ---------------------------------------------------------------------------------------------------
-template <class P, class SRC>
-__device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
-                                            const Geo& G, P& T, SRC& src, const u32* crc_tables) {
-  const i32 n_ev = wfp->ev_count;
-  const i32 empty_at = wfp->empty_batch_at;
-  const i64 now_ns = wfp->now_ns;
-
-  // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
-  Lane L;
-  L.state = CRR_STATE_CREATED; L.close_status = CRR_CLOSE_NONE;
-  L.next_event_id = CRR_FIRST_EVENT_ID; L.last_first_event_id = 0; L.last_event_task_id = 0;
-  L.last_processed_event = CRR_EMPTY_EVENT_ID; L.completion_event_batch_id = 0;
-  L.decision_version = CRR_EMPTY_VERSION; L.decision_schedule_id = CRR_EMPTY_EVENT_ID;
-  L.decision_started_id = CRR_EMPTY_EVENT_ID; L.decision_attempt = 0;
-  L.decision_started_ts = 0; L.decision_scheduled_ts = 0; L.decision_orig_scheduled_ts = 0;
-  L.decision_timeout = 0; L.decision_request_src = CRR_SRC_EMPTY_UUID;
-  L.signal_count = 0; L.decision_start_to_close = 0; L.start_src = -1; L.flags = 0;
-  L.current_version = wfp->init_version;
-  L.vh_last_id = 0; L.vh_last_ver = 0; L.vh_n = 0; L.token_src = 0;
-  L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = 0;
-  L.inconsistencies = 0;
-  L.status = CRR_OK; L.fail_step = -1;
-
-  i64 batch_first_id = 0;
-#define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
-#define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
-
-  src.start();
-  for (i32 s = 0; s < n_ev; ++s) {
-    if (s == empty_at) FAIL(CRR_ERR_EMPTY_HISTORY, s);  // state_builder.go:98-100
-    const Ev ev = src.next(s);
-    const u32 et = ev.et;
-    const i64 id = ev.id;
-    const i64 ver = ev.ver;
-    const i32 t = et & CRR_ETYPE_MASK;
-    if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = id;  // firstEvent := history[0] (:101)
-
-    // :112 UpdateCurrentVersion(event.Version, true) (mutable_state_builder.go:495-533)
-    if (L.state == CRR_STATE_COMPLETED) {
-      if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, s);
-      L.current_version = L.vh_last_ver;
-    } else {
-      L.current_version = ver;
-    }
-    // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
-    if (id < 0 || (ver < 0 && ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, s);
-    if (L.vh_n == 0) {
-      if (G.vh_cap < 1) FAIL(CRR_ERR_CAPACITY, s);
-      L.vh_last_id = id; L.vh_last_ver = ver; L.vh_n = 1;
-    } else if (ver < L.vh_last_ver) {
-      FAIL(CRR_ERR_VH_LOWER_VERSION, s);
-    } else if (id <= L.vh_last_id) {
-      FAIL(CRR_ERR_VH_EVENT_ID_NOT_INCREASING, s);
-    } else if (ver > L.vh_last_ver) {
-      if (L.vh_n >= G.vh_cap) FAIL(CRR_ERR_CAPACITY, s);
-      crr_vh_item* it = G.vh(L.vh_n - 1);
-      it->event_id = L.vh_last_id;
-      it->version = L.vh_last_ver;
-      L.vh_last_id = id; L.vh_last_ver = ver; ++L.vh_n;
-    } else {
-      L.vh_last_id = id;
-    }
-    L.last_event_task_id = ev.task;  // :129
-
-#if CRR_WATERFALL
-    // Waterfall dispatch: one pass per distinct event type present in the wavefront; the type is
-    // wave-uniform inside a pass, so the 42-way switch is a scalar jump, not an exec-mask tree.
-    for (;;) {
-    const i32 tu = uniform32(t);
-    if (t != tu) continue;
-    switch (tu) {
-#else
+// One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
+// code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
+template <class P>
+__device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outputs& out, Lane& L, const Geo& G, P& T,
+                                           const Ev& ev, const i32 s, const i32 t, const i64 batch_first_id,
+                                           const i64 now_ns) {
+  const i64 id = ev.id;
+  const i64 ver = ev.ver;
+#define FAIL(code, step) return (code)
+#define CHECK(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
     switch (t) {
-#endif
       case CRR_EV_WORKFLOW_EXECUTION_STARTED: {  // :132-183 -> mutable_state_builder.go:1751-1829
+#if CRR_EXP & 16
+        crr_start_side ss{10, 100, 0, -1, 0, 0, -1, 0};
+#else
         const crr_start_side ss = in.start_side[ev.aux];
+#endif
         if (ss.parent_domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         L.decision_start_to_close = ss.decision_start_to_close;
         L.start_src = s;
@@ -1580,7 +1566,11 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         fail_decision_and_transient(L, now_ns);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
+#if CRR_EXP & 8
+        crr_activity_side as{10, 20, 30, 0, 0, 0, 1, 0};
+#else
         const crr_activity_side as = in.act_side[ev.aux];
+#endif
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         crr_activity_row row;
         row.schedule_id = id;
@@ -1717,13 +1707,92 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       default:  // :629-630
         FAIL(CRR_ERR_UNKNOWN_EVENT_TYPE, s);
     }
-#if CRR_WATERFALL
-    break;
+#undef CHECK
+#undef FAIL
+  return CRR_OK;
+}
+
+template <class P, class SRC>
+__device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
+                                            const Geo& G, P& T, SRC& src, const u32* crc_tables) {
+  const i32 n_ev = wfp->ev_count;
+  const i32 empty_at = wfp->empty_batch_at;
+  const i64 now_ns = wfp->now_ns;
+
+  // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
+  Lane L;
+  L.state = CRR_STATE_CREATED; L.close_status = CRR_CLOSE_NONE;
+  L.next_event_id = CRR_FIRST_EVENT_ID; L.last_first_event_id = 0; L.last_event_task_id = 0;
+  L.last_processed_event = CRR_EMPTY_EVENT_ID; L.completion_event_batch_id = 0;
+  L.decision_version = CRR_EMPTY_VERSION; L.decision_schedule_id = CRR_EMPTY_EVENT_ID;
+  L.decision_started_id = CRR_EMPTY_EVENT_ID; L.decision_attempt = 0;
+  L.decision_started_ts = 0; L.decision_scheduled_ts = 0; L.decision_orig_scheduled_ts = 0;
+  L.decision_timeout = 0; L.decision_request_src = CRR_SRC_EMPTY_UUID;
+  L.signal_count = 0; L.decision_start_to_close = 0; L.start_src = -1; L.flags = 0;
+  L.current_version = wfp->init_version;
+  L.vh_last_id = 0; L.vh_last_ver = 0; L.vh_n = 0; L.token_src = 0;
+  L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = 0;
+  L.inconsistencies = 0;
+  L.status = CRR_OK; L.fail_step = -1;
+
+  i64 batch_first_id = 0;
+  i32 last_task_step = -1;
+#define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
+#define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
+
+  src.start();
+  for (i32 s = 0; s < n_ev; ++s) {
+    if (s == empty_at) FAIL(CRR_ERR_EMPTY_HISTORY, s);  // state_builder.go:98-100
+    const Ev ev = src.next(s);
+    const u32 et = ev.et;
+    const i64 id = ev.id;
+    const i64 ver = ev.ver;
+    const i32 t = et & CRR_ETYPE_MASK;
+    if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = id;  // firstEvent := history[0] (:101)
+
+    // :112 UpdateCurrentVersion(event.Version, true) (mutable_state_builder.go:495-533)
+    if (L.state == CRR_STATE_COMPLETED) {
+      if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, s);
+      L.current_version = L.vh_last_ver;
+    } else {
+      L.current_version = ver;
     }
-#endif
+    // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
+    if (id < 0 || (ver < 0 && ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, s);
+    if (L.vh_n == 0) {
+      if (G.vh_cap < 1) FAIL(CRR_ERR_CAPACITY, s);
+      L.vh_last_id = id; L.vh_last_ver = ver; L.vh_n = 1;
+    } else if (ver < L.vh_last_ver) {
+      FAIL(CRR_ERR_VH_LOWER_VERSION, s);
+    } else if (id <= L.vh_last_id) {
+      FAIL(CRR_ERR_VH_EVENT_ID_NOT_INCREASING, s);
+    } else if (ver > L.vh_last_ver) {
+      if (L.vh_n >= G.vh_cap) FAIL(CRR_ERR_CAPACITY, s);
+      crr_vh_item* it = G.vh(L.vh_n - 1);
+      it->event_id = L.vh_last_id;
+      it->version = L.vh_last_ver;
+      L.vh_last_id = id; L.vh_last_ver = ver; ++L.vh_n;
+    } else {
+      L.vh_last_id = id;
+    }
+    last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
+
+    // :131-631 the 42-way dispatch.  When every active lane holds the same event type (the
+    // common case: histories of one workflow type replay in lockstep) the type is wave-uniform
+    // and the switch runs on a scalar register -- scalar branches, no exec-mask tree; otherwise
+    // the per-lane switch.
+    {
+      int rc;
+      const i32 tu = uniform32(t);
+      if (__builtin_amdgcn_ballot_w64(t != tu) == 0)
+        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns);
+      else
+        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns);
+      if (rc) FAIL(rc, s);
+    }
 
     if (et & CRR_ETYPE_BATCH_LAST) {
-      T.epilogue(L, G);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
+      if (!(CRR_EXP & 2)) T.epilogue(L, G);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
       L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
@@ -1739,6 +1808,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 done_events:
 #undef CHECK
 #undef FAIL
+  if (last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
     out.exec[w].status = CRR_INTERNAL_RETRY;
@@ -1788,7 +1858,7 @@ done_events:
   R.payload_len = 0;
   R.reserved[0] = 0;
   R.reserved[1] = 0;
-  if (L.status == CRR_OK) R.checksum = payload_crc(R, T, G, wfp, in.arena, crc_tables, &R.payload_len);
+  if (L.status == CRR_OK && !(CRR_EXP & 1)) R.checksum = payload_crc(R, T, G, wfp, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
 }
 
@@ -1853,7 +1923,10 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   replay_body(in, out, w, wfp, G, T, S, crc_tables);
 }
 template <bool WAVE_TAIL>
-__global__ void __launch_bounds__(kBlock, 3) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
+#ifndef CRR_SMALL_WAVES_PER_EU
+#define CRR_SMALL_WAVES_PER_EU 3
+#endif
+__global__ void __launch_bounds__(kBlock, CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
   replay_lds<SmallTier, WAVE_TAIL>(in, out, phase);
 }
 template <bool WAVE_TAIL>

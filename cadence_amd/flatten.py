@@ -359,9 +359,17 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
         key_off[dst_idx] = batch.key_off[src_idx]
         key_len[dst_idx] = batch.key_len[src_idx]
 
+    # side records follow their events: the k-th record of lane l of group g sits at
+    # side_base[g] + k * 64 + l, so a wavefront reading the same ordinal is one coalesced run
+    ev_type = batch.cols["etype"][src_idx] & abi.ETYPE_MASK
+    act_side = _interleave_side(batch.act_side, ev_type == ET.ActivityTaskScheduled, wf_pos, src_idx, dst_idx,
+                                cols, n, n_lane, n_groups, wave, group, lane)
+    start_side = _interleave_side(batch.start_side, ev_type == ET.WorkflowExecutionStarted, wf_pos, src_idx, dst_idx,
+                                  cols, n, n_lane, n_groups, wave, group, lane)
+
     wf = batch.wf[perm].copy()
     wf["ev_begin"] = dev_begin
-    out = HistoryBatch(cols=cols, act_side=batch.act_side, start_side=batch.start_side,
+    out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
                        wave_begin=n_lane if long_threshold is not None else None)
@@ -378,6 +386,35 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
         wf[cap_f][:n_lane] = gcap[group[:n_lane]]
         wf[base_f][n_lane:] = lane_rows + np.concatenate([[0], np.cumsum(tcap)[:-1]]).astype(np.int64)
         out.table_rows[name] = lane_rows + int(tcap.sum())
+    return out
+
+
+def _interleave_side(side: np.ndarray, sel: np.ndarray, wf_pos, src_idx, dst_idx, cols, n, n_lane, n_groups, wave,
+                     group, lane) -> np.ndarray:
+    """Re-home the side records referenced by the selected events (wave-interleaved by ordinal) and
+    point those events' ``aux`` at the new positions (``cols`` is already in device order)."""
+    if not sel.any():
+        return side
+    w = wf_pos[sel]                      # device workflow of each referencing event (ascending)
+    cnt = np.bincount(w, minlength=n).astype(np.int64)
+    k = np.arange(w.size) - np.repeat(np.cumsum(cnt) - cnt, cnt)[: w.size]
+    gcap = np.zeros(max(n_groups, 1), np.int64)
+    if n_lane:
+        np.maximum.at(gcap, group[:n_lane], cnt[:n_lane])
+    gbase = np.concatenate([[0], np.cumsum(gcap * wave)[:-1]]).astype(np.int64)
+    lane_rows = int((gcap * wave).sum())
+    tcnt = cnt[n_lane:]
+    tbase = lane_rows + np.concatenate([[0], np.cumsum(tcnt)[:-1]]).astype(np.int64)
+    is_lane = w < n_lane
+    new_idx = np.empty(w.size, np.int64)
+    wl = w[is_lane]
+    new_idx[is_lane] = gbase[group[wl]] + k[is_lane] * wave + lane[wl]
+    wt = w[~is_lane]
+    new_idx[~is_lane] = tbase[wt - n_lane] + k[~is_lane]
+    out = np.zeros(max(lane_rows + int(tcnt.sum()), 1), side.dtype)
+    dst = dst_idx[sel]
+    out[new_idx] = side[cols["aux"][dst]]
+    cols["aux"][dst] = new_idx.astype(np.int32)
     return out
 
 

@@ -146,6 +146,7 @@ ROW_HAS_RETRY = 8
 ROW_RESETTABLE = 16
 
 WF_FLAG_NEW_RUN = 1
+WF_FLAG_REFRESH_TASKS = 2      # Rebuild's RefreshTasks state effects after the replay
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4

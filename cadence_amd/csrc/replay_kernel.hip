@@ -491,6 +491,15 @@ struct GlobalTables {
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r->last_hb_timeout_vis_s = unix_seconds(B.t);
       }
     }
+    epilogue_timers(L, G);
+  }
+  // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
+  __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
+    for (i32 j = 0; j < hw_act; ++j) G.act(j)->timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+    for (i32 j = 0; j < hw_timer; ++j) G.timer(j)->task_status = CRR_TIMER_TASK_STATUS_NONE;
+    epilogue(L, G);
+  }
+  __device__ __forceinline__ void epilogue_timers(Lane& L, const Geo& G) {
     if (L.n_timer > 0) {
       BestTimer B;
       for (i32 j = 0; j < hw_timer; ++j) {
@@ -551,6 +560,7 @@ using LargeTier = Tier<CRR_LDS_ACT, CRR_LDS_TIMER, CRR_LDS_CHILD, CRR_LDS_RC, CR
                        R_SLOTS = TIER::R_SLOTS, S_SLOTS = TIER::S_SLOTS, P_SLOTS = TIER::P_SLOTS;
 // activity LDS flag bits: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + STARTED; TimerTaskStatus << 8
 constexpr u32 LF_STARTED = 32u;
+constexpr u32 LF_HB_VIS = 64u;  // a heartbeat timer was created: LastHeartbeatTimeoutVisibilityInSeconds set
 constexpr int LF_TTS_SHIFT = 8;
 constexpr u32 TF_CREATED = 2u;  // timer LDS flag: TaskStatus == TimerTaskStatusCreated
 
@@ -657,7 +667,7 @@ struct LdsTables {
     const u32 f = M->a_fl[j][t];
     // a restart after the heartbeat timer was created: LastHeartbeatTimeoutVisibilityInSeconds is no
     // longer derivable from the latest StartedTime -> let the general path replay this workflow
-    if ((f & LF_STARTED) && (f & (CRR_TTS_CREATED_HEARTBEAT << LF_TTS_SHIFT))) return CRR_INTERNAL_RETRY;
+    if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;
     M->a_start_t[j][t] = ts;
     M->a_fl[j][t] = f | LF_STARTED;
     M->a_src[j][t].y = s;
@@ -791,7 +801,8 @@ struct LdsTables {
         activity_candidates(B, j, M->a_sid[j][t], M->a_sched_t[j][t], (f & LF_STARTED) != 0, M->a_start_t[j][t],
                             to.x, to.y, to.z, to.w, f >> LF_TTS_SHIFT);
       }
-      if (B.have && !B.created) M->a_fl[B.j][t] |= timer_mask(B.y) << LF_TTS_SHIFT;
+      if (B.have && !B.created)
+        M->a_fl[B.j][t] |= (timer_mask(B.y) << LF_TTS_SHIFT) | (B.y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
     }
     if (L.n_timer > 0) {
       BestTimer B;
@@ -803,6 +814,15 @@ struct LdsTables {
       }
       if (B.have && !B.created) M->t_fl[B.j][t] |= TF_CREATED;
     }
+  }
+
+  // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
+  __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
+#pragma unroll
+    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] &= ~(0xFu << LF_TTS_SHIFT);
+#pragma unroll
+    for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] &= ~TF_CREATED;
+    epilogue(L, G);
   }
 
   template <int N, class SwapFn>
@@ -853,7 +873,7 @@ struct LdsTables {
       r.started_id = started ? ev_id(src.y) : CRR_EMPTY_EVENT_ID;
       r.started_time = M->a_start_t[i][t];
       r.cancel_request_id = (f & CRR_ROW_CANCEL_REQUESTED) ? ev_id(src.z) : CRR_EMPTY_EVENT_ID;
-      r.last_hb_timeout_vis_s = (tts & CRR_TTS_CREATED_HEARTBEAT) ? unix_seconds(add_seconds(r.started_time, to.w)) : 0;
+      r.last_hb_timeout_vis_s = (f & LF_HB_VIS) ? unix_seconds(add_seconds(r.started_time, to.w)) : 0;
       r.sched_src = src.x;
       r.started_src = started ? src.y : -1;
       r.schedule_to_start = to.x; r.schedule_to_close = to.y; r.start_to_close = to.z; r.heartbeat = to.w;
@@ -1218,6 +1238,13 @@ struct WaveTables {
       wave_min(B);
       if (B.have && !B.created && own(B.j)) S.timer(B.j).task_status = CRR_TIMER_TASK_STATUS_CREATED;
     }
+  }
+  // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365); each lane clears the slots
+  // the epilogue's candidate loop reads with the same lane, so no cross-lane ordering is needed
+  __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
+    for (i32 j = lane; j < hw_act; j += 64) S.act(j).timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+    for (i32 j = lane; j < hw_timer; j += 64) S.timer(j).task_status = CRR_TIMER_TASK_STATUS_NONE;
+    epilogue(L, G);
   }
 
   // LdsRows: live rows -> HBM slots 0..n-1 in event-ID order (rank = number of smaller live IDs);
@@ -1805,6 +1832,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     if (want_id < 0 || (want_ver < 0 && want_ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, n_ev);
     if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
   }
+  if (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS) T.refresh(L, G);  // Rebuild's RefreshTasks (state_rebuilder.go:183)
 done_events:
 #undef CHECK
 #undef FAIL

@@ -253,7 +253,7 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         else:
             r["final_token_off"] = 0
             r["final_token_len"] = abi.NO_TOKEN
-        r["flags"] = abi.WF_FLAG_NEW_RUN if h.is_new_run else 0
+        r["flags"] = (abi.WF_FLAG_NEW_RUN if h.is_new_run else 0) | (abi.WF_FLAG_REFRESH_TASKS if h.refresh_tasks else 0)
         caps["act_cap"][w] = n_act
         caps["timer_cap"][w] = n_timer
         caps["child_cap"][w] = n_child

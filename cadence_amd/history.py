@@ -50,6 +50,7 @@ class WorkflowHistory:
     rebuild_last_event_id: int = 0
     rebuild_last_event_version: int = 0
     is_new_run: bool = False                  # CAN newRunHistory replayed by the outer workflow
+    refresh_tasks: bool = False               # Rebuild: RefreshTasks after the replay (state_rebuilder.go:183)
 
     @property
     def events(self) -> List[HistoryEvent]:

@@ -576,8 +576,11 @@ class StateBuilder:
                 e.attrs["new_run"] = self._new_run_w
         return None
 
-    def set_rebuild_target(self, token: bytes, last_event_id: int, last_event_version: int):
+    def set_rebuild_target(self, token: bytes, last_event_id: int, last_event_version: int, refresh_tasks: bool = True):
+        """Rebuild finalisation: SetCurrentBranchToken(token), the last-item check and (by default)
+        RefreshTasks' timer-status re-selection (state_rebuilder.go:150-183)."""
         self._bb.invalidate()
+        self._h.refresh_tasks = refresh_tasks
         self._h.final_token = token
         self._h.rebuild_last_event_id = last_event_id
         self._h.rebuild_last_event_version = last_event_version
@@ -603,7 +606,9 @@ def rebuild(batches: Sequence[List[HistoryEvent]], target_branch_token: bytes, b
     """``stateRebuilderImpl.Rebuild`` (state_rebuilder.go:97-191) over one workflow's persisted
     batches: replay, ``SetCurrentBranchToken(target)``, the last-item check, ``StartTimestamp = now``.
     Returns (state, rebuilt history size = sum of the pages' blob sizes, ``history_sizes``).
-    (CloseTransactionAsSnapshot / RefreshTasks emit tasks only: SURVEY.md §8f-2.)"""
+    RefreshTasks' state effect -- every pending activity's / user timer's timer-task status cleared
+    and the next timer of each sequence re-created -- is applied on the device
+    (CRR_WF_FLAG_REFRESH_TASKS); the transfer / timer tasks it emits are not."""
     sb = StateBuilder(domain_failover_version, domain_id, workflow_id, run_id, now_ns=now_ns,
                       batch_builder=batch_builder)
     for b in batches:

@@ -1,0 +1,87 @@
+/*
+ * cadence_decode.h -- host-side decoder: persisted history blobs -> the replay engine's SoA input.
+ *
+ * Replaces, for the replay path, the Go work before ApplyEvents:
+ *
+ *   common/persistence/serializer.go:109-119, :312-335   DeserializeBatchEvents (thriftrw blob -> []*HistoryEvent)
+ *   common/codec/version0Thriftrw.go:44-61               0x59 preamble + thrift binary (go.uber.org/thriftrw v1.29.2)
+ *   .gen/go/shared/shared.go:41935-42460                 HistoryEvent / *EventAttributes wire layout
+ *   the cgo shim's flattening loop   events -> columns, side records, interned keys
+ *
+ * Each workflow is a sequence of persisted batches (one blob per ApplyEvents call, in order, as
+ * state_rebuilder.go:135-148 pages them).  A blob is a thriftrw-encoded `shared.History{10: list<
+ * HistoryEvent>}` behind the 0x59 preamble; an empty blob or an empty event list is an empty batch.
+ * The output is a canonical (stride-1) crr_inputs image, byte-identical to what the Python host
+ * flattening (cadence_amd/flatten.py) produces from the same events.
+ *
+ * Plain C ABI: the decoder owns its output buffers until crr_decoded_free.
+ */
+#ifndef CADENCE_DECODE_H_
+#define CADENCE_DECODE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cadence_replay.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Host inputs of one workflow (the values the Go code takes from the shard, the domain cache,
+ * uuid.New() and timeSource.Now()). */
+typedef struct crr_wf_source {
+    uint32_t       blob_begin;            /* this workflow's batches: blobs[blob_begin .. blob_begin + blob_count) */
+    uint32_t       blob_count;
+    int64_t        init_version;          /* domainEntry.GetFailoverVersion() (mutable_state_builder.go:207) */
+    int64_t        now_ns;                /* injected timeSource.Now() */
+    const char*    run_id;                /* NUL-terminated; tree ID of the branch token */
+    const char*    branch_id;             /* injected uuid of NewHistoryBranchToken (state_builder.go:179-183) */
+    const uint8_t* final_token;           /* rebuild target token (state_rebuilder.go:150), NULL: none */
+    uint32_t       final_token_len;
+    int32_t        new_run_wf;            /* workflow index of the CAN new-run history, -1: none */
+    int64_t        rebuild_last_event_id;
+    int64_t        rebuild_last_event_version;
+    int32_t        flags;                 /* CRR_WF_FLAG_NEW_RUN */
+    int32_t        reserved;
+} crr_wf_source;
+
+/* Read-only view of a decoded batch (host pointers, valid until crr_decoded_free). */
+typedef struct crr_decoded_view {
+    crr_events                ev;          /* columns, n_events entries each */
+    uint64_t                  n_events;
+    const crr_activity_side*  act_side;    uint64_t n_act_side;
+    const crr_start_side*     start_side;  uint64_t n_start_side;
+    const uint32_t*           reset_keys;  uint64_t n_reset_keys;
+    const uint8_t*            arena;       uint64_t n_arena;
+    const crr_workflow*       wf;          uint32_t n_wf;
+    uint64_t                  table_rows[7];  /* act, timer, child, rc, sig, vh, rp slot-table sizes */
+    /* per-event key strings (ActivityID / TimerID / BinaryChecksum; "" otherwise), for checkers */
+    const uint32_t*           key_off;
+    const uint32_t*           key_len;
+    const char*               key_arena;   uint64_t n_key_arena;
+} crr_decoded_view;
+
+typedef struct crr_decoded crr_decoded;
+
+#define CRR_DECODE_OK              0
+#define CRR_DECODE_BAD_ARGUMENT   -1
+#define CRR_DECODE_BAD_PREAMBLE   -2   /* not a version-0 thriftrw blob (version0Thriftrw.go:53-58) */
+#define CRR_DECODE_TRUNCATED      -3   /* thrift value runs past the end of the blob */
+#define CRR_DECODE_BAD_TYPE       -4   /* field / element of an unexpected or unknown thrift type */
+
+/* Decode every workflow's blobs.  known_domains: names the domain cache resolves (NULL with
+ * n_known == UINT32_MAX: every name resolves).  n_threads <= 0: hardware concurrency.
+ * Returns NULL on error with *err = CRR_DECODE_* and *err_blob = index of the offending blob
+ * (the Go serializer's CadenceDeserializationError). */
+crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* blob_lens, uint32_t n_blobs,
+                                  const crr_wf_source* wfs, uint32_t n_wf,
+                                  const char* const* known_domains, uint32_t n_known,
+                                  int n_threads, int* err, int64_t* err_blob);
+int  crr_decoded_get_view(const crr_decoded* d, crr_decoded_view* view);
+void crr_decoded_free(crr_decoded* d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CADENCE_DECODE_H_ */

@@ -239,6 +239,10 @@ typedef struct crr_workflow {
 } crr_workflow;
 
 #define CRR_WF_FLAG_NEW_RUN 1
+/* After the replay (and the rebuild last-item check), apply Rebuild's RefreshTasks state effects
+ * (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): clear every pending activity's
+ * TimerTaskStatus and user timer's TaskStatus, then CreateNextActivityTimer / CreateNextUserTimer. */
+#define CRR_WF_FLAG_REFRESH_TASKS 2
 
 typedef struct crr_inputs {
     crr_events               ev;

@@ -572,6 +572,17 @@ class Replayer {
         return out;
       }
     }
+    // Rebuild's RefreshTasks (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): every
+    // pending activity's TimerTaskStatus and user timer's TaskStatus cleared, then one
+    // CreateNextActivityTimer / CreateNextUserTimer (LastHeartbeatTimeoutVisibilityInSeconds is kept)
+    if (wf->flags & CRR_WF_FLAG_REFRESH_TASKS) {
+      for (auto& kv : ms.pendingActivityInfoIDs) kv.second.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+      Err er = CreateNextActivityTimer(ms);
+      if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
+      for (auto& kv : ms.pendingTimerInfoIDs) kv.second.task_status = CRR_TIMER_TASK_STATUS_NONE;
+      er = CreateNextUserTimer(ms);
+      if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
+    }
     return out;
   }
 

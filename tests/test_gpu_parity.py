@@ -127,3 +127,28 @@ def test_c2_full_size_bit_exact(engine):
     engine.launch(db)
     cs = engine.checksum(db)
     assert (cs == got.exec["checksum"]).all()
+
+
+def test_rebuild_refresh_tasks_all_paths(engine):
+    """Rebuild's RefreshTasks (CRR_WF_FLAG_REFRESH_TASKS) on half of the workflows: lane path (small and
+    large LDS tiers), wavefront tail and the canonical-layout global path."""
+    import random
+    rng = random.Random(3)
+    for hs in (synth_mixed.mixed_histories(3000, 41, multi_version=True, invalid_rate=0.1, can_rate=0.3),
+               synth_mixed.long_tail_histories(60, 42, max_len=3000, run_cap=1500, multi_version=True)):
+        for h in hs:
+            h.refresh_tasks = rng.random() < 0.5
+        b = flatten(hs, known_domains=KNOWN)
+        check(engine, interleave(b))
+        check(engine, interleave(b, long_threshold=None))
+        check(engine, b)
+
+
+def test_decoded_blobs_replay_on_device(engine):
+    """Persisted thriftrw blobs -> native decoder -> device replay, bit-exact against the oracle."""
+    from cadence_amd.decode import WorkflowSource, decode_histories
+    from cadence_amd.thrift_codec import serialize_history
+    hs = synth_mixed.mixed_histories(2000, 43, multi_version=True, invalid_rate=0.2)
+    src = [WorkflowSource(blobs=serialize_history(h), run_id=h.run_id, branch_id=h.branch_id,
+                          domain_failover_version=h.domain_failover_version, now_ns=h.now_ns) for h in hs]
+    check(engine, interleave(decode_histories(src, known_domains=KNOWN)))

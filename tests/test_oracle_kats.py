@@ -302,3 +302,34 @@ def test_canonical_vs_interleaved_layout_identical():
     for th in (None, 0, 40):   # all lanes, all wave tail, mixed
         ib = interleave(b, long_threshold=th)
         assert not diff_results(b, want, ib, oracle.replay(ib, 2)), th
+
+
+def test_rebuild_refresh_tasks_reselects_timers():  # mutable_state_task_refresher.go:278-365 (RefreshTasks)
+    # activity A (ScheduleToStart 100 s) gets its timer task in batch 3; activity B (10 s, scheduled
+    # later) gets the next one in batch 4, so both carry a mask after replay.  RefreshTasks clears
+    # every mask and re-creates only the earliest timer of the sequence: B's.
+    b = [[ev(ET.WorkflowExecutionStarted, 1), ev(ET.DecisionTaskScheduled, 2)],
+         [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+         [ev(ET.DecisionTaskCompleted, 4, started_event_id=3),
+          ev(ET.ActivityTaskScheduled, 5, activity_id="A", schedule_to_start_timeout_seconds=100,
+             schedule_to_close_timeout_seconds=1000),
+          ev(ET.TimerStarted, 6, timer_id="t-late", start_to_fire_timeout_seconds=500),
+          ev(ET.DecisionTaskScheduled, 7)],
+         [ev(ET.DecisionTaskStarted, 8, scheduled_event_id=7)],
+         [ev(ET.DecisionTaskCompleted, 9, started_event_id=8),
+          ev(ET.ActivityTaskScheduled, 10, activity_id="B", schedule_to_start_timeout_seconds=10,
+             schedule_to_close_timeout_seconds=1000),
+          ev(ET.TimerStarted, 11, timer_id="t-early", start_to_fire_timeout_seconds=20)]]
+    h = WorkflowHistory(batches=b)
+    plain = oracle.replay(flatten([h]), 1)
+    act = plain.live_rows(flatten([h]), 0)["act"]
+    assert [int(a["timer_task_status"]) for a in act] == [abi.TTS_SCHEDULE_TO_START, abi.TTS_SCHEDULE_TO_START]
+    tim = plain.live_rows(flatten([h]), 0)["timer"]
+    assert [int(t["task_status"]) for t in tim] == [1, 1]
+    h.refresh_tasks = True
+    bt = flatten([h])
+    r = oracle.replay(bt, 1)
+    live = r.live_rows(bt, 0)
+    assert [int(a["timer_task_status"]) for a in live["act"]] == [0, abi.TTS_SCHEDULE_TO_START]
+    assert [int(t["task_status"]) for t in live["timer"]] == [0, 1]
+    assert r.exec[0]["checksum"] == plain.exec[0]["checksum"]   # the checksum does not cover timer masks

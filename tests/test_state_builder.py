@@ -55,6 +55,21 @@ def test_rebuild(engine):  # state_rebuilder_test.go:224-333 TestRebuild
     assert info.signal_count == 1 and ms.get_next_event_id() == 3
 
 
+def test_rebuild_refreshes_timer_tasks(engine):  # state_rebuilder.go:183 RefreshTasks
+    batches = [[ev(ET.WorkflowExecutionStarted, 1), ev(ET.DecisionTaskScheduled, 2)],
+               [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+               [ev(ET.DecisionTaskCompleted, 4, started_event_id=3),
+                ev(ET.ActivityTaskScheduled, 5, activity_id="A", schedule_to_start_timeout_seconds=100,
+                   schedule_to_close_timeout_seconds=1000), ev(ET.DecisionTaskScheduled, 6)],
+               [ev(ET.DecisionTaskStarted, 7, scheduled_event_id=6)],
+               [ev(ET.DecisionTaskCompleted, 8, started_event_id=7),
+                ev(ET.ActivityTaskScheduled, 9, activity_id="B", schedule_to_start_timeout_seconds=10,
+                   schedule_to_close_timeout_seconds=1000)]]
+    ms, _ = rebuild(batches, b"tok", 9, 12, "req", batch_builder=BatchStateBuilder(engine))
+    status = {a.activity_id: a.timer_task_status for a in ms.get_pending_activity_infos().values()}
+    assert status == {"A": 0, "B": abi.TTS_SCHEDULE_TO_START}
+
+
 def test_rebuild_to_middle_of_batch_rejected(engine):  # state_rebuilder.go:160-176
     batches = [[ev(ET.WorkflowExecutionStarted, 1), ev(ET.DecisionTaskScheduled, 2)]]
     with pytest.raises(BadRequestError):

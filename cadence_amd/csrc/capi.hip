@@ -10,16 +10,14 @@ namespace crr {
 template <bool WAVE_TAIL> __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
 template <bool WAVE_TAIL> __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
-__global__ void replay_wave_big_kernel(crr_inputs in, crr_outputs out, int phase);
-__global__ void replay_wave_hbm_kernel(crr_inputs in, crr_outputs out, int phase);
+__global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
 }
 
 namespace {
 
 constexpr int kBlock = 256;
-constexpr unsigned kRetryGrid = 512;
-constexpr unsigned kBigGrid = 1024;   // 2 blocks (waves) per CU x 256 CUs, twice over
+constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 57 KB LDS arena each) per CU x 256 CUs
 
 struct Timing {
   // [0,1] phase 0, [2,3] phase 1, [4,5] the phase-1 fast-path kernel alone
@@ -108,9 +106,8 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
     if (in->stride == 64) {
-      // fast path (LDS-held tables), then the general path for the workflows it handed back
-      hipError_t err = hipMemsetAsync(out->scratch, 0, 2 * sizeof(uint32_t), s);
-      if (err != hipSuccess) return (int)err;
+      // fast path (LDS-held tables), then one retry pass for the workflows it handed back; the
+      // scratch counters are zero on entry (zero-filled by the caller, reset by the retry pass)
       const bool tail = n_lane < in->n_wf;
       const bool small = (in->flags & CRR_IN_LDS_SMALL) != 0;
       if (timed && phase == 1) (void)hipEventRecord(g_timing.ev[4], s);
@@ -124,18 +121,15 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         hipLaunchKernelGGL(crr::replay_lds_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
       else
         hipLaunchKernelGGL(crr::replay_lds_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
-      err = hipGetLastError();
+      hipError_t err = hipGetLastError();
       if (err != hipSuccess) return (int)err;
       if (timed && phase == 1) {
         (void)hipEventRecord(g_timing.ev[5], s);
         g_timing.valid[2] = true;
       }
       if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n++ + 1], s);
-      // the workflows it handed back: one wavefront each, big LDS arena, then HBM rows
-      const unsigned big_grid = in->n_wf < kBigGrid ? in->n_wf : kBigGrid;
-      hipLaunchKernelGGL(crr::replay_wave_big_kernel, dim3(big_grid), dim3(64), 0, s, *in, *out, phase);
-      const unsigned hbm_grid = (in->n_wf + 3) / 4 < kRetryGrid ? (in->n_wf + 3) / 4 : kRetryGrid;
-      hipLaunchKernelGGL(crr::replay_wave_hbm_kernel, dim3(hbm_grid), dim3(kBlock), 0, s, *in, *out, phase);
+      const unsigned retry_grid = in->n_wf < kRetryGrid ? in->n_wf : kRetryGrid;
+      hipLaunchKernelGGL(crr::replay_retry_kernel, dim3(retry_grid), dim3(64), 0, s, *in, *out, phase);
     } else {
       hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 0);
     }

@@ -1022,6 +1022,7 @@ struct WaveTables {
   ST S;
   i32 lane;
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
+  bool retried = false;
 
   __device__ __forceinline__ void init() { lane = (i32)(threadIdx.x & 63); }
 
@@ -1331,7 +1332,9 @@ struct WaveTables {
   __device__ __forceinline__ i64 sig_id(const Geo& G, i32 i) const {
     if constexpr (ST::kLds) return S.M->ids[ST::A + ST::T + ST::C + ST::R + i]; else return G.sig(i)->initiated_id;
   }
-  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) const {
+  // kList < 0: the caller replays the workflow again itself (replay_retry_kernel)
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) {
+    retried = true;
     if constexpr (ST::kList >= 0) {
       if (lane == 0) {
         const u32 k = atomicAdd(out.scratch + ST::kList, 1u);
@@ -1992,10 +1995,11 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
   }
 }
 
-// Retry passes, one wavefront per workflow (lane or tail workflows alike; per-workflow stride):
-//   list 0 -> replay_wave_big_kernel: one wave per block with a 57 KB LDS row arena (2 blocks/CU);
-//   list 1 -> replay_wave_hbm_kernel: tables in the workflow's HBM rows (no size limit).
-// Both grid-stride over their list; an empty list costs one load per block.
+// Retry pass, one wavefront per workflow (lane or tail workflows alike; per-workflow stride), over
+// the workflows the fast path handed back (scratch list 0): first with a 57 KB LDS row arena
+// (2 blocks/CU); a live set that outgrows it is replayed again at once over the workflow's own HBM
+// rows (no size limit).  Grid-strides over the list; an empty list costs one load per block.  The
+// last block to finish zeroes the list counter, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
 template <class ST>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
@@ -2011,29 +2015,30 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
   replay_body(in, out, w, wfp, G, T, S, crc_tables);
 }
-__global__ void __launch_bounds__(64) replay_wave_big_kernel(crr_inputs in, crr_outputs out, int phase) {
+__global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_outputs out, int phase) {
   __shared__ u32 crc_tables[8 * 256];
   __shared__ BigArena arena;
   const u32 n_items = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (n_items == 0) return;
+  if (n_items == 0) return;  // uniform: nothing was handed back, the counters are already zero
   build_crc_tables(crc_tables);
   for (u32 i = blockIdx.x; i < n_items; i += gridDim.x) {
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 0, i)]);
-    WaveTables<LdsRows<BigArena, 1>> T;
+    WaveTables<LdsRows<BigArena, -1>> T;
     T.S.M = &arena;
     replay_wave_item(in, out, phase, w, T, crc_tables);
+    if (T.retried) {
+      WaveTables<HbmRows> H;
+      replay_wave_item(in, out, phase, w, H, crc_tables);
+    }
   }
-}
-__global__ void __launch_bounds__(kBlock) replay_wave_hbm_kernel(crr_inputs in, crr_outputs out, int phase) {
-  __shared__ u32 crc_tables[8 * 256];
-  const u32 n_items = __hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (n_items == 0) return;
-  build_crc_tables(crc_tables);
-  const u32 wv = (u32)uniform32((i32)(threadIdx.x >> 6));
-  for (u32 i = blockIdx.x * kWavesPerBlock + wv; i < n_items; i += gridDim.x * kWavesPerBlock) {
-    const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
-    WaveTables<HbmRows> T;
-    replay_wave_item(in, out, phase, w, T, crc_tables);
+  // every block has read the count: the last one to finish resets it for the next launch
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const u32 done = atomicAdd(out.scratch + 2, 1u);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(out.scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out.scratch + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -357,7 +357,8 @@ typedef struct crr_outputs {
     crr_initiated_row*   sig;
     crr_vh_item*         vh;
     crr_reset_point_row* rp;
-    uint32_t*            scratch;   /* engine scratch: >= 2 * n_wf + 64 words, contents undefined */
+    uint32_t*            scratch;   /* engine scratch: >= 2 * n_wf + 64 words, zero-filled before the
+                                       first call that uses it; every call leaves its counters zeroed */
 } crr_outputs;
 
 /* ---- entry points ----------------------------------------------------------------------------- */

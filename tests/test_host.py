@@ -136,3 +136,16 @@ def test_digest_numpy_matches_torch():
     rows["inconsistencies"] = [0, 1, 0, 2, 0]
     raw = torch.from_numpy(rows.view(np.uint8).copy())
     assert (dist.digest_torch(torch, raw, 5).numpy() == dist.digest_numpy(rows)).all()
+
+
+HOST_LIB = os.path.join(ROOT, "cadence_amd", "libcadence_host.so")
+
+
+@pytest.mark.skipif(not os.path.exists(HOST_LIB), reason="host library not built")
+def test_host_library_exports_every_decode_symbol():
+    txt = open(os.path.join(ROOT, "include", "cadence_decode.h")).read()
+    syms = sorted(set(re.findall(r"^\w[\w\s\*]*?\b(crr_\w+)\s*\(", txt, re.M)))
+    assert {"crr_decode_histories", "crr_decoded_get_view", "crr_decoded_free"} <= set(syms)
+    lib = ctypes.CDLL(HOST_LIB)
+    for s in syms:
+        assert hasattr(lib, s), s

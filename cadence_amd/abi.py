@@ -132,6 +132,11 @@ class Status(enum.IntEnum):
     TIMER_SEQUENCE = 14
     REBUILD_LAST_ITEM = 15
     NEW_RUN_MISSING = 16
+    NDC_NO_LCA = 20
+    NDC_LCA_NOT_IN_BRANCH = 21
+    NDC_FIRST_ITEM_MISMATCH = 22
+    NDC_RETRY_TASK = 23
+    NDC_BAD_INDEX = 24
     CAPACITY = 100
 
 
@@ -211,8 +216,19 @@ VH_ITEM = np.dtype([("event_id", "<i8"), ("version", "<i8")])
 
 RESET_POINT_ROW = np.dtype([("src", "<i4"), ("prev_index", "<i4"), ("key", "<u4"), ("flags", "<u4")])
 
+# NDC branch decisions (crr_ndc_prepare)
+NDC_TASK = np.dtype([("branch_begin", "<u4"), ("branch_count", "<u4"), ("current_index", "<i4"),
+                     ("incoming_begin", "<u4"), ("incoming_count", "<u4"), ("out_begin", "<u4"),
+                     ("first_event_id", "<i8"), ("first_event_version", "<i8")])
+NDC_BRANCH = np.dtype([("item_begin", "<u4"), ("item_count", "<u4")])
+NDC_RESULT = np.dtype([("status", "<i4"), ("action", "<i4"), ("branch_index", "<i4"), ("lca_branch", "<i4"),
+                       ("lca_event_id", "<i8"), ("lca_version", "<i8"), ("last_event_id", "<i8"),
+                       ("last_version", "<i8"), ("new_current_index", "<i4"), ("new_item_count", "<i4"),
+                       ("is_rebuilt", "<i4"), ("branch_changed", "<i4")])
+NDC_APPEND, NDC_NEW_BRANCH, NDC_DUPLICATE = 0, 1, 2
+
 SIZEOF_ORDER = [WORKFLOW, EXEC_ROW, ACTIVITY_ROW, TIMER_ROW, CHILD_ROW, INITIATED_ROW, VH_ITEM,
-                RESET_POINT_ROW, ACTIVITY_SIDE, START_SIDE]
+                RESET_POINT_ROW, ACTIVITY_SIDE, START_SIDE, NDC_TASK, NDC_RESULT]
 
 # (name, dtype, numpy kind) of the event columns, in crr_events order
 EVENT_COLUMNS = [("etype", np.uint8), ("event_id", np.int64), ("version", np.int64),
@@ -231,6 +247,11 @@ TABLES = [("act", ACTIVITY_ROW, "act_base", "act_cap", "n_activity"),
 
 
 # ---- ctypes structs -----------------------------------------------------------------------------------
+class CNdcInputs(ctypes.Structure):
+    _fields_ = [("tasks", ctypes.c_void_p), ("branches", ctypes.c_void_p), ("items", ctypes.c_void_p),
+                ("n_tasks", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 class CEvents(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name, _ in EVENT_COLUMNS]
 

@@ -86,6 +86,8 @@ size_t crr_sizeof(int which) {
     case 7: return sizeof(crr_reset_point_row);
     case 8: return sizeof(crr_activity_side);
     case 9: return sizeof(crr_start_side);
+    case 10: return sizeof(crr_ndc_task);
+    case 11: return sizeof(crr_ndc_result);
     default: return 0;
   }
 }

@@ -44,6 +44,8 @@ def lib():
         L.crr_crc32_ieee.restype = ctypes.c_uint32
         L.crr_last_kernel_ms.argtypes = [ctypes.c_int]
         L.crr_last_kernel_ms.restype = ctypes.c_float
+        L.crr_ndc_prepare.argtypes = [vp, vp, vp, vp]
+        L.crr_ndc_prepare.restype = ctypes.c_int
         L.crr_timing_begin.restype = ctypes.c_int
         L.crr_timing_read.argtypes = [vp, ctypes.c_int]
         L.crr_timing_read.restype = ctypes.c_int

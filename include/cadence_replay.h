@@ -161,6 +161,12 @@ enum crr_status_code {
     CRR_ERR_TIMER_SEQUENCE = 14,          /* InternalService  timer_sequence.go:141-145,176-180    */
     CRR_ERR_REBUILD_LAST_ITEM = 15,       /* BadRequest       state_rebuilder.go:160-176           */
     CRR_ERR_NEW_RUN_MISSING = 16,         /* engine: CAN new-run workflow index out of range       */
+    /* NDC branch decisions (crr_ndc_prepare) */
+    CRR_ERR_NDC_NO_LCA = 20,              /* BadRequest       versionHistory.go:270-272 "No joint point found" */
+    CRR_ERR_NDC_LCA_NOT_IN_BRANCH = 21,   /* BadRequest       versionHistory.go:147-149 DuplicateUntilLCAItem  */
+    CRR_ERR_NDC_FIRST_ITEM_MISMATCH = 22, /* BadRequest       versionHistory.go:474-476 AddVersionHistory      */
+    CRR_ERR_NDC_RETRY_TASK = 23,          /* RetryTaskV2Error ndc/branch_manager.go:214-225 out-of-order batch */
+    CRR_ERR_NDC_BAD_INDEX = 24,           /* BadRequest       versionHistory.go:442-444 invalid branch index   */
     CRR_ERR_CAPACITY = 100                /* engine: a slot table was sized too small by the host  */
 };
 
@@ -361,6 +367,51 @@ typedef struct crr_outputs {
                                        first call that uses it; every call leaves its counters zeroed */
 } crr_outputs;
 
+/* ---- NDC branch decisions ------------------------------------------------------
+ * branchManagerImpl.prepareVersionHistory (service/history/ndc/branch_manager.go:87-149) for a batch
+ * of replication tasks: FindLCAVersionHistoryIndexAndItem (versionHistory.go:501-528) over the local
+ * VersionHistories, IsLCAAppendable (:275-287), DuplicateUntilLCAItem (:142-172), verifyEventsOrder
+ * (branch_manager.go:199-225), AddVersionHistory (:450-498) for a new branch, plus IsRebuilt
+ * (:545-571).  The buffered-events flush (:169-196) and ForkHistoryBranch (the new branch token)
+ * stay on the host: the result names the base branch and fork point (lca_event_id + 1). */
+typedef struct crr_ndc_task {
+    uint32_t branch_begin;        /* local VersionHistories = branches[branch_begin, +branch_count) */
+    uint32_t branch_count;
+    int32_t  current_index;       /* VersionHistories.CurrentVersionHistoryIndex */
+    uint32_t incoming_begin;      /* incoming VersionHistory = items[incoming_begin, +incoming_count) */
+    uint32_t incoming_count;
+    uint32_t out_begin;           /* new-branch items go to out_items[out_begin...] (room: the longest local branch) */
+    int64_t  first_event_id;      /* the task's first event (ID, version) */
+    int64_t  first_event_version;
+} crr_ndc_task;
+
+typedef struct crr_ndc_branch { uint32_t item_begin, item_count; } crr_ndc_branch;
+
+typedef struct crr_ndc_inputs {
+    const crr_ndc_task*   tasks;
+    const crr_ndc_branch* branches;
+    const crr_vh_item*    items;
+    uint32_t              n_tasks;
+    uint32_t              reserved;
+} crr_ndc_inputs;
+
+#define CRR_NDC_APPEND     0   /* doContinue, append to local branch `branch_index` */
+#define CRR_NDC_NEW_BRANCH 1   /* doContinue on a new branch (index `branch_index`) forked from `lca_branch` */
+#define CRR_NDC_DUPLICATE  2   /* !doContinue, no error: the batch was already applied */
+
+typedef struct crr_ndc_result {
+    int32_t status;               /* crr_status_code (CRR_OK or the error prepareVersionHistory returns) */
+    int32_t action;               /* CRR_NDC_* (CRR_NDC_DUPLICATE, i.e. !doContinue, when status != CRR_OK) */
+    int32_t branch_index;         /* branch the batch applies to */
+    int32_t lca_branch;           /* branch holding the LCA (FindLCAVersionHistoryIndexAndItem) */
+    int64_t lca_event_id, lca_version;
+    int64_t last_event_id, last_version;   /* last item of the branch the order check used (RetryTaskV2 hint) */
+    int32_t new_current_index;    /* CurrentVersionHistoryIndex after AddVersionHistory */
+    int32_t new_item_count;       /* items of the new branch (DuplicateUntilLCAItem) at out_items[out_begin] */
+    int32_t is_rebuilt;           /* IsRebuilt() of the local histories */
+    int32_t branch_changed;       /* AddVersionHistory switched the current branch */
+} crr_ndc_result;
+
 /* ---- entry points ----------------------------------------------------------------------------- */
 /* All pointers in crr_inputs / crr_outputs are DEVICE pointers (HBM resident).  `stream` is a
  * hipStream_t (NULL: default stream).  Returns 0 on successful launch, a negative value on an
@@ -381,13 +432,17 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream);
  * mutable_state_builder.go:334-348 -> checksum.go:45-54).  Writes checksums[n_wf]. */
 int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksums, void* stream);
 
+/* Batched prepareVersionHistory over device arrays (one result per task). */
+int crr_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* results, crr_vh_item* out_items, void* stream);
+
 /* Select the HIP device for subsequent calls from this thread. */
 int crr_set_device(int device);
 
 /* Library / ABI version; struct sizes for binding-time layout checks. */
 int crr_abi_version(void);
 size_t crr_sizeof(int which);   /* 0 workflow, 1 exec row, 2 activity, 3 timer, 4 child, 5 initiated,
-                                   6 vh item, 7 reset point, 8 activity side, 9 start side */
+                                   6 vh item, 7 reset point, 8 activity side, 9 start side,
+                                   10 ndc task, 11 ndc result */
 
 /* Host-side CRC32-IEEE (hash/crc32.ChecksumIEEE) used by the shim's standalone verify. */
 uint32_t crr_crc32_ieee(const uint8_t* data, size_t len);

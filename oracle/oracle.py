@@ -43,6 +43,8 @@ def lib():
         L.oracle_update_state.restype = ctypes.c_int
         L.oracle_activity_timer_sequence.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int]
         L.oracle_activity_timer_sequence.restype = ctypes.c_int
+        L.oracle_ndc_prepare.argtypes = [vp, vp, vp]
+        L.oracle_ndc_prepare.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -150,3 +152,18 @@ def activity_timer_sequence(rows: np.ndarray):
     cr = np.zeros(cap, np.int32)
     n = lib().oracle_activity_timer_sequence(_ptr(rows), len(rows), _ptr(ts), _ptr(eid), _ptr(ty), _ptr(cr), cap)
     return [(int(ts[i]), int(eid[i]), int(ty[i]), bool(cr[i])) for i in range(n)]
+
+
+def ndc_prepare(batch):
+    """prepareVersionHistory for every task of a cadence_amd.ndc.NdcBatch (host); (results, out_items)."""
+    n = len(batch.tasks)
+    tasks = np.ascontiguousarray(batch.tasks)
+    branches = np.ascontiguousarray(batch.branches)
+    items = np.ascontiguousarray(batch.items)
+    ci = abi.CNdcInputs()
+    ci.tasks, ci.branches, ci.items = tasks.ctypes.data, branches.ctypes.data, items.ctypes.data
+    ci.n_tasks = n
+    res = np.zeros(max(n, 1), abi.NDC_RESULT)
+    out = np.zeros(batch.n_out_items, abi.VH_ITEM)
+    lib().oracle_ndc_prepare(ctypes.byref(ci), _ptr(res), _ptr(out))
+    return res[:n], out

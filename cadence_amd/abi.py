@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1
@@ -155,6 +155,7 @@ WF_FLAG_REFRESH_TASKS = 2      # Rebuild's RefreshTasks state effects after the 
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4
+IN_EMIT_TASKS = 8
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([
@@ -165,7 +166,7 @@ ACTIVITY_SIDE = np.dtype([
 START_SIDE = np.dtype([
     ("decision_start_to_close", "<i4"), ("workflow_timeout", "<i4"), ("first_decision_backoff", "<i4"),
     ("initiator", "<i4"), ("parent_domain_status", "<i4"), ("prev_reset_key_off", "<u4"),
-    ("prev_reset_count", "<i4"), ("reserved", "<i4")])
+    ("prev_reset_count", "<i4"), ("attempt", "<i4"), ("expiration_ns", "<i8"), ("reserved", "<i8")])
 
 WORKFLOW = np.dtype([
     ("ev_begin", "<i8"), ("ev_count", "<i4"), ("empty_batch_at", "<i4"),
@@ -177,7 +178,7 @@ WORKFLOW = np.dtype([
     ("sig_base", "<i8"), ("vh_base", "<i8"), ("rp_base", "<i8"),
     ("act_cap", "<i4"), ("timer_cap", "<i4"), ("child_cap", "<i4"), ("rc_cap", "<i4"),
     ("sig_cap", "<i4"), ("vh_cap", "<i4"), ("rp_cap", "<i4"), ("flags", "<i4"),
-    ("reserved", "<i8")])
+    ("task_base", "<i8"), ("task_cap", "<i4"), ("retention_days", "<i4")])
 
 EXEC_ROW = np.dtype([
     ("status", "<i4"), ("fail_step", "<i4"), ("inconsistencies", "<i4"), ("flags", "<u4"),
@@ -190,7 +191,7 @@ EXEC_ROW = np.dtype([
     ("decision_request_src", "<i4"), ("start_src", "<i4"),
     ("n_activity", "<i4"), ("n_timer", "<i4"), ("n_child", "<i4"), ("n_rc", "<i4"), ("n_signal", "<i4"),
     ("n_vh_items", "<i4"), ("n_reset_points", "<i4"), ("token_src", "<i4"),
-    ("checksum", "<u4"), ("payload_len", "<u4"), ("reserved", "<i4", (2,))])
+    ("checksum", "<u4"), ("payload_len", "<u4"), ("n_tasks", "<i4"), ("reserved", "<i4")])
 
 ACTIVITY_ROW = np.dtype([
     ("schedule_id", "<i8"), ("version", "<i8"), ("scheduled_batch_id", "<i8"), ("scheduled_time", "<i8"),
@@ -216,6 +217,30 @@ VH_ITEM = np.dtype([("event_id", "<i8"), ("version", "<i8")])
 
 RESET_POINT_ROW = np.dtype([("src", "<i4"), ("prev_index", "<i4"), ("key", "<u4"), ("flags", "<u4")])
 
+TASK_ROW = np.dtype([("kind", "<i4"), ("aux", "<i4"), ("version", "<i8"), ("visibility_ts", "<i8"),
+                     ("event_id", "<i8"), ("attempt", "<i4"), ("src", "<i4")])
+
+
+class TaskKind(enum.IntEnum):
+    """crr_task_kind (transfer / timer tasks ApplyEvents generates)."""
+    RecordWorkflowStarted = 1
+    Decision = 2
+    Activity = 3
+    StartChild = 4
+    CancelExecution = 5
+    SignalExecution = 6
+    UpsertSearchAttributes = 7
+    CloseExecution = 8
+    WorkflowTimeout = 16
+    WorkflowBackoff = 17
+    DecisionTimeout = 18
+    ActivityTimeout = 19
+    UserTimer = 20
+    DeleteHistory = 21
+
+
+BACKOFF_RETRY, BACKOFF_CRON = 0, 1
+
 # NDC branch decisions (crr_ndc_prepare)
 NDC_TASK = np.dtype([("branch_begin", "<u4"), ("branch_count", "<u4"), ("current_index", "<i4"),
                      ("incoming_begin", "<u4"), ("incoming_count", "<u4"), ("out_begin", "<u4"),
@@ -228,7 +253,7 @@ NDC_RESULT = np.dtype([("status", "<i4"), ("action", "<i4"), ("branch_index", "<
 NDC_APPEND, NDC_NEW_BRANCH, NDC_DUPLICATE = 0, 1, 2
 
 SIZEOF_ORDER = [WORKFLOW, EXEC_ROW, ACTIVITY_ROW, TIMER_ROW, CHILD_ROW, INITIATED_ROW, VH_ITEM,
-                RESET_POINT_ROW, ACTIVITY_SIDE, START_SIDE, NDC_TASK, NDC_RESULT]
+                RESET_POINT_ROW, ACTIVITY_SIDE, START_SIDE, NDC_TASK, NDC_RESULT, TASK_ROW]
 
 # (name, dtype, numpy kind) of the event columns, in crr_events order
 EVENT_COLUMNS = [("etype", np.uint8), ("event_id", np.int64), ("version", np.int64),
@@ -243,7 +268,8 @@ TABLES = [("act", ACTIVITY_ROW, "act_base", "act_cap", "n_activity"),
           ("rc", INITIATED_ROW, "rc_base", "rc_cap", "n_rc"),
           ("sig", INITIATED_ROW, "sig_base", "sig_cap", "n_signal"),
           ("vh", VH_ITEM, "vh_base", "vh_cap", "n_vh_items"),
-          ("rp", RESET_POINT_ROW, "rp_base", "rp_cap", "n_reset_points")]
+          ("rp", RESET_POINT_ROW, "rp_base", "rp_cap", "n_reset_points"),
+          ("tasks", TASK_ROW, "task_base", "task_cap", "n_tasks")]   # written with IN_EMIT_TASKS only
 
 
 # ---- ctypes structs -----------------------------------------------------------------------------------

@@ -7,8 +7,8 @@
 #include "cadence_replay.h"
 
 namespace crr {
-template <bool WAVE_TAIL> __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
-template <bool WAVE_TAIL> __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
+template <bool WAVE_TAIL, bool EMIT> __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
+template <bool WAVE_TAIL, bool EMIT> __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
@@ -61,6 +61,7 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!e.etype || !e.event_id || !e.version || !e.timestamp || !e.task_id || !e.ref || !e.key || !e.aux) return false;
   if (!in->act_side || !in->start_side || !in->reset_keys || !in->arena) return false;
   if (!out->act || !out->timer || !out->child || !out->rc || !out->sig || !out->vh || !out->rp) return false;
+  if ((in->flags & CRR_IN_EMIT_TASKS) && !out->tasks) return false;
   if (in->stride == 64 && !out->scratch) return false;
   if (in->flags & CRR_IN_WAVE_TAIL) {
     if (in->stride != 64 || in->wave_begin > in->n_wf) return false;
@@ -88,6 +89,7 @@ size_t crr_sizeof(int which) {
     case 9: return sizeof(crr_start_side);
     case 10: return sizeof(crr_ndc_task);
     case 11: return sizeof(crr_ndc_result);
+    case 12: return sizeof(crr_task_row);
     default: return 0;
   }
 }
@@ -115,14 +117,20 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (timed && phase == 1) (void)hipEventRecord(g_timing.ev[4], s);
       const bool ring = phase == 1 && g_ring.on && g_ring.n < kRing;
       if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n], s);
-      if (small && tail)
-        hipLaunchKernelGGL(crr::replay_lds_small_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
-      else if (small)
-        hipLaunchKernelGGL(crr::replay_lds_small_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
-      else if (tail)
-        hipLaunchKernelGGL(crr::replay_lds_kernel<true>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
-      else
-        hipLaunchKernelGGL(crr::replay_lds_kernel<false>, dim3(lds_grid), dim3(kBlock), 0, s, *in, *out, phase);
+      // task emission is a separate instantiation: the plain replay loop carries none of its registers
+      const bool emit = (in->flags & CRR_IN_EMIT_TASKS) != 0;
+      const dim3 g(lds_grid), b(kBlock);
+      if (emit) {
+        if (small && tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, true>), g, b, 0, s, *in, *out, phase);
+        else if (small) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, true>), g, b, 0, s, *in, *out, phase);
+        else if (tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, true>), g, b, 0, s, *in, *out, phase);
+        else hipLaunchKernelGGL((crr::replay_lds_kernel<false, true>), g, b, 0, s, *in, *out, phase);
+      } else {
+        if (small && tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, false>), g, b, 0, s, *in, *out, phase);
+        else if (small) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, false>), g, b, 0, s, *in, *out, phase);
+        else if (tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, false>), g, b, 0, s, *in, *out, phase);
+        else hipLaunchKernelGGL((crr::replay_lds_kernel<false, false>), g, b, 0, s, *in, *out, phase);
+      }
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return (int)err;
       if (timed && phase == 1) {

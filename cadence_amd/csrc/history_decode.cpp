@@ -118,7 +118,8 @@ struct Attr {
   // ActivityTaskScheduled
   i32 s2s = 0, s2c = 0, st2c = 0, hb = 0, has_retry = 0, expiration = 0;
   // WorkflowExecutionStarted
-  i32 task_s2c = 0, exec_s2c = 0, backoff = 0, initiator = CRR_INITIATOR_NIL;
+  i32 task_s2c = 0, exec_s2c = 0, backoff = 0, initiator = CRR_INITIATOR_NIL, attempt = 0;
+  i64 expiration_ts = 0;
   int prev_mode = -1;        // -1: PrevAutoResetPoints nil, -2: Points nil, 0: list
   std::vector<std::string> prev;
 };
@@ -191,6 +192,8 @@ void read_attributes(Reader& r, int t, Attr& a) {
         else if (id == 40 && ft == T_I32) a.exec_s2c = r.be32();                  // ExecutionStartToCloseTimeoutSeconds
         else if (id == 50 && ft == T_I32) a.task_s2c = r.be32();                  // TaskStartToCloseTimeoutSeconds
         else if (id == 55 && ft == T_I32) a.initiator = r.be32();                 // Initiator
+        else if (id == 80 && ft == T_I32) a.attempt = r.be32();                   // Attempt
+        else if (id == 90 && ft == T_I64) a.expiration_ts = r.be64();             // ExpirationTimestamp
         else if (id == 110 && ft == T_I32) a.backoff = r.be32();                  // FirstDecisionTaskBackoffSeconds
         else if (id == 130 && ft == T_STRUCT) read_reset_points(r, a);            // PrevAutoResetPoints
         else used = false;
@@ -325,6 +328,14 @@ void read_event(Reader& r, Event& e) {
   }
 }
 
+// tasks the task generator adds per event type (state_builder.go:157-625), an upper bound
+constexpr int8_t kTasksPerEvent[CRR_EV_TYPE_COUNT] = {
+    3, 2, 2, 2, 1, 1, 0, 1, 1, 1,   // 0 Started(+backoff) 1-3 closes 4 DTSched 5 DTStarted 6 DTCompleted 7-8 DT fail 9 ATSched
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0,   // 10-19
+    0, 0, 2, 1, 0, 0, 0, 0, 2, 2,   // 22 Canceled 23 RCInitiated 28 Terminated 29 ContinuedAsNew
+    1, 0, 0, 0, 0, 0, 0, 0, 1, 0,   // 30 StartChildInitiated 38 SignalInitiated
+    0, 1};                          // 41 Upsert
+
 // ---- per-chunk output --------------------------------------------------------------------------------
 struct Chunk {
   std::vector<uint8_t> etype;
@@ -387,6 +398,7 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
   i32 empty_at = -1;
   i64 n_act = 0, n_timer = 0, n_child = 0, n_rc = 0, n_sig = 0, n_dtc = 0, n_started = 0, vh_items = 0;
   i64 max_prev = 0;
+  i64 n_tasks = 0;  // upper bound of the tasks ApplyEvents generates (flatten.TASKS_PER_EVENT)
   bool have_ver = false;
   i64 last_ver = 0;
   Event e;
@@ -421,6 +433,7 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
           k.ts.push_back(e.ts);
           k.task.push_back(e.task);
           if (!have_ver || e.ver > last_ver) { ++vh_items; last_ver = e.ver; have_ver = true; }
+          n_tasks += valid ? kTasksPerEvent[t] : 0;
           i64 ref = 0;
           u32 key = 0;
           i32 aux = 0;
@@ -442,6 +455,8 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
               ss.workflow_timeout = a.exec_s2c;
               ss.first_decision_backoff = a.backoff;
               ss.initiator = a.initiator;
+              ss.attempt = a.attempt;
+              ss.expiration_ns = a.expiration_ts;
               // ParentWorkflowDomainID is not on the thrift wire: the name lookup (state_builder.go:137-147)
               ss.parent_domain_status = domain_status(c, a.domain);
               k.start.push_back(ss);
@@ -499,6 +514,7 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
       if (empty_at < 0) empty_at = (i32)(batch_begin - begin);
       continue;
     }
+    n_tasks += 2;  // the batch's timer epilogue
     k.etype[batch_begin] |= CRR_ETYPE_BATCH_FIRST;
     k.etype.back() |= CRR_ETYPE_BATCH_LAST;
   }
@@ -527,6 +543,8 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
   d.rc_cap = (i32)n_rc; d.sig_cap = (i32)n_sig; d.vh_cap = (i32)vh_items;
   d.rp_cap = (i32)(max_prev * std::max<i64>(1, n_started) + n_dtc);
   d.flags = src.flags;
+  d.task_cap = (i32)n_tasks;
+  d.retention_days = src.retention_days;
   k.wf.push_back(d);
 }
 
@@ -547,7 +565,7 @@ void append(std::vector<T>& dst, const std::vector<T>& src) { dst.insert(dst.end
 
 struct crr_decoded {
   Chunk all;
-  uint64_t table_rows[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t table_rows[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 extern "C" {
@@ -612,16 +630,17 @@ crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* b
     Chunk().etype.swap(k.etype);  // release chunk memory early
   }
   // canonical slot-table bases: prefix sums of the per-workflow capacities
-  int64_t base[7] = {0, 0, 0, 0, 0, 0, 0};
+  int64_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (auto& d : a.wf) {
-    const i32 caps[7] = {d.act_cap, d.timer_cap, d.child_cap, d.rc_cap, d.sig_cap, d.vh_cap, d.rp_cap};
-    int64_t* bases[7] = {&d.act_base, &d.timer_base, &d.child_base, &d.rc_base, &d.sig_base, &d.vh_base, &d.rp_base};
-    for (int j = 0; j < 7; ++j) {
+    const i32 caps[8] = {d.act_cap, d.timer_cap, d.child_cap, d.rc_cap, d.sig_cap, d.vh_cap, d.rp_cap, d.task_cap};
+    int64_t* bases[8] = {&d.act_base, &d.timer_base, &d.child_base, &d.rc_base, &d.sig_base, &d.vh_base, &d.rp_base,
+                         &d.task_base};
+    for (int j = 0; j < 8; ++j) {
       *bases[j] = base[j];
       base[j] += std::max(caps[j], 0);
     }
   }
-  for (int j = 0; j < 7; ++j) out->table_rows[j] = (uint64_t)base[j];
+  for (int j = 0; j < 8; ++j) out->table_rows[j] = (uint64_t)base[j];
   return out;
 }
 
@@ -642,7 +661,7 @@ int crr_decoded_get_view(const crr_decoded* d, crr_decoded_view* v) {
   v->reset_keys = a.reset_keys.data(); v->n_reset_keys = a.reset_keys.size();
   v->arena = a.arena.data(); v->n_arena = a.arena.size();
   v->wf = a.wf.data(); v->n_wf = (uint32_t)a.wf.size();
-  for (int j = 0; j < 7; ++j) v->table_rows[j] = d->table_rows[j];
+  for (int j = 0; j < 8; ++j) v->table_rows[j] = d->table_rows[j];
   v->key_off = a.key_off.data();
   v->key_len = a.key_len.data();
   v->key_arena = a.key_arena.data();

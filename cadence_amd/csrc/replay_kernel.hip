@@ -169,6 +169,8 @@ struct Lane {
   i32 n_act, n_timer, n_child, n_rc, n_sig, n_rp;
   i32 inconsistencies;
   i32 status, fail_step;
+  i32 n_tasks;                  // transfer / timer tasks generated (CRR_IN_EMIT_TASKS)
+  i64 expiration_ns;            // executionInfo.ExpirationTime (0: unset)
 };
 
 // Where this lane's output rows live in HBM: row(table, slot) = base + slot * stride.
@@ -177,7 +179,10 @@ struct Geo {
   i64 st;
   i64 act_base, timer_base, child_base, rc_base, sig_base, vh_base, rp_base;
   i32 act_cap, timer_cap, child_cap, rc_cap, sig_cap, vh_cap, rp_cap;
+  i64 task_base;
+  i32 task_cap;
   __device__ __forceinline__ crr_activity_row* act(i32 j) const { return out.act + act_base + (i64)j * st; }
+  __device__ __forceinline__ crr_task_row* task(i32 j) const { return out.tasks + task_base + (i64)j * st; }
   __device__ __forceinline__ crr_timer_row* timer(i32 j) const { return out.timer + timer_base + (i64)j * st; }
   __device__ __forceinline__ crr_child_row* child(i32 j) const { return out.child + child_base + (i64)j * st; }
   __device__ __forceinline__ crr_initiated_row* rc(i32 j) const { return out.rc + rc_base + (i64)j * st; }
@@ -193,6 +198,7 @@ __device__ __forceinline__ void load_geo(Geo& G, const crr_workflow* wfp, const 
   G.rc_base = wfp->rc_base; G.sig_base = wfp->sig_base; G.vh_base = wfp->vh_base; G.rp_base = wfp->rp_base;
   G.act_cap = wfp->act_cap; G.timer_cap = wfp->timer_cap; G.child_cap = wfp->child_cap; G.rc_cap = wfp->rc_cap;
   G.sig_cap = wfp->sig_cap; G.vh_cap = wfp->vh_cap; G.rp_cap = wfp->rp_cap;
+  G.task_base = wfp->task_base; G.task_cap = wfp->task_cap;
 }
 
 // Wave-interleaved layout: every base is group_base + lane and every capacity is the group's.
@@ -208,6 +214,8 @@ __device__ __forceinline__ void uniformize_geo(Geo& G, i64 lane) {
   G.act_cap = uniform32(G.act_cap); G.timer_cap = uniform32(G.timer_cap); G.child_cap = uniform32(G.child_cap);
   G.rc_cap = uniform32(G.rc_cap); G.sig_cap = uniform32(G.sig_cap); G.vh_cap = uniform32(G.vh_cap);
   G.rp_cap = uniform32(G.rp_cap);
+  G.task_base = uniform64(G.task_base - lane) + lane;
+  G.task_cap = uniform32(G.task_cap);
 }
 
 // UpdateWorkflowStateCloseStatus (common/persistence/workflowExecutionInfo.go:45-165).
@@ -265,13 +273,34 @@ __device__ __forceinline__ void update_decision(Lane& L, i64 ver, i64 sched, i64
 }
 
 // FailDecision(true) (:643-676) followed by ReplicateTransientDecisionTaskScheduled (:168-197)
-__device__ __forceinline__ void fail_decision_and_transient(Lane& L, i64 now_ns) {
+__device__ __forceinline__ bool fail_decision_and_transient(Lane& L, i64 now_ns) {
   update_decision(L, CRR_EMPTY_VERSION, CRR_EMPTY_EVENT_ID, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, 0,
                   L.decision_attempt + 1, 0, now_ns, 0);
-  if (L.decision_schedule_id == CRR_EMPTY_EVENT_ID && L.decision_attempt != 0)
+  if (L.decision_schedule_id == CRR_EMPTY_EVENT_ID && L.decision_attempt != 0) {
     update_decision(L, L.current_version, L.next_event_id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID,
                     L.decision_start_to_close, L.decision_attempt, 0, now_ns, 0);
+    return true;
+  }
+  return false;
 }
+
+// One transfer / timer task (crr_task_row) of the task generator, in the order Go adds them; the
+// wavefront-per-workflow path writes it from one lane.
+struct TaskSink {
+  bool on;      // CRR_IN_EMIT_TASKS (uniform)
+  bool writer;  // this lane writes the row
+  __device__ __forceinline__ void add(Lane& L, const Geo& G, i32 kind, i32 aux, i64 version, i64 vis, i64 event_id,
+                                      i32 attempt, i32 src) const {
+    if (!on) return;
+    if (writer && L.n_tasks < G.task_cap) {
+      crr_task_row r;
+      r.kind = kind; r.aux = aux; r.version = version; r.visibility_ts = vis; r.event_id = event_id;
+      r.attempt = attempt; r.src = src;
+      *G.task(L.n_tasks) = r;
+    }
+    ++L.n_tasks;
+  }
+};
 
 __device__ __forceinline__ bool seq_less(i64 ta, i64 ea, i32 ya, i64 tb, i64 eb, i32 yb) {
   if (ta != tb) return ta < tb;
@@ -475,7 +504,7 @@ struct GlobalTables {
     return false;
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
-  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
     if (L.n_act > 0) {
       BestTimer B;
       for (i32 j = 0; j < hw_act; ++j) {
@@ -489,17 +518,18 @@ struct GlobalTables {
         crr_activity_row* r = G.act(B.j);
         r->timer_task_status |= timer_mask(B.y);
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r->last_hb_timeout_vis_s = unix_seconds(B.t);
+        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);  // timer_sequence.go:190-196
       }
     }
-    epilogue_timers(L, G);
+    epilogue_timers(L, G, K);
   }
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
     for (i32 j = 0; j < hw_act; ++j) G.act(j)->timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
     for (i32 j = 0; j < hw_timer; ++j) G.timer(j)->task_status = CRR_TIMER_TASK_STATUS_NONE;
-    epilogue(L, G);
+    epilogue(L, G, TaskSink{false, false});
   }
-  __device__ __forceinline__ void epilogue_timers(Lane& L, const Geo& G) {
+  __device__ __forceinline__ void epilogue_timers(Lane& L, const Geo& G, const TaskSink& K) {
     if (L.n_timer > 0) {
       BestTimer B;
       for (i32 j = 0; j < hw_timer; ++j) {
@@ -507,9 +537,13 @@ struct GlobalTables {
         if (!(r->flags & CRR_ROW_LIVE)) continue;
         B.offer(r->expiry_time, r->started_id, 0, j, r->task_status == CRR_TIMER_TASK_STATUS_CREATED);
       }
-      if (B.have && !B.created) G.timer(B.j)->task_status = CRR_TIMER_TASK_STATUS_CREATED;
+      if (B.have && !B.created) {
+        G.timer(B.j)->task_status = CRR_TIMER_TASK_STATUS_CREATED;
+        K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);  // timer_sequence.go:151-156
+      }
     }
   }
+  __device__ __forceinline__ bool task_writer() const { return true; }
   template <class R, class IdOf>
   __device__ __forceinline__ static void compact_sort(R* (Geo::*row)(i32) const, const Geo& G, i32 hw, i32 n, IdOf id_of) {
     for (i32 i = 0; i < n; ++i) {
@@ -790,7 +824,7 @@ struct LdsTables {
       if (i < L.n_rp && (u32)M->p_row[i][t].z == key) hit = true;
     return hit;
   }
-  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
     if (L.n_act > 0) {
       BestTimer B;
 #pragma unroll
@@ -801,8 +835,10 @@ struct LdsTables {
         activity_candidates(B, j, M->a_sid[j][t], M->a_sched_t[j][t], (f & LF_STARTED) != 0, M->a_start_t[j][t],
                             to.x, to.y, to.z, to.w, f >> LF_TTS_SHIFT);
       }
-      if (B.have && !B.created)
+      if (B.have && !B.created) {
         M->a_fl[B.j][t] |= (timer_mask(B.y) << LF_TTS_SHIFT) | (B.y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
+        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
+      }
     }
     if (L.n_timer > 0) {
       BestTimer B;
@@ -812,9 +848,13 @@ struct LdsTables {
         if (!(f & CRR_ROW_LIVE)) continue;
         B.offer(M->t_exp[j][t], M->t_sid[j][t], 0, j, (f & TF_CREATED) != 0);
       }
-      if (B.have && !B.created) M->t_fl[B.j][t] |= TF_CREATED;
+      if (B.have && !B.created) {
+        M->t_fl[B.j][t] |= TF_CREATED;
+        K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
+      }
     }
   }
+  __device__ __forceinline__ bool task_writer() const { return true; }
 
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
@@ -822,7 +862,7 @@ struct LdsTables {
     for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] &= ~(0xFu << LF_TTS_SHIFT);
 #pragma unroll
     for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] &= ~TF_CREATED;
-    epilogue(L, G);
+    epilogue(L, G, TaskSink{false, false});
   }
 
   template <int N, class SwapFn>
@@ -1212,7 +1252,7 @@ struct WaveTables {
     B.created = uniform32(B.created) != 0;
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
-  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G) {
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
     if (L.n_act > 0) {
       BestTimer B;
       for (i32 j = lane; j < hw_act; j += 64) {
@@ -1228,6 +1268,7 @@ struct WaveTables {
         r.timer_task_status |= timer_mask(B.y);
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r.last_hb_timeout_vis_s = unix_seconds(B.t);
       }
+      if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
     }
     if (L.n_timer > 0) {
       BestTimer B;
@@ -1238,14 +1279,16 @@ struct WaveTables {
       }
       wave_min(B);
       if (B.have && !B.created && own(B.j)) S.timer(B.j).task_status = CRR_TIMER_TASK_STATUS_CREATED;
+      if (B.have && !B.created) K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
     }
   }
+  __device__ __forceinline__ bool task_writer() const { return lane == 0; }
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365); each lane clears the slots
   // the epilogue's candidate loop reads with the same lane, so no cross-lane ordering is needed
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
     for (i32 j = lane; j < hw_act; j += 64) S.act(j).timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
     for (i32 j = lane; j < hw_timer; j += 64) S.timer(j).task_status = CRR_TIMER_TASK_STATUS_NONE;
-    epilogue(L, G);
+    epilogue(L, G, TaskSink{false, false});
   }
 
   // LdsRows: live rows -> HBM slots 0..n-1 in event-ID order (rank = number of smaller live IDs);
@@ -1376,6 +1419,11 @@ constexpr u64 kAux = bit(CRR_EV_WORKFLOW_EXECUTION_STARTED) | bit(CRR_EV_DECISIO
                      bit(CRR_EV_ACTIVITY_TASK_SCHEDULED) | bit(CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED) |
                      bit(CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW) |
                      bit(CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED) | bit(CRR_EV_SIGNAL_EXTERNAL_INITIATED);
+// task emission also reads the start and close events' timestamps (workflow timeout, retention)
+constexpr u64 kTsTasks = bit(CRR_EV_WORKFLOW_EXECUTION_STARTED) | bit(CRR_EV_WORKFLOW_EXECUTION_COMPLETED) |
+                         bit(CRR_EV_WORKFLOW_EXECUTION_FAILED) | bit(CRR_EV_WORKFLOW_EXECUTION_TIMED_OUT) |
+                         bit(CRR_EV_WORKFLOW_EXECUTION_CANCELED) | bit(CRR_EV_WORKFLOW_EXECUTION_TERMINATED) |
+                         bit(CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW);
 __device__ __forceinline__ bool has(u64 mask, u32 et) { return (mask >> (et & CRR_ETYPE_MASK)) & 1ull; }
 }  // namespace need
 
@@ -1385,7 +1433,9 @@ struct LaneSource {
   i32 n;
   Ev nx;      // step s+1 (type and the columns it needs), in flight during step s
   u32 et_nx;  // type byte of step s+2, in flight during step s
-  __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count) : E(e), begin(b), st(stride), n(count) {}
+  u64 ts_mask;  // types whose timestamp is read (uniform)
+  __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count, bool tasks)
+      : E(e), begin(b), st(stride), n(count), ts_mask(need::kTs | (tasks ? need::kTsTasks : 0ull)) {}
   __device__ __forceinline__ i64 ix(i32 step) const { return begin + (i64)step * st; }
   __device__ __forceinline__ Ev load(i32 step, u32 et) const {
     Ev e;
@@ -1393,7 +1443,7 @@ struct LaneSource {
     e.et = et;
     e.id = E.event_id[i];
     e.ver = E.version[i];
-    e.ts = need::has(need::kTs, et) ? E.timestamp[i] : 0;
+    e.ts = need::has(ts_mask, et) ? E.timestamp[i] : 0;
     e.ref = need::has(need::kRef, et) ? E.ref[i] : 0;
     e.key = need::has(need::kKey, et) ? E.key[i] : 0u;
     e.aux = need::has(need::kAux, et) ? E.aux[i] : 0;
@@ -1518,12 +1568,20 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
 }
 
 // ---------------------------------------------------------------------------------------------------
+// GenerateWorkflowCloseTasks (task_generator.go:168-258): the close transfer task (its cross-cluster
+// shape is the host's, from cluster metadata) and DeleteHistoryEventTask at close + retention
+__device__ __forceinline__ void close_tasks(Lane& L, const Geo& G, const TaskSink& K, i64 ver, i64 ts, i32 s,
+                                            i32 retention_days) {
+  K.add(L, G, CRR_TASK_CLOSE_EXECUTION, 0, ver, 0, 0, 0, s);
+  K.add(L, G, CRR_TASK_DELETE_HISTORY, 0, ver, add_seconds(ts, (i64)retention_days * 86400), 0, 0, s);
+}
+
 // One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
 // code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
 template <class P>
 __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outputs& out, Lane& L, const Geo& G, P& T,
                                            const Ev& ev, const i32 s, const i32 t, const i64 batch_first_id,
-                                           const i64 now_ns) {
+                                           const i64 now_ns, const TaskSink& K, const i32 retention_days) {
   const i64 id = ev.id;
   const i64 ver = ev.ver;
 #define FAIL(code, step) return (code)
@@ -1557,22 +1615,38 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
           rp.flags = CRR_ROW_LIVE;
           CHECK(T.rp_push(L, G, rp));
         }
-        // GenerateDelayedDecisionTasks (mutable_state_task_generator.go:242-281)
-        if (ss.first_decision_backoff > 0 && ss.initiator != CRR_INITIATOR_NIL &&
-            ss.initiator != CRR_INITIATOR_RETRY_POLICY && ss.initiator != CRR_INITIATOR_CRON)
-          FAIL(CRR_ERR_BAD_INITIATOR, s);
+        if (ss.expiration_ns != 0) L.expiration_ns = ss.expiration_ns;  // (:1800-1802)
+        // GenerateRecordWorkflowStartedTasks / GenerateWorkflowStartTasks (task_generator.go:143-166, :301-313)
+        K.add(L, G, CRR_TASK_RECORD_WORKFLOW_STARTED, 0, ver, 0, 0, 0, s);
+        if (K.on) {
+          i64 vis = add_seconds(ev.ts, (i64)ss.workflow_timeout + (i64)ss.first_decision_backoff);
+          if (ss.attempt > 0 && L.expiration_ns != 0 && vis > L.expiration_ns) vis = L.expiration_ns;
+          K.add(L, G, CRR_TASK_WORKFLOW_TIMEOUT, 0, ver, vis, 0, 0, s);
+        }
+        // GenerateDelayedDecisionTasks (mutable_state_task_generator.go:260-299)
+        if (ss.first_decision_backoff > 0) {
+          if (ss.initiator != CRR_INITIATOR_NIL && ss.initiator != CRR_INITIATOR_RETRY_POLICY &&
+              ss.initiator != CRR_INITIATOR_CRON)
+            FAIL(CRR_ERR_BAD_INITIATOR, s);
+          K.add(L, G, CRR_TASK_WORKFLOW_BACKOFF, ss.initiator == CRR_INITIATOR_RETRY_POLICY ? CRR_BACKOFF_RETRY : CRR_BACKOFF_CRON,
+                ver, add_seconds(ev.ts, ss.first_decision_backoff), 0, 0, s);
+        }
         L.token_src = 1;  // SetHistoryTree(runID) (:367-376)
         break;
       }
       case CRR_EV_DECISION_TASK_SCHEDULED: {  // :185-208 -> decision_task_manager.go:129-166
         if (L.state != CRR_STATE_ZOMBIE) CHECK(update_state(L, CRR_STATE_RUNNING, CRR_CLOSE_NONE));
         update_decision(L, ver, id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, ev.aux, ev.ref, 0, ev.ts, ev.ts);
+        K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, s);  // GenerateDecisionScheduleTasks
         break;
       }
       case CRR_EV_DECISION_TASK_STARTED: {  // :210-228 -> decision_task_manager.go:199-242
         if (ev.ref != L.decision_schedule_id) FAIL(CRR_ERR_DECISION_NOT_FOUND, s);
         update_decision(L, ver, ev.ref, id, s, L.decision_timeout, 0, ev.ts, L.decision_scheduled_ts,
                         L.decision_orig_scheduled_ts);
+        // GenerateDecisionStartTasks (task_generator.go:352-388)
+        K.add(L, G, CRR_TASK_DECISION_TIMEOUT, CRR_TIMEOUT_START_TO_CLOSE, L.decision_version,
+              add_seconds(ev.ts, L.decision_timeout), L.decision_schedule_id, (i32)L.decision_attempt, s);
         break;
       }
       case CRR_EV_DECISION_TASK_COMPLETED: {  // :230-235 -> decision_task_manager.go:244-249, :827-838
@@ -1593,7 +1667,8 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
       }
       case CRR_EV_DECISION_TASK_TIMED_OUT:  // :237-259 (StickyTaskList == "": incrementAttempt)
       case CRR_EV_DECISION_TASK_FAILED:     // :261-281
-        fail_decision_and_transient(L, now_ns);
+        if (fail_decision_and_transient(L, now_ns))  // the transient decision's schedule task (task list of the start event)
+          K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, L.start_src);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
 #if CRR_EXP & 8
@@ -1622,6 +1697,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
         row.reserved[0] = row.reserved[1] = row.reserved[2] = 0;
         CHECK(T.act_insert(L, G, row));
+        K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks
         break;
       }
       case CRR_EV_ACTIVITY_TASK_STARTED:  // :297-302 -> :2254-2276
@@ -1664,6 +1740,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         row.flags = CRR_ROW_LIVE;
         row.reserved = 0;
         CHECK(T.child_insert(L, G, row));
+        K.add(L, G, CRR_TASK_START_CHILD, 0, ver, 0, id, 0, s);  // GenerateChildWorkflowTasks
         break;
       }
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:  // :390-395 -> :3485-3507
@@ -1688,6 +1765,8 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         CHECK(T.init_insert(L, G, t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED, row));
         // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
         if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
+        K.add(L, G, t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0,
+              ver, 0, id, 0, s);
         break;
       }
       case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
@@ -1716,6 +1795,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
                                                                 : CRR_CLOSE_TERMINATED;
         CHECK(update_state(L, CRR_STATE_COMPLETED, cs));
         L.completion_event_batch_id = batch_first_id;
+        close_tasks(L, G, K, ver, ev.ts, s, retention_days);
         break;
       }
       case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: {  // :587-627 -> :3366-3382
@@ -1727,12 +1807,15 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         }
         CHECK(update_state(L, CRR_STATE_COMPLETED, CRR_CLOSE_CONTINUED_AS_NEW));
         L.completion_event_batch_id = batch_first_id;
+        close_tasks(L, G, K, ver, ev.ts, s, retention_days);
         break;
       }
       case CRR_EV_REQUEST_CANCEL_ACTIVITY_TASK_FAILED:  // :339-340
       case CRR_EV_CANCEL_TIMER_FAILED:                  // :363-364
       case CRR_EV_MARKER_RECORDED:                      // :494-495
+        break;
       case CRR_EV_UPSERT_WORKFLOW_SEARCH_ATTRIBUTES:    // :511-515 (map merge: host materialised)
+        K.add(L, G, CRR_TASK_UPSERT_SEARCH_ATTRIBUTES, 0, L.current_version, 0, 0, 0, s);  // GenerateWorkflowSearchAttrTasks
         break;
       default:  // :629-630
         FAIL(CRR_ERR_UNKNOWN_EVENT_TYPE, s);
@@ -1742,7 +1825,9 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
   return CRR_OK;
 }
 
-template <class P, class SRC>
+// EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
+// the replay loop of a launch that does not ask for tasks carries none of its registers.
+template <bool EMIT, class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
                                             const Geo& G, P& T, SRC& src, const u32* crc_tables) {
   const i32 n_ev = wfp->ev_count;
@@ -1764,6 +1849,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = 0;
   L.inconsistencies = 0;
   L.status = CRR_OK; L.fail_step = -1;
+  L.n_tasks = 0; L.expiration_ns = 0;
+  const TaskSink K{EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0, T.task_writer()};
 
   i64 batch_first_id = 0;
   i32 last_task_step = -1;
@@ -1815,14 +1902,16 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       int rc;
       const i32 tu = uniform32(t);
       if (__builtin_amdgcn_ballot_w64(t != tu) == 0)
-        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns);
+        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
+                         K, wfp->retention_days);
       else
-        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns);
+        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
+                         K, wfp->retention_days);
       if (rc) FAIL(rc, s);
     }
 
     if (et & CRR_ETYPE_BATCH_LAST) {
-      if (!(CRR_EXP & 2)) T.epilogue(L, G);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
+      if (!(CRR_EXP & 2)) T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
       L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
@@ -1835,12 +1924,16 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     if (want_id < 0 || (want_ver < 0 && want_ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, n_ev);
     if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
   }
-  if (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS) T.refresh(L, G);  // Rebuild's RefreshTasks (state_rebuilder.go:183)
+  if (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:183)
+    T.refresh(L, G);
+    L.n_tasks = 0;  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
+  }
 done_events:
 #undef CHECK
 #undef FAIL
   if (last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
+  if (L.status == CRR_OK && K.on && L.n_tasks > G.task_cap) L.status = CRR_ERR_CAPACITY;
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
     out.exec[w].status = CRR_INTERNAL_RETRY;
     T.retry_push(in, out, w);
@@ -1887,8 +1980,8 @@ done_events:
   R.token_src = L.token_src;
   R.checksum = 0;
   R.payload_len = 0;
-  R.reserved[0] = 0;
-  R.reserved[1] = 0;
+  R.n_tasks = L.n_tasks;
+  R.reserved = 0;
   if (L.status == CRR_OK && !(CRR_EXP & 1)) R.checksum = payload_crc(R, T, G, wfp, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
 }
@@ -1915,7 +2008,7 @@ union BlockArena {
 
 // Fast path (stride 64): blocks [0, wave_blocks) replay the long-history tail one workflow per
 // wavefront (dispatched first, they run longest), the remaining blocks replay lane per workflow.
-template <class TIER, bool WAVE_TAIL>
+template <class TIER, bool WAVE_TAIL, bool EMIT>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
@@ -1936,7 +2029,7 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     T.S.M = &arena.wave[wv];
     T.init();
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
-    replay_body(in, out, w, wfp, G, T, S, crc_tables);
+    replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
     return;
   }
   const u32 w = (blockIdx.x - wave_blocks) * blockDim.x + threadIdx.x;
@@ -1950,24 +2043,28 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
   LdsTables<TIER> T;
   T.init(&arena.lane, &in, ev_begin);
-  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count);
-  replay_body(in, out, w, wfp, G, T, S, crc_tables);
+  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
+  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
 }
-template <bool WAVE_TAIL>
+template <bool WAVE_TAIL, bool EMIT>
 #ifndef CRR_SMALL_WAVES_PER_EU
 #define CRR_SMALL_WAVES_PER_EU 3
 #endif
-__global__ void __launch_bounds__(kBlock, CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<SmallTier, WAVE_TAIL>(in, out, phase);
+__global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
+  replay_lds<SmallTier, WAVE_TAIL, EMIT>(in, out, phase);
 }
-template <bool WAVE_TAIL>
+template <bool WAVE_TAIL, bool EMIT>
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<LargeTier, WAVE_TAIL>(in, out, phase);
+  replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase);
 }
-template __global__ void replay_lds_small_kernel<false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_small_kernel<true>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<true, false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<false, false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<true, false>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<false, true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<true, true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<false, true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_kernel<true, true>(crr_inputs, crr_outputs, int);
 
 // General path over HBM slot tables (any layout).  retry_only: replay the workflows the fast path
 // handed back (scratch list), grid-striding so the launch is cheap when there are none.
@@ -1990,8 +2087,8 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
     Geo G;
     load_geo(G, wfp, out, st);
     GlobalTables T;
-    LaneSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-    replay_body(in, out, w, wfp, G, T, S, crc_tables);
+    LaneSource S(in.ev, wfp->ev_begin, st, wfp->ev_count, (in.flags & CRR_IN_EMIT_TASKS) != 0);
+    replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
   }
 }
 
@@ -2013,7 +2110,7 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
 }
 __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_outputs out, int phase) {
   __shared__ u32 crc_tables[8 * 256];

@@ -41,7 +41,7 @@ class CWfSource(ctypes.Structure):
                 ("final_token", ctypes.c_void_p), ("final_token_len", ctypes.c_uint32),
                 ("new_run_wf", ctypes.c_int32),
                 ("rebuild_last_event_id", ctypes.c_int64), ("rebuild_last_event_version", ctypes.c_int64),
-                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("retention_days", ctypes.c_int32)]
 
 
 class CDecodedView(ctypes.Structure):
@@ -51,7 +51,7 @@ class CDecodedView(ctypes.Structure):
                 ("reset_keys", ctypes.c_void_p), ("n_reset_keys", ctypes.c_uint64),
                 ("arena", ctypes.c_void_p), ("n_arena", ctypes.c_uint64),
                 ("wf", ctypes.c_void_p), ("n_wf", ctypes.c_uint32),
-                ("table_rows", ctypes.c_uint64 * 7),
+                ("table_rows", ctypes.c_uint64 * 8),
                 ("key_off", ctypes.c_void_p), ("key_len", ctypes.c_void_p),
                 ("key_arena", ctypes.c_void_p), ("n_key_arena", ctypes.c_uint64)]
 
@@ -88,6 +88,7 @@ class WorkflowSource:
     new_run: Optional[int] = None        # workflow index of the CAN new-run history
     is_new_run: bool = False
     refresh_tasks: bool = False          # Rebuild's RefreshTasks after the replay
+    retention_days: int = 1
 
 
 def _copy(ptr, n, dtype):
@@ -121,6 +122,7 @@ def decode_histories(sources: Sequence[WorkflowSource], known_domains: Optional[
         c.new_run_wf = -1 if s.new_run is None else int(s.new_run)
         c.rebuild_last_event_id = s.rebuild_last_event_id
         c.rebuild_last_event_version = s.rebuild_last_event_version
+        c.retention_days = s.retention_days
         c.flags = (abi.WF_FLAG_NEW_RUN if s.is_new_run else 0) | (abi.WF_FLAG_REFRESH_TASKS if s.refresh_tasks else 0)
     nb = len(blobs)
     bptr = (ctypes.c_void_p * max(nb, 1))()

@@ -127,6 +127,8 @@ class ReplayEngine:
         co.exec = T["exec"].data_ptr()
         for name, dt, *_ in abi.TABLES:
             rows = max(batch.table_rows.get(name, 0), 1)
+            if name == "tasks" and not batch.emit_tasks:
+                rows = 1   # not written without CRR_IN_EMIT_TASKS
             T["out_" + name] = torch.zeros(rows * dt.itemsize, dtype=torch.uint8, device=dev)
             setattr(co, name, T["out_" + name].data_ptr())
         T["scratch"] = torch.zeros(2 * batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)

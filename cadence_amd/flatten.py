@@ -43,6 +43,8 @@ class HistoryBatch:
     # length bucketing: workflows [wave_begin, n_wf) are long histories, contiguous (stride 1),
     # replayed one per wavefront (CRR_IN_WAVE_TAIL); None: every workflow uses `stride`
     wave_begin: Optional[int] = None
+    # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
+    emit_tasks: bool = False
 
     def wf_strides(self) -> np.ndarray:
         """Column / row stride of every workflow."""
@@ -52,7 +54,7 @@ class HistoryBatch:
         return st
 
     def c_flags(self) -> int:
-        return abi.IN_WAVE_TAIL if self.wave_begin is not None else 0
+        return (abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
 
     @property
     def n_wf(self) -> int:
@@ -126,6 +128,7 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         begin = i
         empty_at = -1
         n_act = n_timer = n_child = n_rc = n_sig = n_dtc = 0
+        n_tasks = 0          # upper bound of the tasks ApplyEvents generates (task_cap)
         max_prev = 0
         vh_items = 0
         last_ver = None
@@ -134,8 +137,10 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
                 if empty_at < 0:
                     empty_at = i - begin
                 continue
+            n_tasks += 2         # the batch's timer epilogue: one activity + one user timer task at most
             for j, e in enumerate(batch):
                 t = int(e.event_type)
+                n_tasks += TASKS_PER_EVENT.get(t, 0)
                 flags = (abi.BATCH_FIRST if j == 0 else 0) | (abi.BATCH_LAST if j == len(batch) - 1 else 0)
                 cols["etype"][i] = (t & abi.ETYPE_MASK) | flags if 0 <= t < abi.EV_TYPE_COUNT else (abi.EV_PAD - 1) | flags
                 cols["event_id"][i] = e.id
@@ -166,7 +171,8 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
                     init = e.attrs.get("initiator")
                     start_side.append((a("task_start_to_close_timeout_seconds", 0), a("execution_start_to_close_timeout_seconds", 0),
                                        a("first_decision_task_backoff_seconds", 0),
-                                       abi.INITIATOR_NIL if init is None else int(init), pstat, prev_off, prev_cnt, 0))
+                                       abi.INITIATOR_NIL if init is None else int(init), pstat, prev_off, prev_cnt,
+                                       a("attempt", 0), a("expiration_timestamp", 0), 0))
                     aux = len(start_side) - 1
                 elif t == ET.DecisionTaskScheduled:
                     ref = a("attempt", 0)
@@ -260,11 +266,13 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         caps["rc_cap"][w] = n_rc
         caps["sig_cap"][w] = n_sig
         caps["vh_cap"][w] = vh_items
+        caps["task_cap"][w] = n_tasks
+        r["retention_days"] = h.retention_days
         caps["rp_cap"][w] = max_prev * max(1, sum(1 for e in h.events if e.event_type == ET.WorkflowExecutionStarted)) + n_dtc
     batch = HistoryBatch(
         cols=cols,
         act_side=np.array(act_side or [(0,) * 8], dtype=abi.ACTIVITY_SIDE),
-        start_side=np.array(start_side or [(0,) * 8], dtype=abi.START_SIDE),
+        start_side=np.array(start_side or [(0,) * 10], dtype=abi.START_SIDE),
         reset_keys=np.array(reset_keys or [0], dtype=np.uint32),
         arena=np.frombuffer(bytes(arena) or b"\0", dtype=np.uint8).copy(),
         wf=wf, stride=1,
@@ -285,6 +293,16 @@ def assign_canonical_tables(batch: HistoryBatch, caps: Dict[str, np.ndarray]):
         batch.wf[cap_f] = c
         batch.table_rows[name] = int(c.sum()) if c.size else 0
 
+
+# tasks the task generator adds per event type (state_builder.go:157-625): an upper bound
+TASKS_PER_EVENT = {int(ET.WorkflowExecutionStarted): 3, int(ET.DecisionTaskScheduled): 1, int(ET.DecisionTaskStarted): 1,
+                   int(ET.DecisionTaskTimedOut): 1, int(ET.DecisionTaskFailed): 1, int(ET.ActivityTaskScheduled): 1,
+                   int(ET.StartChildWorkflowExecutionInitiated): 1,
+                   int(ET.RequestCancelExternalWorkflowExecutionInitiated): 1,
+                   int(ET.SignalExternalWorkflowExecutionInitiated): 1, int(ET.UpsertWorkflowSearchAttributes): 1,
+                   int(ET.WorkflowExecutionCompleted): 2, int(ET.WorkflowExecutionFailed): 2,
+                   int(ET.WorkflowExecutionTimedOut): 2, int(ET.WorkflowExecutionCanceled): 2,
+                   int(ET.WorkflowExecutionTerminated): 2, int(ET.WorkflowExecutionContinuedAsNew): 2}
 
 LONG_HISTORY = 256   # lane per workflow up to ~256 events, a wavefront per workflow above
 
@@ -372,7 +390,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
-                       wave_begin=n_lane if long_threshold is not None else None)
+                       wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)
         cap[:n_lane] = wf[cap_f][:n_lane]

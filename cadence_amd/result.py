@@ -29,7 +29,8 @@ def allocate_host(batch: HistoryBatch) -> ReplayResult:
     ex = np.zeros(max(batch.n_wf, 1), dtype=abi.EXEC_ROW)[:batch.n_wf]
     tables = {}
     for name, dt, *_ in abi.TABLES:
-        tables[name] = np.zeros(max(batch.table_rows.get(name, 0), 1), dtype=dt)
+        rows = batch.table_rows.get(name, 0) if (name != "tasks" or batch.emit_tasks) else 0
+        tables[name] = np.zeros(max(rows, 1), dtype=dt)
     return ReplayResult(ex, tables)
 
 

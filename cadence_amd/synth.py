@@ -11,7 +11,7 @@ import numpy as np
 
 from . import abi
 from .abi import EventType as ET
-from .flatten import HistoryBatch, assign_canonical_tables
+from .flatten import TASKS_PER_EVENT, HistoryBatch, assign_canonical_tables
 
 SEED_C1 = 0xCAD00001
 SEED_C2 = 0xCAD00002
@@ -152,9 +152,11 @@ def activity_chain(n_wf: int, k: int, seed: int, version: int = 1, with_keys: bo
     wf["final_token_len"] = abi.NO_TOKEN
     batch = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                          reset_keys=np.zeros(1, np.uint32), arena=arena, wf=wf, stride=1)
+    wf["retention_days"] = 1
+    n_task = sum(TASKS_PER_EVENT.get(int(t), 0) for t in types) + 2 * int((flags & abi.BATCH_LAST != 0).sum())
     caps = {"act_cap": np.full(n_wf, k), "timer_cap": np.zeros(n_wf), "child_cap": np.zeros(n_wf),
             "rc_cap": np.zeros(n_wf), "sig_cap": np.zeros(n_wf), "vh_cap": np.ones(n_wf),
-            "rp_cap": np.ones(n_wf)}
+            "rp_cap": np.ones(n_wf), "task_cap": np.full(n_wf, n_task)}
     assign_canonical_tables(batch, caps)
     if with_keys:
         # per-event key strings for the oracle: "bin-v1" for decisions, str(i) for activity IDs
@@ -172,7 +174,7 @@ def activity_chain(n_wf: int, k: int, seed: int, version: int = 1, with_keys: bo
 def algorithmic_bytes(batch: HistoryBatch, res=None) -> int:
     """Algorithmic HBM bytes of one replay launch (DESIGN.md "Roofline").
 
-    reads : 49 B per event (8 columns) + 32 B per activity/start side record read
+    reads : 49 B per event (8 columns) + 32 / 48 B per activity / start side record read
             + the workflow descriptor (160 B) + the branch token bytes checksummed
     writes: the execution row (192 B) + 16 B per version-history item + the live pending rows
             (activity 112, timer 40, child 48, request-cancel / signal 32, reset point 16 B)
@@ -183,7 +185,8 @@ def algorithmic_bytes(batch: HistoryBatch, res=None) -> int:
     n_act_sched = int(((t == ET.ActivityTaskScheduled) & real).sum())
     n_started = int(((t == ET.WorkflowExecutionStarted) & real).sum())
     tok = int(np.minimum(batch.wf["start_token_len"], 4096).sum())
-    b = n_ev * abi.BYTES_PER_EVENT + 32 * (n_act_sched + n_started) + batch.n_wf * abi.WORKFLOW.itemsize + tok
+    b = (n_ev * abi.BYTES_PER_EVENT + abi.ACTIVITY_SIDE.itemsize * n_act_sched + abi.START_SIDE.itemsize * n_started
+         + batch.n_wf * abi.WORKFLOW.itemsize + tok)
     b += batch.n_wf * abi.EXEC_ROW.itemsize
     if res is not None:
         ex = res.exec

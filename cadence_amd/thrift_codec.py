@@ -149,7 +149,9 @@ def attribute_fields(e: HistoryEvent, rng: Optional[random.Random] = None) -> Li
               _i32(50, g("task_start_to_close_timeout_seconds", 0))]
         if a.get("initiator") is not None:
             f.append(_i32(55, a["initiator"]))
-        f += [_s(60, "identity"), _i32(80, 0)]
+        f += [_s(60, "identity"), _i32(80, g("attempt", 0))]
+        if g("expiration_timestamp", 0):
+            f.append(_i64(90, g("expiration_timestamp")))
         f.append(_i32(110, g("first_decision_task_backoff_seconds", 0)))
         if a.get("prev_auto_reset_points") is not None:
             f.append(_reset_points(130, a["prev_auto_reset_points"]))

@@ -42,8 +42,8 @@ typedef struct crr_wf_source {
     int32_t        new_run_wf;            /* workflow index of the CAN new-run history, -1: none */
     int64_t        rebuild_last_event_id;
     int64_t        rebuild_last_event_version;
-    int32_t        flags;                 /* CRR_WF_FLAG_NEW_RUN */
-    int32_t        reserved;
+    int32_t        flags;                 /* CRR_WF_FLAG_* */
+    int32_t        retention_days;        /* domain retention (DeleteHistoryEventTask) */
 } crr_wf_source;
 
 /* Read-only view of a decoded batch (host pointers, valid until crr_decoded_free). */
@@ -55,7 +55,7 @@ typedef struct crr_decoded_view {
     const uint32_t*           reset_keys;  uint64_t n_reset_keys;
     const uint8_t*            arena;       uint64_t n_arena;
     const crr_workflow*       wf;          uint32_t n_wf;
-    uint64_t                  table_rows[7];  /* act, timer, child, rc, sig, vh, rp slot-table sizes */
+    uint64_t                  table_rows[8];  /* act, timer, child, rc, sig, vh, rp, tasks slot-table sizes */
     /* per-event key strings (ActivityID / TimerID / BinaryChecksum; "" otherwise), for checkers */
     const uint32_t*           key_off;
     const uint32_t*           key_len;

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define CRR_ABI_VERSION 1
+#define CRR_ABI_VERSION 2
 
 /* ---- constants restated from the reference ------------------------------------------------ */
 /* common/constants.go:30-58 */
@@ -211,7 +211,7 @@ typedef struct crr_activity_side {
     int32_t reserved;
 } crr_activity_side;
 
-/* WorkflowExecutionStartedEventAttributes fields the state machine reads (32 B). */
+/* WorkflowExecutionStartedEventAttributes fields the state machine reads (48 B). */
 typedef struct crr_start_side {
     int32_t decision_start_to_close;   /* GetTaskStartToCloseTimeoutSeconds (DecisionStartToCloseTimeout) */
     int32_t workflow_timeout;          /* GetExecutionStartToCloseTimeoutSeconds */
@@ -220,10 +220,12 @@ typedef struct crr_start_side {
     int32_t parent_domain_status;      /* CRR_DOMAIN_* of the ParentWorkflowDomain lookup (state_builder.go:137-147) */
     uint32_t prev_reset_key_off;       /* PrevAutoResetPoints binary checksums (keys) in crr_inputs.reset_keys */
     int32_t prev_reset_count;          /* -1 == PrevAutoResetPoints nil (or Points nil) */
-    int32_t reserved;
+    int32_t attempt;                   /* GetAttempt() (GenerateWorkflowStartTasks, task_generator.go:156) */
+    int64_t expiration_ns;             /* GetExpirationTimestamp() (0: unset; mutable_state_builder.go:1800-1802) */
+    int64_t reserved;
 } crr_start_side;
 
-/* Per-workflow descriptor (160 B). */
+/* Per-workflow descriptor (168 B). */
 typedef struct crr_workflow {
     int64_t  ev_begin;          /* column index of step 0 */
     int32_t  ev_count;          /* number of real events */
@@ -240,8 +242,10 @@ typedef struct crr_workflow {
     int64_t  act_base;  int64_t timer_base; int64_t child_base; int64_t rc_base;
     int64_t  sig_base;  int64_t vh_base;    int64_t rp_base;
     int32_t  act_cap, timer_cap, child_cap, rc_cap, sig_cap, vh_cap, rp_cap;
-    int32_t  flags;             /* bit0: is a CAN new-run history (replayed in the first phase) */
-    int64_t  reserved;
+    int32_t  flags;             /* CRR_WF_FLAG_* */
+    int64_t  task_base;         /* emitted-task rows (CRR_IN_EMIT_TASKS): task_base + slot * stride */
+    int32_t  task_cap;
+    int32_t  retention_days;    /* domainEntry.GetRetentionDays (DeleteHistoryEventTask, task_generator.go:238-255) */
 } crr_workflow;
 
 #define CRR_WF_FLAG_NEW_RUN 1
@@ -271,6 +275,7 @@ typedef struct crr_inputs {
                                    the general path, so the hint affects speed only */
 #define CRR_IN_WAVE_TAIL   4u   /* length bucketing (stride-64 batches only): workflows
                                    [wave_begin, n_wf) are replayed one per wavefront */
+#define CRR_IN_EMIT_TASKS  8u   /* write the transfer / timer tasks ApplyEvents generates (crr_task_row) */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (192 B). */
@@ -293,7 +298,8 @@ typedef struct crr_exec_row {
     int32_t  token_src;              /* 0: none (empty token), 1: start token, 2: final token */
     uint32_t checksum;               /* crc32.ChecksumIEEE of the thriftrw payload (crc.go:46) */
     uint32_t payload_len;            /* bytes the checksum was computed over (0x59 preamble included) */
-    int32_t  reserved[2];
+    int32_t  n_tasks;                /* task rows written (CRR_IN_EMIT_TASKS) */
+    int32_t  reserved;
 } crr_exec_row;
 
 #define CRR_EXEC_CANCEL_REQUESTED  1u
@@ -354,6 +360,43 @@ typedef struct crr_reset_point_row {
 #define CRR_ROW_HAS_RETRY        8u
 #define CRR_ROW_RESETTABLE      16u
 
+/* Transfer / timer tasks ApplyEvents generates, one row per task in the order
+ * the Go code adds them: the task-generator calls of state_builder.go:157-625
+ * (mutable_state_task_generator.go:143-612) and the per-batch timer epilogue (timer_sequence.go:127-199).
+ * Strings (task list, target domain / workflow / run) come from the event at step `src`; what depends
+ * on cluster metadata -- whether a child / cancel / signal task is cross-cluster
+ * (isCrossClusterTask) and the shape of the close tasks (getTargetCluster / getParentCluster) --
+ * is decided by the host from CRR_TASK_CLOSE_EXECUTION and the target domain. */
+enum crr_task_kind {
+    CRR_TASK_RECORD_WORKFLOW_STARTED = 1,   /* transfer: version = start event version            */
+    CRR_TASK_DECISION = 2,                  /* transfer: event_id = ScheduleID, version = decision  */
+    CRR_TASK_ACTIVITY = 3,                  /* transfer: event_id = ScheduleID                      */
+    CRR_TASK_START_CHILD = 4,               /* transfer: event_id = InitiatedID                     */
+    CRR_TASK_CANCEL_EXECUTION = 5,          /* transfer: event_id = InitiatedID                     */
+    CRR_TASK_SIGNAL_EXECUTION = 6,          /* transfer: event_id = InitiatedID                     */
+    CRR_TASK_UPSERT_SEARCH_ATTRIBUTES = 7,  /* transfer: version = current version                  */
+    CRR_TASK_CLOSE_EXECUTION = 8,           /* transfer: version = close event version              */
+    CRR_TASK_WORKFLOW_TIMEOUT = 16,         /* timer                                                */
+    CRR_TASK_WORKFLOW_BACKOFF = 17,         /* timer: aux = WorkflowBackoffTimeoutType              */
+    CRR_TASK_DECISION_TIMEOUT = 18,         /* timer: aux = TimerType, event_id = ScheduleID         */
+    CRR_TASK_ACTIVITY_TIMEOUT = 19,         /* timer: aux = TimerType, event_id = ScheduleID         */
+    CRR_TASK_USER_TIMER = 20,               /* timer: event_id = TimerStarted event ID              */
+    CRR_TASK_DELETE_HISTORY = 21            /* timer: close timestamp + retention                   */
+};
+/* persistence.WorkflowBackoffTimeoutType* (dataManagerInterfaces.go) */
+#define CRR_BACKOFF_RETRY 0
+#define CRR_BACKOFF_CRON  1
+
+typedef struct crr_task_row {
+    int32_t kind;             /* crr_task_kind */
+    int32_t aux;
+    int64_t version;
+    int64_t visibility_ts;    /* timer tasks (Unix ns); 0 for transfer tasks */
+    int64_t event_id;
+    int32_t attempt;
+    int32_t src;              /* step of the event the task's strings come from (-1: none) */
+} crr_task_row;               /* 40 B */
+
 typedef struct crr_outputs {
     crr_exec_row*        exec;      /* [n_wf], indexed by workflow */
     crr_activity_row*    act;       /* slot tables, rows addressed by crr_workflow bases */
@@ -363,6 +406,7 @@ typedef struct crr_outputs {
     crr_initiated_row*   sig;
     crr_vh_item*         vh;
     crr_reset_point_row* rp;
+    crr_task_row*        tasks;     /* CRR_IN_EMIT_TASKS only (else may be NULL) */
     uint32_t*            scratch;   /* engine scratch: >= 2 * n_wf + 64 words, zero-filled before the
                                        first call that uses it; every call leaves its counters zeroed */
 } crr_outputs;
@@ -442,7 +486,7 @@ int crr_set_device(int device);
 int crr_abi_version(void);
 size_t crr_sizeof(int which);   /* 0 workflow, 1 exec row, 2 activity, 3 timer, 4 child, 5 initiated,
                                    6 vh item, 7 reset point, 8 activity side, 9 start side,
-                                   10 ndc task, 11 ndc result */
+                                   10 ndc task, 11 ndc result, 12 task row */
 
 /* Host-side CRC32-IEEE (hash/crc32.ChecksumIEEE) used by the shim's standalone verify. */
 uint32_t crr_crc32_ieee(const uint8_t* data, size_t len);

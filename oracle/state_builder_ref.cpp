@@ -270,6 +270,16 @@ struct MutableState {
   i64 currentVersion = 0;
   i64 now_ns = 0;     // injected clock.TimeSource
   int inconsistencies = 0;
+  i64 expiration_ns = 0;                 // executionInfo.ExpirationTime (0: unset)
+  bool emit_tasks = false;               // CRR_IN_EMIT_TASKS
+  std::vector<crr_task_row> tasks;       // AddTransferTasks / AddTimerTasks, in order
+  void AddTask(int kind, int aux, i64 version, i64 vis, i64 event_id, int attempt, int src) {
+    if (!emit_tasks) return;
+    crr_task_row r;
+    r.kind = kind; r.aux = aux; r.version = version; r.visibility_ts = vis; r.event_id = event_id;
+    r.attempt = attempt; r.src = src;
+    tasks.push_back(r);
+  }
 
   // logDataInconsistency (:4720-4731)
   void log_data_inconsistency() { ++inconsistencies; }
@@ -506,7 +516,8 @@ Err CreateNextActivityTimer(MutableState& ms) {
   ActivityInfo& ai = it->second;
   ai.timer_task_status |= timer_type_to_mask(first.timer_type);
   if (first.timer_type == CRR_TIMEOUT_HEARTBEAT) ai.last_hb_timeout_vis_s = unix_seconds(first.timestamp);
-  // UpdateActivity (:1292-1307) cannot fail: the info is pending.  AddTimerTasks: task output ("next").
+  // UpdateActivity (:1292-1307) cannot fail: the info is pending.  AddTimerTasks (:190-196):
+  ms.AddTask(CRR_TASK_ACTIVITY_TIMEOUT, first.timer_type, ms.currentVersion, first.timestamp, first.event_id, 0, -1);
   return Err{};
 }
 // CreateNextUserTimer (:127-160)
@@ -521,6 +532,7 @@ Err CreateNextUserTimer(MutableState& ms) {
   auto jt = ms.pendingTimerInfoIDs.find(it->second);
   if (jt == ms.pendingTimerInfoIDs.end()) return mk(CRR_ERR_TIMER_SEQUENCE);
   jt->second.task_status = CRR_TIMER_TASK_STATUS_CREATED;  // UpdateUserTimer (:1363-1387) succeeds
+  ms.AddTask(CRR_TASK_USER_TIMER, 0, ms.currentVersion, first.timestamp, first.event_id, 0, -1);  // (:151-156)
   return Err{};
 }
 
@@ -541,6 +553,7 @@ class Replayer {
     WfView v{in_, wf, ks_};
     ms.currentVersion = wf->init_version;  // domainEntry.GetFailoverVersion() (:207)
     ms.now_ns = wf->now_ns;
+    ms.emit_tasks = (in_->flags & CRR_IN_EMIT_TASKS) != 0;
     Outcome out;
     int k = 0;
     const int n = wf->ev_count;
@@ -576,17 +589,26 @@ class Replayer {
     // pending activity's TimerTaskStatus and user timer's TaskStatus cleared, then one
     // CreateNextActivityTimer / CreateNextUserTimer (LastHeartbeatTimeoutVisibilityInSeconds is kept)
     if (wf->flags & CRR_WF_FLAG_REFRESH_TASKS) {
+      ms.emit_tasks = false;
       for (auto& kv : ms.pendingActivityInfoIDs) kv.second.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
       Err er = CreateNextActivityTimer(ms);
       if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
       for (auto& kv : ms.pendingTimerInfoIDs) kv.second.task_status = CRR_TIMER_TASK_STATUS_NONE;
       er = CreateNextUserTimer(ms);
       if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
+      ms.tasks.clear();  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
     }
     return out;
   }
 
  private:
+  // GenerateWorkflowCloseTasks (task_generator.go:168-258): close transfer task + DeleteHistoryEventTask
+  static void CloseTasks(MutableState& ms, const WfView& v, int s) {
+    ms.AddTask(CRR_TASK_CLOSE_EXECUTION, 0, v.version(s), 0, 0, 0, s);
+    ms.AddTask(CRR_TASK_DELETE_HISTORY, 0, v.version(s), wadd(v.ts(s), wmul((i64)v.wf->retention_days * 86400, kSecond)),
+               0, 0, s);
+  }
+
   // stateBuilderImpl.ApplyEvents (state_builder.go:90-648) for history = steps [b, e)
   Outcome ApplyEvents(const WfView& v, MutableState& ms, int b, int e) {
     Outcome out;
@@ -637,11 +659,22 @@ class Replayer {
             x.reset_points.push_back(rp);
           }
           // taskGenerator.GenerateRecordWorkflowStartedTasks / GenerateWorkflowStartTasks: tasks only
-          // GenerateDelayedDecisionTasks (mutable_state_task_generator.go:242-281)
+          if (ss.expiration_ns != 0) ms.expiration_ns = ss.expiration_ns;  // (mutable_state_builder.go:1800-1802)
+          // GenerateRecordWorkflowStartedTasks (task_generator.go:301-313)
+          ms.AddTask(CRR_TASK_RECORD_WORKFLOW_STARTED, 0, v.version(s), 0, 0, 0, s);
+          {  // GenerateWorkflowStartTasks (:143-166), startTime = event timestamp
+            i64 vis = wadd(v.ts(s), wmul(wadd(ss.workflow_timeout, ss.first_decision_backoff), kSecond));
+            if (ss.attempt > 0 && ms.expiration_ns != 0 && vis > ms.expiration_ns) vis = ms.expiration_ns;
+            ms.AddTask(CRR_TASK_WORKFLOW_TIMEOUT, 0, v.version(s), vis, 0, 0, s);
+          }
+          // GenerateDelayedDecisionTasks (mutable_state_task_generator.go:260-299)
           if (ss.first_decision_backoff > 0) {
             if (ss.initiator != CRR_INITIATOR_NIL && ss.initiator != CRR_INITIATOR_RETRY_POLICY &&
                 ss.initiator != CRR_INITIATOR_CRON)
               return fail(CRR_ERR_BAD_INITIATOR, s);
+            ms.AddTask(CRR_TASK_WORKFLOW_BACKOFF,
+                       ss.initiator == CRR_INITIATOR_RETRY_POLICY ? CRR_BACKOFF_RETRY : CRR_BACKOFF_CRON, v.version(s),
+                       wadd(v.ts(s), wmul(ss.first_decision_backoff, kSecond)), 0, 0, s);
           }
           // SetHistoryTree(runID) (:367-376): the branch token with the injected branchID
           ms.vh.token_src = 1;
@@ -650,12 +683,18 @@ class Replayer {
         case CRR_EV_DECISION_TASK_SCHEDULED: {  // :185-208
           er = ms.ReplicateDecisionTaskScheduledEvent(v.version(s), v.id(s), v.aux(s), v.ref(s), v.ts(s), v.ts(s));
           if (!er.ok()) return fail(er.code, s);
-          break;  // GenerateDecisionScheduleTasks finds the decision just written
+          // GenerateDecisionScheduleTasks (task_generator.go:315-350): sticky cleared, no schedule-to-start timer
+          ms.AddTask(CRR_TASK_DECISION, 0, ms.exec.decision_version, 0, ms.exec.decision_schedule_id, 0, s);
+          break;
         }
         case CRR_EV_DECISION_TASK_STARTED: {  // :210-228
           er = ms.ReplicateDecisionTaskStartedEvent(v.version(s), v.ref(s), v.id(s), s, v.ts(s));
           if (!er.ok()) return fail(er.code, s);
-          break;  // GenerateDecisionStartTasks: Attempt == 0, no state change (task_generator.go:371-376)
+          // GenerateDecisionStartTasks (task_generator.go:352-388): Attempt == 0, no timeout override
+          ms.AddTask(CRR_TASK_DECISION_TIMEOUT, CRR_TIMEOUT_START_TO_CLOSE, ms.exec.decision_version,
+                     wadd(v.ts(s), wmul(ms.exec.decision_timeout, kSecond)), ms.exec.decision_schedule_id,
+                     (int)ms.exec.decision_attempt, s);
+          break;
         }
         case CRR_EV_DECISION_TASK_COMPLETED:  // :230-235
           ms.ReplicateDecisionTaskCompletedEvent(v.ref(s), v.kstr(s), v.key(s), s);
@@ -663,11 +702,15 @@ class Replayer {
         case CRR_EV_DECISION_TASK_TIMED_OUT:  // :237-259
           // ReplicateDecisionTaskTimedOutEvent (:256-271): StickyTaskList == "" after ClearStickyness
           ms.FailDecision(true);
-          ms.ReplicateTransientDecisionTaskScheduled();
+          if (ms.ReplicateTransientDecisionTaskScheduled())  // its schedule task: task list of the start event
+            ms.AddTask(CRR_TASK_DECISION, 0, ms.exec.decision_version, 0, ms.exec.decision_schedule_id, 0,
+                       ms.exec.start_src);
           break;
         case CRR_EV_DECISION_TASK_FAILED:  // :261-281
           ms.FailDecision(true);
-          ms.ReplicateTransientDecisionTaskScheduled();
+          if (ms.ReplicateTransientDecisionTaskScheduled())  // its schedule task: task list of the start event
+            ms.AddTask(CRR_TASK_DECISION, 0, ms.exec.decision_version, 0, ms.exec.decision_schedule_id, 0,
+                       ms.exec.start_src);
           break;
         case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
           const crr_activity_side& as = in_->act_side[v.aux(s)];
@@ -693,7 +736,9 @@ class Replayer {
           ai.has_retry_policy = as.has_retry_policy != 0;
           ms.pendingActivityInfoIDs[ai.schedule_id] = ai;
           ms.pendingActivityIDToEventID[ai.activity_id] = ai.schedule_id;
-          break;  // GenerateActivityTransferTasks: ai.DomainID != "" -> no lookup
+          // GenerateActivityTransferTasks (task_generator.go:390-428): ai.DomainID != "" -> no lookup
+          ms.AddTask(CRR_TASK_ACTIVITY, 0, ai.version, 0, ai.schedule_id, 0, s);
+          break;
         }
         case CRR_EV_ACTIVITY_TASK_STARTED: {  // :297-302 -> :2254-2276
           auto it = ms.pendingActivityInfoIDs.find(v.ref(s));
@@ -750,7 +795,9 @@ class Replayer {
           ci.started_id = CRR_EMPTY_EVENT_ID;
           ci.src = s;  // StartedWorkflowID / WorkflowTypeName / ParentClosePolicy / CreateRequestID=uuid(s)
           ms.pendingChildExecutionInfoIDs[ci.initiated_id] = ci;
-          break;  // GenerateChildWorkflowTasks: info present, domain resolved
+          // GenerateChildWorkflowTasks (task_generator.go:451-498): info present, domain resolved
+          ms.AddTask(CRR_TASK_START_CHILD, 0, ci.version, 0, ci.initiated_id, 0, s);
+          break;
         }
         case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED:      // :383-388 -> :3537-3545
         case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:         // :397-402 -> :3590-3598
@@ -776,6 +823,7 @@ class Replayer {
           ms.pendingRequestCancelInfoIDs[ri.initiated_id] = ri;
           // GenerateRequestCancelExternalTasks -> getTargetDomainID (task_generator.go:556-559)
           if (v.aux(s) == CRR_DOMAIN_UNKNOWN) return fail(CRR_ERR_DOMAIN_NOT_FOUND, s);
+          ms.AddTask(CRR_TASK_CANCEL_EXECUTION, 0, v.version(s), 0, v.id(s), 0, s);  // (:529-546)
           break;
         }
         case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:               // :449-454 -> :2849-2856
@@ -791,6 +839,7 @@ class Replayer {
           ms.pendingSignalInfoIDs[si.initiated_id] = si;
           // GenerateSignalExternalTasks -> getTargetDomainID (task_generator.go:604-607)
           if (v.aux(s) == CRR_DOMAIN_UNKNOWN) return fail(CRR_ERR_DOMAIN_NOT_FOUND, s);
+          ms.AddTask(CRR_TASK_SIGNAL_EXECUTION, 0, v.version(s), 0, v.id(s), 0, s);  // (:580-597)
           break;
         }
         case CRR_EV_SIGNAL_EXTERNAL_FAILED:                 // :480-485 -> :3020-3027
@@ -806,6 +855,7 @@ class Replayer {
           ms.exec.cancel_requested = true;
           break;
         case CRR_EV_UPSERT_WORKFLOW_SEARCH_ATTRIBUTES:  // :511-515 -> :2926-2948 (map merge: host materialised)
+          ms.AddTask(CRR_TASK_UPSERT_SEARCH_ATTRIBUTES, 0, ms.currentVersion, 0, 0, 0, s);  // (:602-612)
           break;
         case CRR_EV_WORKFLOW_EXECUTION_COMPLETED:   // :517-529 -> :2561-2576
         case CRR_EV_WORKFLOW_EXECUTION_FAILED:      // :531-543 -> :2601-2616
@@ -821,7 +871,8 @@ class Replayer {
           if (!er.ok()) return fail(er.code, s);
           ms.exec.completion_event_batch_id = firstEventID;
           ms.ClearStickyness();
-          break;  // GenerateWorkflowCloseTasks: domain lookups resolve (host-validated)
+          CloseTasks(ms, v, s);  // GenerateWorkflowCloseTasks: domain lookups resolve (host-validated)
+          break;
         }
         case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: {  // :587-627
           int nr = v.aux(s);
@@ -834,6 +885,7 @@ class Replayer {
           if (!er.ok()) return fail(er.code, s);
           ms.exec.completion_event_batch_id = firstEventID;
           ms.ClearStickyness();
+          CloseTasks(ms, v, s);
           break;
         }
         default:  // :629-630
@@ -1029,6 +1081,9 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
     o.event_id = ms.vh.items[i].event_id;
     o.version = ms.vh.items[i].version;
   }
+  r.n_tasks = (i32)ms.tasks.size();
+  if (in->flags & CRR_IN_EMIT_TASKS)
+    for (size_t i = 0; i < ms.tasks.size() && (i32)i < wf->task_cap; ++i) out->tasks[wf->task_base + (i64)i * st] = ms.tasks[i];
   r.n_reset_points = (i32)x.reset_points.size();
   for (size_t i = 0; i < x.reset_points.size() && (i32)i < wf->rp_cap; ++i) {
     crr_reset_point_row& o = out->rp[wf->rp_base + (i64)i * st];
@@ -1037,7 +1092,7 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
   }
   bool overflow = r.n_activity > wf->act_cap || r.n_timer > wf->timer_cap || r.n_child > wf->child_cap ||
                   r.n_rc > wf->rc_cap || r.n_signal > wf->sig_cap || r.n_vh_items > wf->vh_cap ||
-                  r.n_reset_points > wf->rp_cap;
+                  r.n_reset_points > wf->rp_cap || r.n_tasks > wf->task_cap;
   if (overflow && r.status == CRR_OK) r.status = CRR_ERR_CAPACITY;
   if (r.status == CRR_OK) {
     std::vector<uint8_t> payload;

@@ -214,6 +214,28 @@ class Checksum:  # common/checksum/defs.go: Checksum{Version, Flavor, Value}
 
 
 @dataclasses.dataclass
+class Task:
+    """A persistence.Task the task generator added (mutable_state_task_generator.go); ``kind`` is an
+    abi.TaskKind.  Strings come from the event at step ``src``: the task list (decision / activity),
+    the target domain / workflow (child, cancel, signal).  Cross-cluster wrapping of child / cancel /
+    signal / close tasks needs cluster metadata and is left to the caller."""
+    kind: int
+    version: int
+    visibility_timestamp: int = 0     # timer tasks
+    event_id: int = 0                 # ScheduleID / InitiatedID / timer EventID
+    timeout_type: int = 0             # timer / backoff type
+    attempt: int = 0
+    task_list: str = ""
+    target_domain: str = ""
+    target_workflow_id: str = ""
+
+
+TRANSFER_KINDS = {abi.TaskKind.RecordWorkflowStarted, abi.TaskKind.Decision, abi.TaskKind.Activity,
+                  abi.TaskKind.StartChild, abi.TaskKind.CancelExecution, abi.TaskKind.SignalExecution,
+                  abi.TaskKind.UpsertSearchAttributes, abi.TaskKind.CloseExecution}
+
+
+@dataclasses.dataclass
 class WorkflowExecutionInfo:  # persistence.WorkflowExecutionInfo (the fields replay writes)
     domain_id: str
     workflow_id: str
@@ -256,6 +278,8 @@ class MutableState:
         self.current_version: int = abi.EMPTY_VERSION
         self.checksum: Optional[Checksum] = None
         self.inconsistencies: int = 0
+        self.transfer_tasks: List[Task] = []
+        self.timer_tasks: List[Task] = []
 
     # mutable_state.go:59-239 (the subset replay callers read)
     def get_execution_info(self) -> WorkflowExecutionInfo:
@@ -328,6 +352,12 @@ class MutableState:
     def get_checksum(self) -> Optional[Checksum]:
         return self.checksum
 
+    def get_transfer_tasks(self) -> List[Task]:  # mutable_state.go:226
+        return self.transfer_tasks
+
+    def get_timer_tasks(self) -> List[Task]:  # mutable_state.go:228
+        return self.timer_tasks
+
 
 # ---- the batched engine ---------------------------------------------------------------------------------
 @dataclasses.dataclass
@@ -351,11 +381,13 @@ class BatchStateBuilder:
     """
 
     def __init__(self, engine=None, domain_ids: Optional[Dict[str, str]] = None,
-                 uuid_fn: Callable[[str, str, int], str] = _default_uuid, layout: str = "interleaved"):
+                 uuid_fn: Callable[[str, str, int], str] = _default_uuid, layout: str = "interleaved",
+                 emit_tasks: bool = True):
         self.engine = engine          # None: a ReplayEngine on device 0, created at the first replay
         self.domain_ids = domain_ids
         self.uuid_fn = uuid_fn
         self.layout = layout
+        self.emit_tasks = emit_tasks       # generate the transfer / timer tasks (CRR_IN_EMIT_TASKS)
         self.histories: List[WorkflowHistory] = []
         self._outcomes: Optional[List[ReplayOutcome]] = None
 
@@ -381,6 +413,7 @@ class BatchStateBuilder:
         """One device replay of every staged workflow (canonical order of ``add``)."""
         known = None if self.domain_ids is None else set(self.domain_ids)
         canon = flatten(self.histories, known_domains=known)
+        canon.emit_tasks = self.emit_tasks
         batch = interleave(canon) if self.layout == "interleaved" else canon
         if self.engine is None:
             from .engine import ReplayEngine   # raises EngineUnavailable without the HIP library / a GPU
@@ -529,6 +562,18 @@ def _materialise_one(h: WorkflowHistory, events: List[HistoryEvent], ex, rows, d
         token = h.final_token
     items = [VersionHistoryItem(int(r["event_id"]), int(r["version"])) for r in rows["vh"]]
     ms.version_histories = VersionHistories(0, [VersionHistory(token, items)])
+    for r in rows.get("tasks", ()):
+        src = ev(int(r["src"]))
+        kind = abi.TaskKind(int(r["kind"]))
+        task = Task(kind=kind, version=int(r["version"]), visibility_timestamp=int(r["visibility_ts"]),
+                    event_id=int(r["event_id"]), timeout_type=int(r["aux"]), attempt=int(r["attempt"]))
+        if src is not None:
+            if kind in (abi.TaskKind.Decision, abi.TaskKind.Activity):
+                task.task_list = str(src.get("task_list", ""))
+            elif kind in (abi.TaskKind.StartChild, abi.TaskKind.CancelExecution, abi.TaskKind.SignalExecution):
+                task.target_domain = _domain_id(src.get("domain", ""), own_domain, domain_ids)
+                task.target_workflow_id = str(src.get("workflow_id", ""))
+        (ms.transfer_tasks if kind in TRANSFER_KINDS else ms.timer_tasks).append(task)
     if int(ex["flags"]) & abi.EXEC_CHECKSUM_VALID:
         ms.checksum = Checksum(version=1, flavor=1, value=int(ex["checksum"]).to_bytes(4, "big"))
     return ms

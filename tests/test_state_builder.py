@@ -208,3 +208,19 @@ def test_many_state_builders_share_one_replay(engine):
     assert calls == [50]
     assert [s.get_execution_info().signal_count for s in states] == [i % 4 + 1 for i in range(50)]
     assert all(s.get_execution_info().run_id == f"run-{i}" for i, s in enumerate(states))
+
+
+def test_generated_tasks_materialised(engine):  # MutableState.GetTransferTasks / GetTimerTasks (mutable_state.go:226-228)
+    sb = StateBuilder(batch_builder=BatchStateBuilder(engine))
+    for b in _started_decision():
+        sb.apply_events("d", "req", {}, b)
+    sb.apply_events("d", "req", {}, [ev(ET.ActivityTaskScheduled, 5, activity_id="a", task_list="act-tl",
+                                        schedule_to_start_timeout_seconds=10, schedule_to_close_timeout_seconds=20)])
+    ms = sb.get_mutable_state()
+    kinds = [t.kind for t in ms.get_transfer_tasks()]
+    assert kinds == [abi.TaskKind.RecordWorkflowStarted, abi.TaskKind.Decision, abi.TaskKind.Activity]
+    assert ms.get_transfer_tasks()[2].task_list == "act-tl" and ms.get_transfer_tasks()[2].event_id == 5
+    timers = ms.get_timer_tasks()
+    assert [t.kind for t in timers] == [abi.TaskKind.WorkflowTimeout, abi.TaskKind.DecisionTimeout,
+                                        abi.TaskKind.ActivityTimeout]
+    assert timers[-1].visibility_timestamp == NOW + 5 * SEC + 10 * SEC

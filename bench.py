@@ -101,7 +101,8 @@ def main():
     from cadence_amd import abi
     tier = "replay_lds_small_kernel" if db.c_in.flags & abi.IN_LDS_SMALL else "replay_lds_kernel"
     tail = bool(db.c_in.flags & abi.IN_WAVE_TAIL) and db.c_in.wave_begin < db.n_wf
-    kernel_name = tier + ("<true>" if tail else "<false>")
+    emit = bool(db.c_in.flags & abi.IN_EMIT_TASKS)
+    kernel_name = f"{tier}<{str(tail).lower()}, {str(emit).lower()}>"  # <WAVE_TAIL, EMIT>, as rocprofv3 names it
     ok = bool((res.exec["status"] == 0).all())
     alg_bytes = synth.algorithmic_bytes(batch, res)
     achieved_gbs = alg_bytes / (kernel_avg_ms * 1e-3) / 1e9
@@ -137,7 +138,8 @@ def main():
     if os.path.exists(PROFILE_TRAFFIC):
         try:
             tr = json.load(open(PROFILE_TRAFFIC))
-            if tr.get("workflows") == n_wf and tr.get("events_per_workflow") == n_events // n_wf:
+            if (tr.get("workflows") == n_wf and tr.get("events_per_workflow") == n_events // n_wf
+                    and tr.get("kernel") == kernel_name):
                 line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
         except Exception:
             pass

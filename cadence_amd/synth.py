@@ -175,7 +175,7 @@ def algorithmic_bytes(batch: HistoryBatch, res=None) -> int:
     """Algorithmic HBM bytes of one replay launch (DESIGN.md "Roofline").
 
     reads : 49 B per event (8 columns) + 32 / 48 B per activity / start side record read
-            + the workflow descriptor (160 B) + the branch token bytes checksummed
+            + the workflow descriptor (168 B) + the branch token bytes checksummed
     writes: the execution row (192 B) + 16 B per version-history item + the live pending rows
             (activity 112, timer 40, child 48, request-cancel / signal 32, reset point 16 B)
     """

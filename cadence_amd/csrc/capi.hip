@@ -17,7 +17,7 @@ __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checks
 namespace {
 
 constexpr int kBlock = 256;
-constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 57 KB LDS arena each) per CU x 256 CUs
+constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
 
 struct Timing {
   // [0,1] phase 0, [2,3] phase 1, [4,5] the phase-1 fast-path kernel alone

@@ -583,15 +583,19 @@ struct GlobalTables {
 // ===================================================================================================
 // LDS slot tiers: workflows whose live sets fit the small tier run at 3 blocks/CU (48 KB LDS/block),
 // the large tier at 2 blocks/CU (76.8 KB); anything larger falls back to GlobalTables.
-template <int A, int T, int C, int R, int S, int P>
+template <int A, int T, int C, int R, int S, int P, int LANES_ = kBlock>
 struct Tier {
   static constexpr int A_SLOTS = A, T_SLOTS = T, C_SLOTS = C, R_SLOTS = R, S_SLOTS = S, P_SLOTS = P;
+  static constexpr int LANES = LANES_;  // threads of the block that share the arena
 };
 using SmallTier = Tier<1, 1, 1, 1, 1, 1>;
 using LargeTier = Tier<CRR_LDS_ACT, CRR_LDS_TIMER, CRR_LDS_CHILD, CRR_LDS_RC, CRR_LDS_SIG, CRR_LDS_RP>;
+// retry pass, lane per workflow, one wavefront per block (67 KB arena: 2 blocks/CU)
+using HugeTier = Tier<8, 8, 4, 4, 4, 8, 64>;
 #define CRR_TIER_SLOTS                                                                      \
   static constexpr int A_SLOTS = TIER::A_SLOTS, T_SLOTS = TIER::T_SLOTS, C_SLOTS = TIER::C_SLOTS, \
-                       R_SLOTS = TIER::R_SLOTS, S_SLOTS = TIER::S_SLOTS, P_SLOTS = TIER::P_SLOTS;
+                       R_SLOTS = TIER::R_SLOTS, S_SLOTS = TIER::S_SLOTS, P_SLOTS = TIER::P_SLOTS, \
+                       LANES = TIER::LANES;
 // activity LDS flag bits: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + STARTED; TimerTaskStatus << 8
 constexpr u32 LF_STARTED = 32u;
 constexpr u32 LF_HB_VIS = 64u;  // a heartbeat timer was created: LastHeartbeatTimeoutVisibilityInSeconds set
@@ -601,28 +605,28 @@ constexpr u32 TF_CREATED = 2u;  // timer LDS flag: TaskStatus == TimerTaskStatus
 template <class TIER>
 struct LdsArena {
   CRR_TIER_SLOTS
-  i64 a_sid[A_SLOTS][kBlock];
-  i64 a_sched_t[A_SLOTS][kBlock];
-  i64 a_start_t[A_SLOTS][kBlock];
-  int4 a_to[A_SLOTS][kBlock];    // s2s, s2c, st2c, hb
-  u32 a_key[A_SLOTS][kBlock];
-  u32 a_fl[A_SLOTS][kBlock];
-  int4 a_src[A_SLOTS][kBlock];   // sched step, started step, cancel-requested step, -
-  i64 t_sid[T_SLOTS][kBlock];
-  i64 t_exp[T_SLOTS][kBlock];
-  u32 t_key[T_SLOTS][kBlock];
-  u32 t_fl[T_SLOTS][kBlock];
-  i32 t_src[T_SLOTS][kBlock];
-  i64 c_id[C_SLOTS][kBlock];
-  u32 c_fl[C_SLOTS][kBlock];
-  int2 c_src[C_SLOTS][kBlock];   // initiated step, started step
-  i64 r_id[R_SLOTS][kBlock];
-  u32 r_fl[R_SLOTS][kBlock];
-  i32 r_src[R_SLOTS][kBlock];
-  i64 s_id[S_SLOTS][kBlock];
-  u32 s_fl[S_SLOTS][kBlock];
-  i32 s_src[S_SLOTS][kBlock];
-  int4 p_row[P_SLOTS][kBlock];   // crr_reset_point_row
+  i64 a_sid[A_SLOTS][LANES];
+  i64 a_sched_t[A_SLOTS][LANES];
+  i64 a_start_t[A_SLOTS][LANES];
+  int4 a_to[A_SLOTS][LANES];    // s2s, s2c, st2c, hb
+  u32 a_key[A_SLOTS][LANES];
+  u32 a_fl[A_SLOTS][LANES];
+  int4 a_src[A_SLOTS][LANES];   // sched step, started step, cancel-requested step, -
+  i64 t_sid[T_SLOTS][LANES];
+  i64 t_exp[T_SLOTS][LANES];
+  u32 t_key[T_SLOTS][LANES];
+  u32 t_fl[T_SLOTS][LANES];
+  i32 t_src[T_SLOTS][LANES];
+  i64 c_id[C_SLOTS][LANES];
+  u32 c_fl[C_SLOTS][LANES];
+  int2 c_src[C_SLOTS][LANES];   // initiated step, started step
+  i64 r_id[R_SLOTS][LANES];
+  u32 r_fl[R_SLOTS][LANES];
+  i32 r_src[R_SLOTS][LANES];
+  i64 s_id[S_SLOTS][LANES];
+  u32 s_fl[S_SLOTS][LANES];
+  i32 s_src[S_SLOTS][LANES];
+  int4 p_row[P_SLOTS][LANES];   // crr_reset_point_row
 };
 
 template <class TIER>
@@ -633,6 +637,9 @@ struct LdsTables {
   int t;  // threadIdx.x
   const crr_inputs* in;
   i64 ev_begin;
+  int list = 0;  // scratch list a workflow that outgrows the tier is handed to; < 0: the caller
+                 // replays it again itself (retried)
+  bool retried = false;
 
   __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin) {
     M = arena;
@@ -758,7 +765,7 @@ struct LdsTables {
   }
 
   template <int N>
-  __device__ __forceinline__ i32 find_init(const i64 (*ids)[kBlock], const u32 (*fl)[kBlock], i64 id) const {
+  __device__ __forceinline__ i32 find_init(const i64 (*ids)[LANES], const u32 (*fl)[LANES], i64 id) const {
     i32 hit = -1;
 #pragma unroll
     for (int j = N - 1; j >= 0; --j)
@@ -766,7 +773,7 @@ struct LdsTables {
     return hit;
   }
   template <int N>
-  __device__ __forceinline__ i32 free_init(const u32 (*fl)[kBlock]) const {
+  __device__ __forceinline__ i32 free_init(const u32 (*fl)[LANES]) const {
     i32 hit = -1;
 #pragma unroll
     for (int j = N - 1; j >= 0; --j)
@@ -866,7 +873,7 @@ struct LdsTables {
   }
 
   template <int N, class SwapFn>
-  __device__ __forceinline__ void sort_slots(i64 (*ids)[kBlock], u32 (*fl)[kBlock], i32 n, SwapFn swap_fn) {
+  __device__ __forceinline__ void sort_slots(i64 (*ids)[LANES], u32 (*fl)[LANES], i32 n, SwapFn swap_fn) {
     for (i32 i = 0; i < n; ++i) {
       i32 best = -1;
       i64 bid = 0;
@@ -986,15 +993,16 @@ struct LdsTables {
 
   // Hand a workflow back to the general path: one atomic per wavefront (ballot + mbcnt prefix
   // count compacts the retrying lanes into the scratch list).
-  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) const {
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) {
+    if (list < 0) { retried = true; return; }
     const u64 m = __builtin_amdgcn_ballot_w64(true);
     const u32 lane = threadIdx.x & 63;
     const u32 leader = (u32)__builtin_ctzll(m);
     const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
     u32 base = 0;
-    if (lane == leader) base = atomicAdd(out.scratch, (u32)__builtin_popcountll(m));
+    if (lane == leader) base = atomicAdd(out.scratch + list, (u32)__builtin_popcountll(m));
     base = (u32)__shfl((int)base, (int)leader, 64);
-    out.scratch[retry_slot(in, 0, base + below)] = w;
+    out.scratch[retry_slot(in, list, base + below)] = w;
   }
 };
 
@@ -1859,38 +1867,37 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 
   src.start();
   for (i32 s = 0; s < n_ev; ++s) {
-    if (s == empty_at) FAIL(CRR_ERR_EMPTY_HISTORY, s);  // state_builder.go:98-100
+    // one loop exit for the whole prologue: the checks become a select chain (no divergent branch
+    // per check), and on success vh_last = (id, ver) in every case (new item, same version, first).
     const Ev ev = src.next(s);
     const u32 et = ev.et;
     const i64 id = ev.id;
     const i64 ver = ev.ver;
     const i32 t = et & CRR_ETYPE_MASK;
     if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = id;  // firstEvent := history[0] (:101)
-
-    // :112 UpdateCurrentVersion(event.Version, true) (mutable_state_builder.go:495-533)
-    if (L.state == CRR_STATE_COMPLETED) {
-      if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, s);
-      L.current_version = L.vh_last_ver;
-    } else {
-      L.current_version = ver;
-    }
-    // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
-    if (id < 0 || (ver < 0 && ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, s);
-    if (L.vh_n == 0) {
-      if (G.vh_cap < 1) FAIL(CRR_ERR_CAPACITY, s);
-      L.vh_last_id = id; L.vh_last_ver = ver; L.vh_n = 1;
-    } else if (ver < L.vh_last_ver) {
-      FAIL(CRR_ERR_VH_LOWER_VERSION, s);
-    } else if (id <= L.vh_last_id) {
-      FAIL(CRR_ERR_VH_EVENT_ID_NOT_INCREASING, s);
-    } else if (ver > L.vh_last_ver) {
-      if (L.vh_n >= G.vh_cap) FAIL(CRR_ERR_CAPACITY, s);
-      crr_vh_item* it = G.vh(L.vh_n - 1);
-      it->event_id = L.vh_last_id;
-      it->version = L.vh_last_ver;
-      L.vh_last_id = id; L.vh_last_ver = ver; ++L.vh_n;
-    } else {
+    {
+      const bool completed = L.state == CRR_STATE_COMPLETED;
+      const bool first = L.vh_n == 0;
+      const bool grow = !first && ver > L.vh_last_ver;
+      // :98-100 empty batch; :112 UpdateCurrentVersion (mutable_state_builder.go:495-533)
+      i32 rc0 = s == empty_at ? (i32)CRR_ERR_EMPTY_HISTORY : (completed && first) ? (i32)CRR_ERR_VH_EMPTY : 0;
+      if (rc0 == 0) L.current_version = completed ? L.vh_last_ver : ver;
+      // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
+      const i32 vh_rc = (id < 0 || (ver < 0 && ver != CRR_EMPTY_VERSION)) ? (i32)CRR_ERR_VH_INVALID_ITEM
+                        : first ? (G.vh_cap < 1 ? (i32)CRR_ERR_CAPACITY : 0)
+                        : ver < L.vh_last_ver ? (i32)CRR_ERR_VH_LOWER_VERSION
+                        : id <= L.vh_last_id ? (i32)CRR_ERR_VH_EVENT_ID_NOT_INCREASING
+                        : (grow && L.vh_n >= G.vh_cap) ? (i32)CRR_ERR_CAPACITY : 0;
+      rc0 = rc0 ? rc0 : vh_rc;
+      if (rc0) FAIL(rc0, s);
+      if (grow) {
+        crr_vh_item* it = G.vh(L.vh_n - 1);
+        it->event_id = L.vh_last_id;
+        it->version = L.vh_last_ver;
+      }
+      L.vh_n += (first || grow) ? 1 : 0;
       L.vh_last_id = id;
+      L.vh_last_ver = ver;
     }
     last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
 
@@ -2025,7 +2032,7 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
     Geo G;
     load_geo(G, wfp, out, 1);
-    WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 0>> T;
+    WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 1>> T;  // outgrown: the retry pass's wave list
     T.S.M = &arena.wave[wv];
     T.init();
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
@@ -2092,11 +2099,16 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
   }
 }
 
-// Retry pass, one wavefront per workflow (lane or tail workflows alike; per-workflow stride), over
-// the workflows the fast path handed back (scratch list 0): first with a 57 KB LDS row arena
-// (2 blocks/CU); a live set that outgrows it is replayed again at once over the workflow's own HBM
-// rows (no size limit).  Grid-strides over the list; an empty list costs one load per block.  The
-// last block to finish zeroes the list counter, so the next crr_replay needs no memset.
+// Retry pass over the workflows the fast path handed back (one launch, 64 threads per block,
+// 2 blocks/CU; grid-strided, so an empty retry costs one load per block):
+//   1. long-tail workflows the fast path's per-wave arenas could not hold (scratch list 1), one
+//      wavefront per workflow, first with a 57 KB LDS row arena; a live set that outgrows that is
+//      replayed again at once over the workflow's own HBM rows (no size limit);
+//   2. lane workflows (list 0), lane per workflow again with the 8/8/4/4/4/8-slot LDS tier (gathered
+//      lanes: each reads its own workflow's interleaved columns); a lane that outgrows that replays
+//      its workflow again at once over its HBM rows.
+// Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
+// the list counters, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
 template <class ST>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
@@ -2112,28 +2124,58 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
   replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
 }
+__device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
+                                                 LdsArena<HugeTier>* arena, const u32* crc_tables) {
+  const crr_workflow* wfp = in.wf + w;
+  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  Geo G;
+  load_geo(G, wfp, out, 64);
+  const bool tasks = (in.flags & CRR_IN_EMIT_TASKS) != 0;
+  LdsTables<HugeTier> T;
+  T.list = -1;
+  T.init(arena, &in, wfp->ev_begin);
+  LaneSource S(in.ev, wfp->ev_begin, 64, wfp->ev_count, tasks);
+  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+  if (T.retried) {
+    GlobalTables H;
+    LaneSource S2(in.ev, wfp->ev_begin, 64, wfp->ev_count, tasks);
+    replay_body<true>(in, out, w, wfp, G, H, S2, crc_tables);
+  }
+}
+union RetryArena {
+  LdsArena<HugeTier> lane;
+  BigArena wave;
+};
 __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_outputs out, int phase) {
   __shared__ u32 crc_tables[8 * 256];
-  __shared__ BigArena arena;
-  const u32 n_items = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (n_items == 0) return;  // uniform: nothing was handed back, the counters are already zero
+  __shared__ RetryArena arena;
+  const u32 n0 = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const u32 n1 = __hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
   build_crc_tables(crc_tables);
-  for (u32 i = blockIdx.x; i < n_items; i += gridDim.x) {
-    const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 0, i)]);
+  for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
+    const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
     WaveTables<LdsRows<BigArena, -1>> T;
-    T.S.M = &arena;
+    T.S.M = &arena.wave;
     replay_wave_item(in, out, phase, w, T, crc_tables);
     if (T.retried) {
       WaveTables<HbmRows> H;
       replay_wave_item(in, out, phase, w, H, crc_tables);
     }
   }
-  // every block has read the count: the last one to finish resets it for the next launch
+  __syncthreads();  // the lane arena reuses the wave arena's LDS
+  const u32 start = (blockIdx.x + gridDim.x - (n1 % gridDim.x)) % gridDim.x;  // blocks that did fewer wave items first
+  for (u32 base = start * 64u; base < n0; base += gridDim.x * 64u) {  // 2. lane workflows
+    const u32 i = base + threadIdx.x;
+    if (i < n0) replay_lane_item(in, out, phase, out.scratch[retry_slot(in, 0, i)], &arena.lane, crc_tables);
+  }
+  // every block has read both counts: the last one to finish resets them for the next launch
   if (threadIdx.x == 0) {
     __threadfence();
     const u32 done = atomicAdd(out.scratch + 2, 1u);
     if (done == gridDim.x - 1) {
       __hip_atomic_store(out.scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out.scratch + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(out.scratch + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -152,3 +152,19 @@ def test_decoded_blobs_replay_on_device(engine):
     src = [WorkflowSource(blobs=serialize_history(h), run_id=h.run_id, branch_id=h.branch_id,
                           domain_failover_version=h.domain_failover_version, now_ns=h.now_ns) for h in hs]
     check(engine, interleave(decode_histories(src, known_domains=KNOWN)))
+
+
+def test_retry_routes(engine):
+    """Every route of the retry pass: lane workflows that outgrow the fast tier but fit the 8-slot
+    retry tier, lane workflows that outgrow that too (HBM rows, same lane), and long-tail workflows
+    whose per-wave arena overflows (wavefront pass)."""
+    from cadence_amd.flatten import live_set_bounds
+    hs = synth_mixed.mixed_histories(3000, 31, mean_len=90, multi_version=True, invalid_rate=0.1)
+    b = flatten(hs, known_domains=KNOWN)
+    peak = np.max(np.stack([v for v in live_set_bounds(b).values()]), axis=0)
+    assert ((peak > 2) & (peak <= 4)).sum() > 100      # retried, fit the retry tier
+    assert (peak > 8).sum() > 10                       # retried, outgrow it
+    check(engine, interleave(b, long_threshold=None))
+    lt = flatten(synth_mixed.long_tail_histories(120, 9, max_len=3000, run_cap=1200, caps=None),
+                 known_domains=KNOWN)
+    check(engine, interleave(lt))

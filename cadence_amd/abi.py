@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1
@@ -156,6 +156,7 @@ IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4
 IN_EMIT_TASKS = 8
+IN_TIERED = 16              # lane workflows ordered by expected live-set size (large_begin / wide_begin)
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([
@@ -286,7 +287,7 @@ class CInputs(ctypes.Structure):
     _fields_ = [("ev", CEvents), ("act_side", ctypes.c_void_p), ("start_side", ctypes.c_void_p),
                 ("reset_keys", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("wf", ctypes.c_void_p),
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("wave_begin", ctypes.c_uint32)]
+                ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32)]
 
 
 class COutputs(ctypes.Structure):
@@ -304,4 +305,4 @@ def check_layout(lib):
         got = lib.crr_sizeof(i)
         if got != dt.itemsize:
             raise RuntimeError(f"ABI layout mismatch for struct #{i}: C {got} vs numpy {dt.itemsize}")
-    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 16
+    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 24

@@ -7,8 +7,11 @@
 #include "cadence_replay.h"
 
 namespace crr {
-template <bool WAVE_TAIL, bool EMIT> __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase);
-template <bool WAVE_TAIL, bool EMIT> __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase);
+template <bool WAVE_TAIL, bool EMIT>
+__global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+template <bool WAVE_TAIL, bool EMIT>
+__global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+__global__ void replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
@@ -17,6 +20,10 @@ __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checks
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef CRR_WIDE_GLOBAL
+#define CRR_WIDE_GLOBAL 1
+#endif
+constexpr int kWideBlock = CRR_WIDE_GLOBAL ? 256 : 64;  // replay_wide_kernel's block
 constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
 
 struct Timing {
@@ -49,6 +56,29 @@ bool ensure_events() {
   for (auto& e : g_timing.ev)
     if (hipEventCreate(&e) != hipSuccess) return false;
   g_timing.device = dev;
+  return true;
+}
+
+// Tier segments of one phase run concurrently: two side streams fork from and join back into the
+// caller's stream with events (created once per thread and device).
+struct SideStreams {
+  hipStream_t st[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+  int device = -1;
+};
+thread_local SideStreams g_side;
+
+bool ensure_side_streams() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (g_side.device == dev) return true;
+  if (g_side.device >= 0) return false;  // one device per thread (crr_set_device): keep it simple
+  for (auto& x : g_side.st)
+    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return false;
+  if (hipEventCreateWithFlags(&g_side.fork, hipEventDisableTiming) != hipSuccess) return false;
+  for (auto& e : g_side.join)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+  g_side.device = dev;
   return true;
 }
 
@@ -104,7 +134,6 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
   // fast-path grid: one block per 4 long (wave-tail) workflows, then one per 256 lane workflows
   const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
-  const unsigned lds_grid = (in->n_wf - n_lane + kBlock / 64 - 1) / (kBlock / 64) + (n_lane + kBlock - 1) / kBlock;
   g_timing.valid[0] = g_timing.valid[1] = g_timing.valid[2] = false;
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
@@ -119,17 +148,52 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n], s);
       // task emission is a separate instantiation: the plain replay loop carries none of its registers
       const bool emit = (in->flags & CRR_IN_EMIT_TASKS) != 0;
-      const dim3 g(lds_grid), b(kBlock);
-      if (emit) {
-        if (small && tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, true>), g, b, 0, s, *in, *out, phase);
-        else if (small) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, true>), g, b, 0, s, *in, *out, phase);
-        else if (tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, true>), g, b, 0, s, *in, *out, phase);
-        else hipLaunchKernelGGL((crr::replay_lds_kernel<false, true>), g, b, 0, s, *in, *out, phase);
+      // one fast launch: the wave tail first (optional), then lane workflows [lo, hi)
+      auto launch_fast = [&](hipStream_t s, bool small_tier, bool with_tail, uint32_t lo, uint32_t hi) {
+        const unsigned wave_blocks = with_tail ? (in->n_wf - n_lane + kBlock / 64 - 1) / (kBlock / 64) : 0;
+        const unsigned blocks = wave_blocks + (hi - lo + kBlock - 1) / kBlock;
+        if (blocks == 0) return;
+        const dim3 g(blocks), b(kBlock);
+        if (emit) {
+          if (small_tier && with_tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, true>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else if (small_tier) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, true>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else if (with_tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, true>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else hipLaunchKernelGGL((crr::replay_lds_kernel<false, true>), g, b, 0, s, *in, *out, phase, lo, hi);
+        } else {
+          if (small_tier && with_tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, false>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else if (small_tier) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, false>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else if (with_tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, false>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else hipLaunchKernelGGL((crr::replay_lds_kernel<false, false>), g, b, 0, s, *in, *out, phase, lo, hi);
+        }
+      };
+      if (in->flags & CRR_IN_TIERED) {
+        // segments by expected live-set size: 1 entry per map | 2 | more (the wide tier, 64 per block);
+        // CRR_IN_LDS_SMALL picks the kernel whose per-wave arenas also take the long-history tail
+        const uint32_t lb = in->large_begin < n_lane ? in->large_begin : n_lane;
+        const uint32_t wb = in->wide_begin < lb ? lb : (in->wide_begin < n_lane ? in->wide_begin : n_lane);
+        const bool run_small = lb > 0 || (tail && small), run_large = wb > lb || (tail && !small), run_wide = wb < n_lane;
+        // more than one segment: the others fork onto the side streams (each launch alone leaves
+        // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
+        const bool fork = (int)run_small + (int)run_large + (int)run_wide > 1 && ensure_side_streams();
+        hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s;
+        if (fork) {
+          (void)hipEventRecord(g_side.fork, s);
+          (void)hipStreamWaitEvent(s_large, g_side.fork, 0);
+          (void)hipStreamWaitEvent(s_wide, g_side.fork, 0);
+        }
+        if (run_wide)  // the biggest segment first
+          hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
+                             s_wide, *in, *out, phase, wb, n_lane);
+        launch_fast(s_large, false, tail && !small, lb, wb);
+        launch_fast(s, true, tail && small, 0, lb);
+        if (fork) {
+          (void)hipEventRecord(g_side.join[0], s_large);
+          (void)hipEventRecord(g_side.join[1], s_wide);
+          (void)hipStreamWaitEvent(s, g_side.join[0], 0);
+          (void)hipStreamWaitEvent(s, g_side.join[1], 0);
+        }
       } else {
-        if (small && tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, false>), g, b, 0, s, *in, *out, phase);
-        else if (small) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, false>), g, b, 0, s, *in, *out, phase);
-        else if (tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, false>), g, b, 0, s, *in, *out, phase);
-        else hipLaunchKernelGGL((crr::replay_lds_kernel<false, false>), g, b, 0, s, *in, *out, phase);
+        launch_fast(s, small, tail, 0, n_lane);
       }
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return (int)err;

@@ -2016,7 +2016,7 @@ union BlockArena {
 // Fast path (stride 64): blocks [0, wave_blocks) replay the long-history tail one workflow per
 // wavefront (dispatched first, they run longest), the remaining blocks replay lane per workflow.
 template <class TIER, bool WAVE_TAIL, bool EMIT>
-__device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase) {
+__device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
   __shared__ u32 crc_tables[8 * 256];
@@ -2039,8 +2039,8 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
     return;
   }
-  const u32 w = (blockIdx.x - wave_blocks) * blockDim.x + threadIdx.x;
-  if (w >= n_lane) return;
+  const u32 w = lo + (blockIdx.x - wave_blocks) * blockDim.x + threadIdx.x;  // lanes [lo, hi)
+  if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
   if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   const i64 lane = threadIdx.x & 63;
@@ -2057,21 +2057,21 @@ template <bool WAVE_TAIL, bool EMIT>
 #ifndef CRR_SMALL_WAVES_PER_EU
 #define CRR_SMALL_WAVES_PER_EU 3
 #endif
-__global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<SmallTier, WAVE_TAIL, EMIT>(in, out, phase);
+__global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_lds<SmallTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi);
 }
 template <bool WAVE_TAIL, bool EMIT>
-__global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase) {
-  replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase);
+__global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi);
 }
-template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_small_kernel<true, false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<false, false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<true, false>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_small_kernel<false, true>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_small_kernel<true, true>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<false, true>(crr_inputs, crr_outputs, int);
-template __global__ void replay_lds_kernel<true, true>(crr_inputs, crr_outputs, int);
+template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_small_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_small_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_small_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
 
 // General path over HBM slot tables (any layout).  retry_only: replay the workflows the fast path
 // handed back (scratch list), grid-striding so the launch is cheap when there are none.
@@ -2142,6 +2142,49 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
     replay_body<true>(in, out, w, wfp, G, H, S2, crc_tables);
   }
 }
+// Wide segment (CRR_IN_TIERED): lane workflows [lo, hi) whose live sets the host expects to outgrow
+// the 2-slot LDS tier.
+#ifndef CRR_WIDE_GLOBAL
+#define CRR_WIDE_GLOBAL 1
+#endif
+#if CRR_WIDE_GLOBAL
+// Lane per workflow over the workflows' own HBM rows (GlobalTables: no LDS, so the occupancy is the
+// register-limited one; interleaved rows keep slot j of a group one coalesced run).
+#ifndef CRR_WIDE_WAVES_PER_EU
+#define CRR_WIDE_WAVES_PER_EU 2
+#endif
+__global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase,
+                                                                                    u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  build_crc_tables(crc_tables);
+  const u32 w = lo + blockIdx.x * kBlock + threadIdx.x;
+  if (w >= hi) return;
+  const crr_workflow* wfp = in.wf + w;
+  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  const i64 lane = threadIdx.x & 63;
+  Geo G;
+  load_geo(G, wfp, out, 64);
+  i64 ev_begin = wfp->ev_begin;
+  if ((lo & 63u) == 0) {  // wavefront == one interleaved group: group-uniform geometry in SGPRs
+    uniformize_geo(G, lane);
+    ev_begin = uniform64(ev_begin - lane) + lane;
+  }
+  GlobalTables T;
+  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, (in.flags & CRR_IN_EMIT_TASKS) != 0);
+  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+}
+#else
+// Lane per workflow with the 8/8/4/4/4/8-slot LDS tier (64 per block); a lane that outgrows it
+// replays again at once over HBM rows.
+__global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  __shared__ LdsArena<HugeTier> arena;
+  build_crc_tables(crc_tables);
+  const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
+  if (w >= hi) return;
+  replay_lane_item(in, out, phase, w, &arena, crc_tables);
+}
+#endif
 union RetryArena {
   LdsArena<HugeTier> lane;
   BigArena wave;
@@ -2152,6 +2195,9 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   const u32 n0 = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const u32 n1 = __hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
+#if CRR_EXP & 64  // diagnostics only: leave the handed-back workflows at CRR_INTERNAL_RETRY
+  return;
+#endif
   build_crc_tables(crc_tables);
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
@@ -2164,10 +2210,15 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
     }
   }
   __syncthreads();  // the lane arena reuses the wave arena's LDS
-  const u32 start = (blockIdx.x + gridDim.x - (n1 % gridDim.x)) % gridDim.x;  // blocks that did fewer wave items first
-  for (u32 base = start * 64u; base < n0; base += gridDim.x * 64u) {  // 2. lane workflows
+  // 2. lane workflows, spread over every block (a few handed-back lanes each when there are few:
+  // the gathered loads are latency-bound, so more wavefronts beat fuller ones); blocks that did
+  // fewer wave items take the first chunks
+  const u32 start = (blockIdx.x + gridDim.x - (n1 % gridDim.x)) % gridDim.x;
+  const u32 chunk = min(64u, (n0 + gridDim.x - 1) / gridDim.x);
+  for (u32 base = start * chunk; base < n0; base += gridDim.x * chunk) {
     const u32 i = base + threadIdx.x;
-    if (i < n0) replay_lane_item(in, out, phase, out.scratch[retry_slot(in, 0, i)], &arena.lane, crc_tables);
+    if (threadIdx.x < chunk && i < n0)
+      replay_lane_item(in, out, phase, out.scratch[retry_slot(in, 0, i)], &arena.lane, crc_tables);
   }
   // every block has read both counts: the last one to finish resets them for the next launch
   if (threadIdx.x == 0) {

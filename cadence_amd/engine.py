@@ -120,7 +120,12 @@ class ReplayEngine:
         has_new_run = bool((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()) if batch.n_wf else False
         ci.flags = (abi.IN_HAS_NEW_RUN if has_new_run else 0) | batch.c_flags()
         ci.wave_begin = batch.wave_begin or 0
-        if batch.stride == 64 and fits_small_tier(batch):
+        if batch.tiers is not None:
+            # segments by expected live-set size; LDS_SMALL then only places the wave tail
+            ci.large_begin, ci.wide_begin = batch.tiers
+            if fits_small_tier(batch, lanes=False):
+                ci.flags |= abi.IN_LDS_SMALL
+        elif batch.stride == 64 and fits_small_tier(batch):
             ci.flags |= abi.IN_LDS_SMALL
         co = abi.COutputs()
         T["exec"] = torch.zeros(max(batch.n_wf, 1) * abi.EXEC_ROW.itemsize, dtype=torch.uint8, device=dev)

@@ -11,7 +11,7 @@ code flattens decoded HistoryEvent batches into structure-of-arrays columns").  
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Optional, Sequence
+from typing import Tuple, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -45,6 +45,8 @@ class HistoryBatch:
     wave_begin: Optional[int] = None
     # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
     emit_tasks: bool = False
+    # CRR_IN_TIERED: (large_begin, wide_begin) -- lane workflows ordered by expected live-set size
+    tiers: Optional[Tuple[int, int]] = None
 
     def wf_strides(self) -> np.ndarray:
         """Column / row stride of every workflow."""
@@ -54,7 +56,8 @@ class HistoryBatch:
         return st
 
     def c_flags(self) -> int:
-        return (abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
+        return ((abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
+                | (abi.IN_TIERED if self.tiers is not None else 0))
 
     @property
     def n_wf(self) -> int:
@@ -307,7 +310,8 @@ TASKS_PER_EVENT = {int(ET.WorkflowExecutionStarted): 3, int(ET.DecisionTaskSched
 LONG_HISTORY = 256   # lane per workflow up to ~256 events, a wavefront per workflow above
 
 
-def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[int] = LONG_HISTORY) -> HistoryBatch:
+def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[int] = LONG_HISTORY,
+               tiered: bool = True) -> HistoryBatch:
     """Permute a canonical batch into the device layout.
 
     Workflows are sorted by event count (descending; ties by index) and packed 64 per group.
@@ -315,19 +319,29 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     workflow see CRR_EV_PAD slots.  With ``long_threshold`` (length bucketing), workflows longer
     than it form a tail after the groups: contiguous events and rows (stride 1), one wavefront
     each on the device (``long_threshold=None``: every workflow lane per workflow).  CAN ``aux``
-    references are remapped to device positions.
+    references are remapped to device positions.  ``tiered``: lane workflows are first ordered by
+    the LDS tier their live sets are expected to fit (``live_set_bounds``: 1 entry per map, 2, more;
+    CRR_IN_TIERED), so each segment runs with the tier that holds it instead of being retried.
     """
     assert batch.stride == 1
     n = batch.n_wf
     counts = batch.wf["ev_count"].astype(np.int64)
     order = np.lexsort((np.arange(n), -counts)).astype(np.int64)
-    if long_threshold is not None:
-        is_long = counts[order] > long_threshold
-        perm = np.concatenate([order[~is_long], order[is_long]])   # device pos -> canonical wf
-        n_lane = int((~is_long).sum())
-    else:
-        perm = order
-        n_lane = n
+    is_long = counts[order] > long_threshold if long_threshold is not None else np.zeros(n, bool)
+    lanes = order[~is_long]
+    tier = tier_classes(batch) if (tiered and n) else np.zeros(n, np.int64)
+    if tiered:
+        lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
+    perm = np.concatenate([lanes, order[is_long]])                # device pos -> canonical wf
+    n_lane = int(lanes.size)
+    tiers = None
+    if tiered:
+        lane_tier = tier[perm[:n_lane]]
+        n0, n01 = int((lane_tier == 0).sum()), int((lane_tier <= 1).sum())
+        # segment boundaries on group boundaries, rounded down (a mixed group takes the larger tier)
+        lb = n_lane if n0 == n_lane else n0 // wave * wave
+        wb = n_lane if n01 == n_lane else n01 // wave * wave
+        tiers = (lb, max(wb, lb))
     inv = np.empty(n, np.int64)
     inv[perm] = np.arange(n)
     n_groups = (n_lane + wave - 1) // wave
@@ -390,7 +404,8 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
-                       wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks)
+                       wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks,
+                       tiers=tiers)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)
         cap[:n_lane] = wf[cap_f][:n_lane]
@@ -449,6 +464,7 @@ def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, 
 
 
 SMALL_TIER = {"act": 1, "timer": 1, "child": 1, "rc": 1, "sig": 1, "rp": 1}
+LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # CRR_LDS_* defaults
 
 
 def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
@@ -514,11 +530,22 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
 WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp": 24}
 
 
-def fits_small_tier(batch: HistoryBatch) -> bool:
+def tier_classes(batch: HistoryBatch) -> np.ndarray:
+    """Per workflow: 0 if its live sets are expected to fit the 1-slot tier, 1 the 2-slot tier, else 2."""
+    b = live_set_bounds(batch)
+    small = np.ones(batch.n_wf, bool)
+    large = np.ones(batch.n_wf, bool)
+    for k in SMALL_TIER:
+        small &= b[k] <= SMALL_TIER[k]
+        large &= b[k] <= LARGE_TIER[k]
+    return np.where(small, 0, np.where(large, 1, 2)).astype(np.int64)
+
+
+def fits_small_tier(batch: HistoryBatch, lanes: bool = True) -> bool:
     """Whether the 3-blocks/CU LDS tier holds every workflow's live sets (lane part: 1 entry per
-    map; wave tail: the small per-wave arena)."""
+    map, unless ``lanes`` is False; wave tail: the small per-wave arena)."""
     b = live_set_bounds(batch)
     nl = batch.n_wf if batch.wave_begin is None else batch.wave_begin
-    lane_ok = all(bool((b[k][:nl] <= v).all()) for k, v in SMALL_TIER.items())
+    lane_ok = not lanes or all(bool((b[k][:nl] <= v).all()) for k, v in SMALL_TIER.items())
     tail_ok = all(bool((b[k][nl:] <= v).all()) for k, v in WAVE_SMALL_TIER.items())
     return lane_ok and tail_ok

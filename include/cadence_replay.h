@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define CRR_ABI_VERSION 2
+#define CRR_ABI_VERSION 3
 
 /* ---- constants restated from the reference ------------------------------------------------ */
 /* common/constants.go:30-58 */
@@ -267,6 +267,10 @@ typedef struct crr_inputs {
     uint32_t                 wave_begin;   /* CRR_IN_WAVE_TAIL: workflows [wave_begin, n_wf) are long
                                               histories laid out contiguously (stride 1), replayed one
                                               per wavefront; [0, wave_begin) use `stride` */
+    uint32_t                 large_begin;  /* CRR_IN_TIERED: lane workflows [0, large_begin) are expected */
+    uint32_t                 wide_begin;   /* to hold <= 1 pending entry per map, [large_begin,
+                                              wide_begin) <= 2, [wide_begin, lanes) more (multiples of
+                                              64 except at the end) */
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
@@ -276,6 +280,10 @@ typedef struct crr_inputs {
 #define CRR_IN_WAVE_TAIL   4u   /* length bucketing (stride-64 batches only): workflows
                                    [wave_begin, n_wf) are replayed one per wavefront */
 #define CRR_IN_EMIT_TASKS  8u   /* write the transfer / timer tasks ApplyEvents generates (crr_task_row) */
+#define CRR_IN_TIERED     16u   /* stride-64 batches: lane workflows are ordered by expected live-set
+                                   size (large_begin / wide_begin); each segment is launched with the
+                                   LDS tier that holds it (1, 2 or 8 entries per map).  A hint like
+                                   CRR_IN_LDS_SMALL (which it overrides): speed only, never results */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (192 B). */

@@ -164,7 +164,11 @@ def test_retry_routes(engine):
     peak = np.max(np.stack([v for v in live_set_bounds(b).values()]), axis=0)
     assert ((peak > 2) & (peak <= 4)).sum() > 100      # retried, fit the retry tier
     assert (peak > 8).sum() > 10                       # retried, outgrow it
-    check(engine, interleave(b, long_threshold=None))
+    check(engine, interleave(b, long_threshold=None, tiered=False))   # fast tier, then the retry pass
+    tb = interleave(b, long_threshold=None)                            # tier segments: small | large | wide
+    assert 0 < tb.tiers[0] <= tb.tiers[1] < tb.n_wf
+    check(engine, tb)
     lt = flatten(synth_mixed.long_tail_histories(120, 9, max_len=3000, run_cap=1200, caps=None),
                  known_domains=KNOWN)
     check(engine, interleave(lt))
+    check(engine, interleave(lt, tiered=False))

@@ -149,3 +149,30 @@ def test_host_library_exports_every_decode_symbol():
     lib = ctypes.CDLL(HOST_LIB)
     for s in syms:
         assert hasattr(lib, s), s
+
+
+def test_interleave_tier_segments():
+    """CRR_IN_TIERED layout: lane workflows ordered by expected tier (1 / 2 / more entries per
+    map), longest first within a tier; segment boundaries on group boundaries (a mixed group is
+    given the larger tier); the wave tail stays longest first."""
+    from cadence_amd.flatten import tier_classes
+    hs = synth_mixed.mixed_histories(1000, 33, mean_len=50)
+    b = flatten(hs)
+    cls = tier_classes(b)
+    assert len(np.unique(cls)) == 3
+    ib = interleave(b, long_threshold=70)
+    lb, wb = ib.tiers
+    nl = ib.wave_begin
+    c = cls[ib.perm[:nl]]
+    assert (np.diff(c) >= 0).all()
+    assert lb % 64 == 0 and (wb % 64 == 0 or wb == nl) and lb <= wb <= nl
+    assert (c[:lb] == 0).all() and (c[lb:wb] <= 1).all()
+    assert ib.c_flags() & abi.IN_TIERED
+    cnt = ib.wf["ev_count"]
+    assert (np.diff(cnt[nl:]) <= 0).all()
+    for k in range(3):
+        seg = cnt[:nl][c == k]
+        assert (np.diff(seg) <= 0).all()
+    # one tier only: no segments beyond the lanes
+    ic = interleave(synth.activity_chain(1000, 2, 3))
+    assert ic.tiers == (ic.n_wf, ic.n_wf)

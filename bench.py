@@ -144,12 +144,35 @@ def main():
         except Exception:
             pass
 
+    if rank == 0 and world == 1:
+        line["pcie_inclusive"] = pcie_inclusive(eng, batch, torch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, res, batch, k)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pcie_inclusive(eng, batch, torch, reps=3):
+    """SURVEY.md §8d's second figure: one replay with host buffers -- device allocation + H2D of the
+    columns, side records and descriptors, the replay, D2H of the execution rows and the slot
+    tables -- never the headline `value` (which has the inputs resident in HBM)."""
+    times = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        db = eng.upload(batch)
+        eng.launch(db)
+        r = eng.download(db)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        del db, r
+    t = float(np.median(times))
+    h2d = sum(v.nbytes for v in batch.cols.values()) + batch.act_side.nbytes + batch.start_side.nbytes \
+        + batch.arena.nbytes + batch.wf.nbytes
+    return {"events_per_s": batch.n_events / t, "ms": t * 1e3, "h2d_bytes": int(h2d),
+            "note": "pageable host buffers, allocation + upload + replay + download of exec rows and slot tables"}
 
 
 def cpu_baseline(args, gpu_res, gpu_batch, k):

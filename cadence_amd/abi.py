@@ -152,6 +152,7 @@ ROW_RESETTABLE = 16
 
 WF_FLAG_NEW_RUN = 1
 WF_FLAG_REFRESH_TASKS = 2      # Rebuild's RefreshTasks state effects after the replay
+WF_FLAG_BIG_LIVE_SET = 4       # hint: long-tail workflow expected to outgrow the fast per-wave arenas
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4

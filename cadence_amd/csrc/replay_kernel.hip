@@ -1239,8 +1239,32 @@ struct WaveTables {
     return find(P_(), L.n_rp, [&](const crr_reset_point_row& r) { return r.key == key; }) >= 0;
   }
 
-  // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type))
+  // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type)).
+  // Few candidate lanes (the usual case): a scalar pass over them with readlane; many: a shuffle
+  // tree (each level is an LDS-crossbar round trip, ~6x the cost of one readlane step).
+  __device__ __forceinline__ static i64 readlane64(i64 v, i32 l) {
+    const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
+    const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
+    return (i64)(((u64)hi << 32) | lo);
+  }
   __device__ __forceinline__ static void wave_min(BestTimer& B) {
+    u64 m = __builtin_amdgcn_ballot_w64(B.have);
+    if (__builtin_popcountll(m) <= 12) {
+      BestTimer R;
+      while (m) {
+        const i32 l = (i32)__builtin_ctzll(m);
+        m &= m - 1;
+        const i64 t = readlane64(B.t, l), e = readlane64(B.e, l);
+        const i32 y = (i32)__builtin_amdgcn_readlane((u32)B.y, l);
+        if (!R.have || seq_less(t, e, y, R.t, R.e, R.y)) {
+          R.have = true; R.t = t; R.e = e; R.y = y;
+          R.j = (i32)__builtin_amdgcn_readlane((u32)B.j, l);
+          R.created = __builtin_amdgcn_readlane((u32)B.created, l) != 0;
+        }
+      }
+      B = R;
+      return;
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       BestTimer o;
@@ -2035,6 +2059,11 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 1>> T;  // outgrown: the retry pass's wave list
     T.S.M = &arena.wave[wv];
     T.init();
+    if (wfp->flags & CRR_WF_FLAG_BIG_LIVE_SET) {  // expected to outgrow this arena: one replay, in the retry pass
+      out.exec[w].status = CRR_INTERNAL_RETRY;
+      T.retry_push(in, out, w);
+      return;
+    }
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
     replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
     return;

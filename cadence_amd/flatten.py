@@ -329,7 +329,8 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     order = np.lexsort((np.arange(n), -counts)).astype(np.int64)
     is_long = counts[order] > long_threshold if long_threshold is not None else np.zeros(n, bool)
     lanes = order[~is_long]
-    tier = tier_classes(batch) if (tiered and n) else np.zeros(n, np.int64)
+    bounds = live_set_bounds(batch) if (tiered and n) else None
+    tier = tier_classes(batch, bounds) if (tiered and n) else np.zeros(n, np.int64)
     if tiered:
         lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
     perm = np.concatenate([lanes, order[is_long]])                # device pos -> canonical wf
@@ -401,6 +402,12 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
 
     wf = batch.wf[perm].copy()
     wf["ev_begin"] = dev_begin
+    if tiered and n_lane < n:  # long-tail workflows no fast per-wave arena holds: straight to the retry pass
+        tb = {k: v[perm[n_lane:]] for k, v in (bounds if bounds is not None else live_set_bounds(batch)).items()}
+        big = np.zeros(n - n_lane, bool)
+        for k, cap in WAVE_LARGE_TIER.items():
+            big |= tb[k] > cap
+        wf["flags"][n_lane:] |= np.where(big, abi.WF_FLAG_BIG_LIVE_SET, 0).astype(wf["flags"].dtype)
     out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
@@ -468,8 +475,8 @@ LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # 
 
 
 def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
-    """Approximate peak live-set size per workflow and map (running inserts - deletes; reset points:
-    distinct non-empty binary checksums + previous points).  Used only to pick the LDS tier: a
+    """Approximate peak live-set size per workflow and map (running inserts - deletes of inserted
+    keys; reset points: distinct non-empty binary checksums + previous points).  Used only to pick the LDS tier: a
     workflow that outgrows its tier is replayed by the general path, so this affects speed only."""
     n = batch.n_wf
     cnt = batch.wf["ev_count"].astype(np.int64)
@@ -498,6 +505,23 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
         lut[[int(x) for x in ins]] = 1
         lut[[int(x) for x in dels]] = -1
         d = lut[t]
+        # a delete of an entry that is not live only logs an inconsistency (Go): count a delete only
+        # if its key was inserted earlier in the workflow (and, for ID-keyed maps, deleted once)
+        dpos = np.nonzero(d < 0)[0]
+        if dpos.size:
+            ipos = np.nonzero(d > 0)[0]
+            col, ins_col = ("key", "key") if name == "timer" else ("ref", "event_id")
+            mask40 = np.int64((1 << 40) - 1)
+            ik = (wf_of[ipos].astype(np.int64) << 40) | (batch.cols[ins_col][idx[ipos]].astype(np.int64) & mask40)
+            dk = (wf_of[dpos].astype(np.int64) << 40) | (batch.cols[col][idx[dpos]].astype(np.int64) & mask40)
+            valid = np.isin(dk, ik)
+            if name != "timer":
+                valid &= batch.cols["ref"][idx[dpos]] < batch.cols["event_id"][idx[dpos]]
+                first = np.zeros(dpos.size, bool)
+                first[np.unique(dk, return_index=True)[1]] = True
+                valid &= first
+            d = d.copy()
+            d[dpos[~valid]] = 0
         if d.size == 0 or not d.any():
             out[name] = np.zeros(n, np.int64)
             continue
@@ -507,16 +531,13 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
         mx = np.zeros(n, np.int64)
         mx[nz] = np.maximum.reduceat(rel, starts[nz])
         out[name] = np.maximum(mx, 0)
-    # reset points: non-empty binary checksums that differ from the workflow's previous one (an upper
-    # bound of the distinct count) + points carried over by the start event
+    # reset points: distinct non-empty binary checksums per workflow (the replay path never evicts:
+    # maxResetPoints = MaxInt32) + points carried over by the start event
     dtc_pos = np.nonzero((t == ET.DecisionTaskCompleted) & (batch.cols["key"][idx] != 0))[0]
     rp = np.zeros(n, np.int64)
     if dtc_pos.size:
-        keys = batch.cols["key"][idx[dtc_pos]]
-        wfs = wf_of[dtc_pos]
-        new_key = np.ones(dtc_pos.size, bool)
-        new_key[1:] = (keys[1:] != keys[:-1]) | (wfs[1:] != wfs[:-1])
-        rp = np.bincount(wfs[new_key], minlength=n).astype(np.int64)
+        pair = (wf_of[dtc_pos].astype(np.uint64) << np.uint64(32)) | batch.cols["key"][idx[dtc_pos]].astype(np.uint64)
+        rp = np.bincount((np.unique(pair) >> np.uint64(32)).astype(np.int64), minlength=n).astype(np.int64)
     prev = np.zeros(n, np.int64)
     st = t == ET.WorkflowExecutionStarted
     if st.any():
@@ -528,11 +549,12 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
 
 # per-wave LDS arenas of the wave-per-workflow tail (replay_kernel.hip WaveTier<SmallTier>)
 WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp": 24}
+WAVE_LARGE_TIER = {"act": 64, "timer": 48, "child": 24, "rc": 16, "sig": 16, "rp": 32}   # WaveTier<LargeTier>
 
 
-def tier_classes(batch: HistoryBatch) -> np.ndarray:
+def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:
     """Per workflow: 0 if its live sets are expected to fit the 1-slot tier, 1 the 2-slot tier, else 2."""
-    b = live_set_bounds(batch)
+    b = live_set_bounds(batch) if bounds is None else bounds
     small = np.ones(batch.n_wf, bool)
     large = np.ones(batch.n_wf, bool)
     for k in SMALL_TIER:
@@ -544,8 +566,10 @@ def tier_classes(batch: HistoryBatch) -> np.ndarray:
 def fits_small_tier(batch: HistoryBatch, lanes: bool = True) -> bool:
     """Whether the 3-blocks/CU LDS tier holds every workflow's live sets (lane part: 1 entry per
     map, unless ``lanes`` is False; wave tail: the small per-wave arena)."""
-    b = live_set_bounds(batch)
     nl = batch.n_wf if batch.wave_begin is None else batch.wave_begin
+    if not lanes and nl == batch.n_wf:
+        return True
+    b = live_set_bounds(batch)
     lane_ok = not lanes or all(bool((b[k][:nl] <= v).all()) for k, v in SMALL_TIER.items())
     tail_ok = all(bool((b[k][nl:] <= v).all()) for k, v in WAVE_SMALL_TIER.items())
     return lane_ok and tail_ok

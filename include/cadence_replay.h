@@ -253,6 +253,10 @@ typedef struct crr_workflow {
  * (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): clear every pending activity's
  * TimerTaskStatus and user timer's TaskStatus, then CreateNextActivityTimer / CreateNextUserTimer. */
 #define CRR_WF_FLAG_REFRESH_TASKS 2
+/* Hint (speed only): the host expects this long-tail workflow's live sets to outgrow the fast
+ * path's per-wave LDS arenas, so the fast kernels hand it straight to the retry pass instead of
+ * replaying it twice. */
+#define CRR_WF_FLAG_BIG_LIVE_SET 4
 
 typedef struct crr_inputs {
     crr_events               ev;

@@ -10,4 +10,8 @@ timeout -k 10 300 python tools/prof_kernel.py --reps 7 >> gpurun_out/check.jsonl
 rc=$?; echo "config2 timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python tools/prof_kernel.py --mixed --wf ${MIXED_WF:-200000} --reps 5 >> gpurun_out/check.jsonl 2>> gpurun_out/check.err
 rc=$?; echo "mixed timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
+if [ -n "${LT_N:-}" ]; then
+  timeout -k 10 400 python -u tools/prof_longtail.py --n $LT_N --thresholds 256 >> gpurun_out/check_lt.jsonl 2>> gpurun_out/check.err
+  rc=$?; echo "longtail timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
+fi
 bash scripts/gpu_exp.sh

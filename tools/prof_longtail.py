@@ -22,7 +22,10 @@ def main():
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--thresholds", default="none,256,64")
     p.add_argument("--unbounded", action="store_true", help="unbounded pending sets (random walk)")
+    p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
     a = p.parse_args()
+    if a.lib:
+        os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
     import numpy as np
     import torch
     from cadence_amd import synth_mixed
@@ -49,7 +52,7 @@ def main():
             eng.launch(db)
             torch.cuda.synchronize()
             k = eng.last_kernel_ms()
-            ms.append(sum(x for x in k if x > 0))
+            ms.append(sum(x for x in k[:2] if x > 0))   # phase 0 (new runs) + phase 1; k[2] is inside k[1]
         res = eng.download(db)
         retries = [int(x) for x in db.tensors["scratch"][:2].cpu().tolist()]
         same = None
@@ -58,7 +61,7 @@ def main():
         else:
             same = not diff_results(ref[0], ref[1], ib, res)
         med = float(np.median(ms))
-        print(json.dumps({"threshold": th, "unbounded": a.unbounded, "workflows": b.n_wf, "events": int(cnt.sum()), "max_len": int(cnt.max()),
+        print(json.dumps({"lib": a.lib, "threshold": th, "unbounded": a.unbounded, "workflows": b.n_wf, "events": int(cnt.sum()), "max_len": int(cnt.max()),
                           "wave_tail": int(b.n_wf - (ib.wave_begin if ib.wave_begin is not None else b.n_wf)),
                           "kernel_ms": ms, "median_ms": med, "events_per_s": float(cnt.sum()) / (med * 1e-3),
                           "ok": int((res.exec["status"] == 0).sum()), "same_as_first": same,

@@ -152,7 +152,6 @@ ROW_RESETTABLE = 16
 
 WF_FLAG_NEW_RUN = 1
 WF_FLAG_REFRESH_TASKS = 2      # Rebuild's RefreshTasks state effects after the replay
-WF_FLAG_BIG_LIVE_SET = 4       # hint: long-tail workflow expected to outgrow the fast per-wave arenas
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4
@@ -288,7 +287,8 @@ class CInputs(ctypes.Structure):
     _fields_ = [("ev", CEvents), ("act_side", ctypes.c_void_p), ("start_side", ctypes.c_void_p),
                 ("reset_keys", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("wf", ctypes.c_void_p),
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32)]
+                ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
+                ("big_begin", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class COutputs(ctypes.Structure):
@@ -306,4 +306,4 @@ def check_layout(lib):
         got = lib.crr_sizeof(i)
         if got != dt.itemsize:
             raise RuntimeError(f"ABI layout mismatch for struct #{i}: C {got} vs numpy {dt.itemsize}")
-    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 24
+    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 32

@@ -12,6 +12,7 @@ __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, uin
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+__global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
@@ -59,11 +60,12 @@ bool ensure_events() {
   return true;
 }
 
-// Tier segments of one phase run concurrently: two side streams fork from and join back into the
+// Tier segments of one phase run concurrently: side streams fork from and join back into the
 // caller's stream with events (created once per thread and device).
+constexpr int kSide = 3;
 struct SideStreams {
-  hipStream_t st[2] = {nullptr, nullptr};
-  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+  hipStream_t st[kSide] = {};
+  hipEvent_t fork = nullptr, join[kSide] = {};
   int device = -1;
 };
 thread_local SideStreams g_side;
@@ -148,9 +150,12 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n], s);
       // task emission is a separate instantiation: the plain replay loop carries none of its registers
       const bool emit = (in->flags & CRR_IN_EMIT_TASKS) != 0;
+      // long-tail workflows [tail_end, n_wf) that no fast per-wave arena is expected to hold
+      const uint32_t tail_end = ((in->flags & CRR_IN_TIERED) && in->big_begin >= n_lane && in->big_begin < in->n_wf)
+                                    ? in->big_begin : in->n_wf;
       // one fast launch: the wave tail first (optional), then lane workflows [lo, hi)
       auto launch_fast = [&](hipStream_t s, bool small_tier, bool with_tail, uint32_t lo, uint32_t hi) {
-        const unsigned wave_blocks = with_tail ? (in->n_wf - n_lane + kBlock / 64 - 1) / (kBlock / 64) : 0;
+        const unsigned wave_blocks = with_tail ? (tail_end - n_lane + kBlock / 64 - 1) / (kBlock / 64) : 0;
         const unsigned blocks = wave_blocks + (hi - lo + kBlock - 1) / kBlock;
         if (blocks == 0) return;
         const dim3 g(blocks), b(kBlock);
@@ -172,25 +177,29 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         const uint32_t lb = in->large_begin < n_lane ? in->large_begin : n_lane;
         const uint32_t wb = in->wide_begin < lb ? lb : (in->wide_begin < n_lane ? in->wide_begin : n_lane);
         const bool run_small = lb > 0 || (tail && small), run_large = wb > lb || (tail && !small), run_wide = wb < n_lane;
+        const bool run_big = tail_end < in->n_wf;
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
-        const bool fork = (int)run_small + (int)run_large + (int)run_wide > 1 && ensure_side_streams();
-        hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s;
+        const bool fork =
+            (int)run_small + (int)run_large + (int)run_wide + (int)run_big > 1 && ensure_side_streams();
+        hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
         if (fork) {
           (void)hipEventRecord(g_side.fork, s);
-          (void)hipStreamWaitEvent(s_large, g_side.fork, 0);
-          (void)hipStreamWaitEvent(s_wide, g_side.fork, 0);
+          for (hipStream_t x : g_side.st) (void)hipStreamWaitEvent(x, g_side.fork, 0);
         }
-        if (run_wide)  // the biggest segment first
+        if (run_big)  // the longest histories first
+          hipLaunchKernelGGL(crr::replay_big_kernel, dim3(in->n_wf - tail_end), dim3(64), 0, s_big, *in, *out, phase,
+                             tail_end, in->n_wf);
+        if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, wb, n_lane);
         launch_fast(s_large, false, tail && !small, lb, wb);
         launch_fast(s, true, tail && small, 0, lb);
         if (fork) {
-          (void)hipEventRecord(g_side.join[0], s_large);
-          (void)hipEventRecord(g_side.join[1], s_wide);
-          (void)hipStreamWaitEvent(s, g_side.join[0], 0);
-          (void)hipStreamWaitEvent(s, g_side.join[1], 0);
+          for (int i = 0; i < kSide; ++i) {
+            (void)hipEventRecord(g_side.join[i], g_side.st[i]);
+            (void)hipStreamWaitEvent(s, g_side.join[i], 0);
+          }
         }
       } else {
         launch_fast(s, small, tail, 0, n_lane);

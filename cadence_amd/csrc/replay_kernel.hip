@@ -2023,6 +2023,9 @@ done_events:
 __device__ __forceinline__ u32 lane_count(const crr_inputs& in) {
   return (in.flags & CRR_IN_WAVE_TAIL) ? in.wave_begin : in.n_wf;
 }
+__device__ __forceinline__ u32 tail_count_end(const crr_inputs& in) {
+  return ((in.flags & CRR_IN_TIERED) && in.big_begin >= in.wave_begin && in.big_begin < in.n_wf) ? in.big_begin : in.n_wf;
+}
 __device__ __forceinline__ i64 wf_stride(const crr_inputs& in, u32 w) {
   return ((in.flags & CRR_IN_WAVE_TAIL) && w >= in.wave_begin) ? 1 : (i64)in.stride;
 }
@@ -2047,11 +2050,12 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   __shared__ BlockArena<TIER> arena;
   build_crc_tables(crc_tables);
   const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
-  const u32 wave_blocks = WAVE_TAIL ? (in.n_wf - n_lane + kWavesPerBlock - 1) / kWavesPerBlock : 0;
+  const u32 tail_end = WAVE_TAIL ? tail_count_end(in) : in.n_wf;  // [tail_end, n_wf): replay_big_kernel
+  const u32 wave_blocks = WAVE_TAIL ? (tail_end - n_lane + kWavesPerBlock - 1) / kWavesPerBlock : 0;
   if (WAVE_TAIL && blockIdx.x < wave_blocks) {
     const u32 wv = (u32)uniform32((i32)(threadIdx.x >> 6));
     const u32 w = n_lane + blockIdx.x * kWavesPerBlock + wv;
-    if (w >= in.n_wf) return;
+    if (w >= tail_end) return;
     const crr_workflow* wfp = in.wf + w;
     if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
     Geo G;
@@ -2059,11 +2063,7 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 1>> T;  // outgrown: the retry pass's wave list
     T.S.M = &arena.wave[wv];
     T.init();
-    if (wfp->flags & CRR_WF_FLAG_BIG_LIVE_SET) {  // expected to outgrow this arena: one replay, in the retry pass
-      out.exec[w].status = CRR_INTERNAL_RETRY;
-      T.retry_push(in, out, w);
-      return;
-    }
+
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
     replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
     return;
@@ -2214,6 +2214,23 @@ __global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outp
   replay_lane_item(in, out, phase, w, &arena, crc_tables);
 }
 #endif
+// Long-tail workflows the host expects to outgrow the fast kernels' per-wave arenas
+// (CRR_IN_TIERED, [big_begin, n_wf)): one wavefront each with the 57 KB row arena, then HBM rows;
+// launched next to the fast kernels, so the longest of them is not replayed after them.
+__global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  __shared__ BigArena arena;
+  const u32 w = lo + blockIdx.x;
+  if (w >= hi) return;
+  build_crc_tables(crc_tables);
+  WaveTables<LdsRows<BigArena, -1>> T;
+  T.S.M = &arena;
+  replay_wave_item(in, out, phase, w, T, crc_tables);
+  if (T.retried) {
+    WaveTables<HbmRows> H;
+    replay_wave_item(in, out, phase, w, H, crc_tables);
+  }
+}
 union RetryArena {
   LdsArena<HugeTier> lane;
   BigArena wave;

@@ -120,9 +120,10 @@ class ReplayEngine:
         has_new_run = bool((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()) if batch.n_wf else False
         ci.flags = (abi.IN_HAS_NEW_RUN if has_new_run else 0) | batch.c_flags()
         ci.wave_begin = batch.wave_begin or 0
+        ci.big_begin = batch.n_wf
         if batch.tiers is not None:
             # segments by expected live-set size; LDS_SMALL then only places the wave tail
-            ci.large_begin, ci.wide_begin = batch.tiers
+            ci.large_begin, ci.wide_begin, ci.big_begin = batch.tiers
             if fits_small_tier(batch, lanes=False):
                 ci.flags |= abi.IN_LDS_SMALL
         elif batch.stride == 64 and fits_small_tier(batch):

@@ -45,8 +45,9 @@ class HistoryBatch:
     wave_begin: Optional[int] = None
     # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
     emit_tasks: bool = False
-    # CRR_IN_TIERED: (large_begin, wide_begin) -- lane workflows ordered by expected live-set size
-    tiers: Optional[Tuple[int, int]] = None
+    # CRR_IN_TIERED: (large_begin, wide_begin, big_begin) -- lane workflows ordered by expected
+    # live-set size; long-tail workflows no fast per-wave arena is expected to hold from big_begin on
+    tiers: Optional[Tuple[int, int, int]] = None
 
     def wf_strides(self) -> np.ndarray:
         """Column / row stride of every workflow."""
@@ -329,11 +330,18 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     order = np.lexsort((np.arange(n), -counts)).astype(np.int64)
     is_long = counts[order] > long_threshold if long_threshold is not None else np.zeros(n, bool)
     lanes = order[~is_long]
+    longs = order[is_long]
     bounds = live_set_bounds(batch) if (tiered and n) else None
     tier = tier_classes(batch, bounds) if (tiered and n) else np.zeros(n, np.int64)
+    n_big = 0
     if tiered:
         lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
-    perm = np.concatenate([lanes, order[is_long]])                # device pos -> canonical wf
+        big = np.zeros(longs.size, bool)                          # the tail: arena-sized first, then big
+        for k, cap in WAVE_LARGE_TIER.items():
+            big |= bounds[k][longs] > cap
+        longs = np.concatenate([longs[~big], longs[big]])
+        n_big = int(big.sum())
+    perm = np.concatenate([lanes, longs])                          # device pos -> canonical wf
     n_lane = int(lanes.size)
     tiers = None
     if tiered:
@@ -342,7 +350,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
         # segment boundaries on group boundaries, rounded down (a mixed group takes the larger tier)
         lb = n_lane if n0 == n_lane else n0 // wave * wave
         wb = n_lane if n01 == n_lane else n01 // wave * wave
-        tiers = (lb, max(wb, lb))
+        tiers = (lb, max(wb, lb), n - n_big)
     inv = np.empty(n, np.int64)
     inv[perm] = np.arange(n)
     n_groups = (n_lane + wave - 1) // wave
@@ -402,12 +410,6 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
 
     wf = batch.wf[perm].copy()
     wf["ev_begin"] = dev_begin
-    if tiered and n_lane < n:  # long-tail workflows no fast per-wave arena holds: straight to the retry pass
-        tb = {k: v[perm[n_lane:]] for k, v in (bounds if bounds is not None else live_set_bounds(batch)).items()}
-        big = np.zeros(n - n_lane, bool)
-        for k, cap in WAVE_LARGE_TIER.items():
-            big |= tb[k] > cap
-        wf["flags"][n_lane:] |= np.where(big, abi.WF_FLAG_BIG_LIVE_SET, 0).astype(wf["flags"].dtype)
     out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
@@ -567,9 +569,10 @@ def fits_small_tier(batch: HistoryBatch, lanes: bool = True) -> bool:
     """Whether the 3-blocks/CU LDS tier holds every workflow's live sets (lane part: 1 entry per
     map, unless ``lanes`` is False; wave tail: the small per-wave arena)."""
     nl = batch.n_wf if batch.wave_begin is None else batch.wave_begin
-    if not lanes and nl == batch.n_wf:
+    te = batch.tiers[2] if batch.tiers is not None else batch.n_wf   # [te, n): replay_big_kernel
+    if not lanes and nl == te:
         return True
     b = live_set_bounds(batch)
     lane_ok = not lanes or all(bool((b[k][:nl] <= v).all()) for k, v in SMALL_TIER.items())
-    tail_ok = all(bool((b[k][nl:] <= v).all()) for k, v in WAVE_SMALL_TIER.items())
+    tail_ok = all(bool((b[k][nl:te] <= v).all()) for k, v in WAVE_SMALL_TIER.items())
     return lane_ok and tail_ok

@@ -253,10 +253,6 @@ typedef struct crr_workflow {
  * (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): clear every pending activity's
  * TimerTaskStatus and user timer's TaskStatus, then CreateNextActivityTimer / CreateNextUserTimer. */
 #define CRR_WF_FLAG_REFRESH_TASKS 2
-/* Hint (speed only): the host expects this long-tail workflow's live sets to outgrow the fast
- * path's per-wave LDS arenas, so the fast kernels hand it straight to the retry pass instead of
- * replaying it twice. */
-#define CRR_WF_FLAG_BIG_LIVE_SET 4
 
 typedef struct crr_inputs {
     crr_events               ev;
@@ -274,7 +270,11 @@ typedef struct crr_inputs {
     uint32_t                 large_begin;  /* CRR_IN_TIERED: lane workflows [0, large_begin) are expected */
     uint32_t                 wide_begin;   /* to hold <= 1 pending entry per map, [large_begin,
                                               wide_begin) <= 2, [wide_begin, lanes) more (multiples of
-                                              64 except at the end) */
+                                              64 except at the end); */
+    uint32_t                 big_begin;    /* long-tail workflows [big_begin, n_wf) are expected to outgrow
+                                              the fast kernels' per-wave arenas (replayed concurrently
+                                              with the 57-KB arena); n_wf: none */
+    uint32_t                 reserved;
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */

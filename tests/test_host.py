@@ -161,7 +161,7 @@ def test_interleave_tier_segments():
     cls = tier_classes(b)
     assert len(np.unique(cls)) == 3
     ib = interleave(b, long_threshold=70)
-    lb, wb = ib.tiers
+    lb, wb, bb = ib.tiers
     nl = ib.wave_begin
     c = cls[ib.perm[:nl]]
     assert (np.diff(c) >= 0).all()
@@ -169,10 +169,11 @@ def test_interleave_tier_segments():
     assert (c[:lb] == 0).all() and (c[lb:wb] <= 1).all()
     assert ib.c_flags() & abi.IN_TIERED
     cnt = ib.wf["ev_count"]
-    assert (np.diff(cnt[nl:]) <= 0).all()
+    assert nl <= bb <= ib.n_wf
+    assert (np.diff(cnt[nl:bb]) <= 0).all() and (np.diff(cnt[bb:]) <= 0).all()
     for k in range(3):
         seg = cnt[:nl][c == k]
         assert (np.diff(seg) <= 0).all()
     # one tier only: no segments beyond the lanes
     ic = interleave(synth.activity_chain(1000, 2, 3))
-    assert ic.tiers == (ic.n_wf, ic.n_wf)
+    assert ic.tiers == (ic.n_wf, ic.n_wf, ic.n_wf)

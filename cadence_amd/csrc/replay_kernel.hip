@@ -1239,17 +1239,42 @@ struct WaveTables {
     return find(P_(), L.n_rp, [&](const crr_reset_point_row& r) { return r.key == key; }) >= 0;
   }
 
-  // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type)).
-  // Few candidate lanes (the usual case): a scalar pass over them with readlane; many: a shuffle
-  // tree (each level is an LDS-crossbar round trip, ~6x the cost of one readlane step).
+  // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type)):
+  // a scalar pass with readlane over the candidate lanes -- all of them when few, else only those
+  // holding the minimum timestamp (found with a shuffle tree over the timestamp alone).
   __device__ __forceinline__ static i64 readlane64(i64 v, i32 l) {
     const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
     const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
     return (i64)(((u64)hi << 32) | lo);
   }
+  // minimum over the 64 lanes (all active), uniform: DPP steps inside each row of 16, then the
+  // row broadcasts of 15 / 31 (lane 63 ends with the wave minimum) -- VALU moves, no LDS crossbar
+  template <int CTRL, int ROW_MASK>
+  __device__ __forceinline__ static i64 dpp_min_step(i64 v) {
+    const u32 lo = (u32)(u64)v, hi = (u32)((u64)v >> 32);
+    const u32 olo = (u32)__builtin_amdgcn_update_dpp((int)lo, (int)lo, CTRL, ROW_MASK, 0xF, false);
+    const u32 ohi = (u32)__builtin_amdgcn_update_dpp((int)hi, (int)hi, CTRL, ROW_MASK, 0xF, false);
+    const i64 o = (i64)(((u64)ohi << 32) | olo);
+    return o < v ? o : v;
+  }
+  __device__ __forceinline__ static i64 wave_min_i64(i64 v) {
+    v = dpp_min_step<0x128, 0xF>(v);  // row_ror:8
+    v = dpp_min_step<0x124, 0xF>(v);  // row_ror:4
+    v = dpp_min_step<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+    v = dpp_min_step<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+    v = dpp_min_step<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+    v = dpp_min_step<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+    return readlane64(v, 63);
+  }
   __device__ __forceinline__ static void wave_min(BestTimer& B) {
     u64 m = __builtin_amdgcn_ballot_w64(B.have);
-    if (__builtin_popcountll(m) <= 12) {
+    if (__builtin_popcountll(m) > 12) {
+      // many candidates: reduce the timestamp alone (two crossbar shuffles per level), then keep only
+      // the lanes holding the minimum (almost always one) for the scalar pass below
+      const i64 t = wave_min_i64(B.have ? B.t : (i64)0x7fffffffffffffffLL);
+      m = __builtin_amdgcn_ballot_w64(B.have && B.t == t);
+    }
+    {
       BestTimer R;
       while (m) {
         const i32 l = (i32)__builtin_ctzll(m);
@@ -1263,25 +1288,7 @@ struct WaveTables {
         }
       }
       B = R;
-      return;
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      BestTimer o;
-      o.have = __shfl_xor((int)B.have, off, 64) != 0;
-      o.t = __shfl_xor((long long)B.t, off, 64);
-      o.e = __shfl_xor((long long)B.e, off, 64);
-      o.y = __shfl_xor(B.y, off, 64);
-      o.j = __shfl_xor(B.j, off, 64);
-      o.created = __shfl_xor((int)B.created, off, 64) != 0;
-      if (o.have && (!B.have || seq_less(o.t, o.e, o.y, B.t, B.e, B.y))) B = o;
-    }
-    B.have = uniform32(B.have) != 0;
-    B.t = uniform64(B.t);
-    B.e = uniform64(B.e);
-    B.y = uniform32(B.y);
-    B.j = uniform32(B.j);
-    B.created = uniform32(B.created) != 0;
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {

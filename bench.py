@@ -158,20 +158,28 @@ def pcie_inclusive(eng, batch, torch, reps=3):
     """SURVEY.md §8d's second figure: one replay with host buffers -- device allocation + H2D of the
     columns, side records and descriptors, the replay, D2H of the execution rows and the slot
     tables -- never the headline `value` (which has the inputs resident in HBM)."""
-    times = []
+    times, parts = [], []
     for _ in range(reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         db = eng.upload(batch)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         eng.launch(db)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
         r = eng.download(db)
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
+        t3 = time.perf_counter()
+        times.append(t3 - t0)
+        parts.append((t1 - t0, t2 - t1, t3 - t2))
         del db, r
     t = float(np.median(times))
+    up, run, down = (float(np.median([p[i] for p in parts])) * 1e3 for i in range(3))
     h2d = sum(v.nbytes for v in batch.cols.values()) + batch.act_side.nbytes + batch.start_side.nbytes \
         + batch.arena.nbytes + batch.wf.nbytes
     return {"events_per_s": batch.n_events / t, "ms": t * 1e3, "h2d_bytes": int(h2d),
+            "upload_ms": up, "replay_ms": run, "download_ms": down,
             "note": "pageable host buffers, allocation + upload + replay + download of exec rows and slot tables"}
 
 

@@ -186,7 +186,7 @@ class ReplayEngine:
         ex = T["exec"].cpu().numpy().view(abi.EXEC_ROW)[:db.n_wf].copy()
         tables = {}
         for name, dt, *_ in abi.TABLES:
-            tables[name] = T["out_" + name].cpu().numpy().view(dt).copy()
+            tables[name] = T["out_" + name].cpu().numpy().view(dt)   # .cpu() is already a fresh host copy
         return ReplayResult(ex, tables)
 
     def replay(self, batch: HistoryBatch) -> ReplayResult:

@@ -1071,6 +1071,9 @@ struct WaveTables {
   i32 lane;
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
   bool retried = false;
+  // a map changed since its last batch epilogue; an unchanged map would select the same, already
+  // created, timer again (a no-op), so its epilogue is skipped
+  bool dirty_act = false, dirty_timer = false;
 
   __device__ __forceinline__ void init() { lane = (i32)(threadIdx.x & 63); }
 
@@ -1134,11 +1137,13 @@ struct WaveTables {
     if (m >= 0 && own(m)) S.act(m).flags &= ~CRR_ROW_MAPPED;
     if (own(j)) S.act(j) = row;
     ++L.n_act;
+    dirty_act = true;
     return CRR_OK;
   }
   __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
     const i32 j = find_act_by_id(sched);
     if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
+    dirty_act = true;
     if (own(j)) {
       crr_activity_row& r = S.act(j);
       r.version = ver;
@@ -1155,6 +1160,7 @@ struct WaveTables {
     const u32 key = bcast(j, S.act(j).key);
     if (own(j)) S.act(j).flags = f & ~(CRR_ROW_LIVE | CRR_ROW_MAPPED);
     --L.n_act;
+    dirty_act = true;
     if (f & CRR_ROW_MAPPED) return;
     const i32 m = find_act_mapped(key);
     if (m >= 0) { if (own(m)) S.act(m).flags &= ~CRR_ROW_MAPPED; }
@@ -1178,6 +1184,7 @@ struct WaveTables {
       ++L.n_timer;
     }
     if (own(j)) S.timer(j) = row;
+    dirty_timer = true;
     return CRR_OK;
   }
   __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
@@ -1185,6 +1192,7 @@ struct WaveTables {
     if (j < 0) { ++L.inconsistencies; return; }
     if (own(j)) S.timer(j).flags = 0;
     --L.n_timer;
+    dirty_timer = true;
   }
   __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
     const i32 j = take(C_(), hw_child, ST::C, G.child_cap);
@@ -1292,7 +1300,7 @@ struct WaveTables {
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
-    if (L.n_act > 0) {
+    if (L.n_act > 0 && dirty_act) {
       BestTimer B;
       for (i32 j = lane; j < hw_act; j += 64) {
         const crr_activity_row& r = S.act(j);
@@ -1309,7 +1317,8 @@ struct WaveTables {
       }
       if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
     }
-    if (L.n_timer > 0) {
+    dirty_act = false;
+    if (L.n_timer > 0 && dirty_timer) {
       BestTimer B;
       for (i32 j = lane; j < hw_timer; j += 64) {
         const crr_timer_row& r = S.timer(j);
@@ -1320,6 +1329,7 @@ struct WaveTables {
       if (B.have && !B.created && own(B.j)) S.timer(B.j).task_status = CRR_TIMER_TASK_STATUS_CREATED;
       if (B.have && !B.created) K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
     }
+    dirty_timer = false;
   }
   __device__ __forceinline__ bool task_writer() const { return lane == 0; }
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365); each lane clears the slots
@@ -1327,6 +1337,7 @@ struct WaveTables {
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
     for (i32 j = lane; j < hw_act; j += 64) S.act(j).timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
     for (i32 j = lane; j < hw_timer; j += 64) S.timer(j).task_status = CRR_TIMER_TASK_STATUS_NONE;
+    dirty_act = dirty_timer = true;
     epilogue(L, G, TaskSink{false, false});
   }
 

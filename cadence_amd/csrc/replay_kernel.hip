@@ -354,6 +354,9 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
 // ===================================================================================================
 struct GlobalTables {
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
+  // a map changed since its last batch epilogue (an unchanged one would reselect the same created
+  // timer: a no-op, skipped -- each skipped pass is a scan of HBM rows)
+  bool dirty_act = false, dirty_timer = false;
 
   template <class R>
   __device__ __forceinline__ static i32 free_slot(R* (Geo::*row)(i32) const, const Geo& G, i32& hw, i32 cap) {
@@ -400,6 +403,7 @@ struct GlobalTables {
     if (j < 0) return CRR_ERR_CAPACITY;
     *G.act(j) = row;
     ++L.n_act;
+    dirty_act = true;
     return CRR_OK;
   }
   // ReplicateActivityTaskStartedEvent (:2254-2276)
@@ -407,6 +411,7 @@ struct GlobalTables {
     i32 j = find_act_by_id(G, sched);
     if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
     crr_activity_row* r = G.act(j);
+    dirty_act = true;
     r->version = ver;
     r->started_id = id;
     r->started_src = s;
@@ -422,6 +427,7 @@ struct GlobalTables {
     u32 key = r->key;
     r->flags = f & ~(CRR_ROW_LIVE | CRR_ROW_MAPPED);
     --L.n_act;
+    dirty_act = true;
     if (f & CRR_ROW_MAPPED) return;
     i32 m = find_act_mapped(G, key);
     if (m >= 0) G.act(m)->flags &= ~CRR_ROW_MAPPED;
@@ -445,6 +451,7 @@ struct GlobalTables {
       ++L.n_timer;
     }
     *G.timer(j) = row;
+    dirty_timer = true;
     return CRR_OK;
   }
   // DeleteUserTimer (:1390-1419)
@@ -453,6 +460,7 @@ struct GlobalTables {
     if (j < 0) { ++L.inconsistencies; return; }
     G.timer(j)->flags = 0;
     --L.n_timer;
+    dirty_timer = true;
   }
   // ReplicateStartChildWorkflowExecutionInitiatedEvent (:3417-3453)
   __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
@@ -505,7 +513,7 @@ struct GlobalTables {
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
-    if (L.n_act > 0) {
+    if (L.n_act > 0 && dirty_act) {
       BestTimer B;
       for (i32 j = 0; j < hw_act; ++j) {
         const crr_activity_row* r = G.act(j);
@@ -521,16 +529,18 @@ struct GlobalTables {
         K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);  // timer_sequence.go:190-196
       }
     }
+    dirty_act = false;
     epilogue_timers(L, G, K);
   }
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
     for (i32 j = 0; j < hw_act; ++j) G.act(j)->timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
     for (i32 j = 0; j < hw_timer; ++j) G.timer(j)->task_status = CRR_TIMER_TASK_STATUS_NONE;
+    dirty_act = dirty_timer = true;
     epilogue(L, G, TaskSink{false, false});
   }
   __device__ __forceinline__ void epilogue_timers(Lane& L, const Geo& G, const TaskSink& K) {
-    if (L.n_timer > 0) {
+    if (L.n_timer > 0 && dirty_timer) {
       BestTimer B;
       for (i32 j = 0; j < hw_timer; ++j) {
         const crr_timer_row* r = G.timer(j);
@@ -542,6 +552,7 @@ struct GlobalTables {
         K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);  // timer_sequence.go:151-156
       }
     }
+    dirty_timer = false;
   }
   __device__ __forceinline__ bool task_writer() const { return true; }
   template <class R, class IdOf>

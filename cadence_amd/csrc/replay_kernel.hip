@@ -1091,6 +1091,9 @@ struct WaveTables {
   // HbmRows ownership: slot j is only ever written and searched by lane j % 64, so every HBM read
   // follows that lane's own writes (single work-item ordering, no fences); a uniform read of a
   // row field takes the owner lane's value.  LDS rows are shared by the whole wave.
+  // Every lane stores a shared LDS row itself: with one writer lane the compiler may forward the old
+  // value to the others' later loads (per-thread reasoning: they never stored), and the lanes'
+  // copies of the wave-uniform state diverge (measured: corrupted exec rows).
   __device__ __forceinline__ bool own(i32 j) const { return ST::kLds || lane == (j & 63); }
   __device__ __forceinline__ u32 bcast(i32 j, u32 v) const {
     if constexpr (ST::kLds) return v;

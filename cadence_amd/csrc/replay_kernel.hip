@@ -133,16 +133,19 @@ struct Crc {
   }
 };
 
+// NT: the block size when the launch fixes it (no read of the dispatch packet), 0: blockDim.x
+template <int NT = 0>
 __device__ void build_crc_tables(u32* T) {
+  const int nt = NT ? NT : (int)blockDim.x;
   // table 0: byte-wise reflected CRC32 (poly 0xEDB88320); tables 1..7: slicing-by-8 extensions
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+  for (int i = threadIdx.x; i < 256; i += nt) {
     u32 c = (u32)i;
     for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
     T[i] = c;
   }
   __syncthreads();
   for (int t = 1; t < 8; ++t) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    for (int i = threadIdx.x; i < 256; i += nt) {
       u32 p = T[(t - 1) * 256 + i];
       T[t * 256 + i] = (p >> 8) ^ T[p & 0xff];
     }
@@ -1514,9 +1517,20 @@ struct LaneSource {
     e.task = 0;
     return e;
   }
+  // step 0: every column with both type bytes, no load waiting on another (one round trip)
   __device__ __forceinline__ void start() {
-    if (n > 0) nx = load(0, E.etype[ix(0)]);
-    if (n > 1) et_nx = E.etype[ix(1)];
+    if (n > 0) {
+      const i64 i = ix(0);
+      nx.et = E.etype[i];
+      if (n > 1) et_nx = E.etype[ix(1)];
+      nx.id = E.event_id[i];
+      nx.ver = E.version[i];
+      nx.ts = E.timestamp[i];
+      nx.ref = E.ref[i];
+      nx.key = E.key[i];
+      nx.aux = E.aux[i];
+      nx.task = 0;
+    }
   }
   __device__ __forceinline__ Ev next(i32 s) {
     const Ev e = nx;
@@ -1574,8 +1588,32 @@ struct WaveSource {
 // ---------------------------------------------------------------------------------------------------
 // generateMutableStateChecksum (checksum.go:36-114) -> GenerateCRC32 (crc.go:35-54) over
 // 0x59 + MutableStateChecksumPayload.Encode (.gen/go/checksum/checksum.go:539-821).
+// The VersionHistory branch token the checksum covers, fetched whole before it is needed: its words
+// are issued back to back (one memory round trip) instead of one dependent load per CRC block.
+// Tokens are 96 bytes (NewHistoryBranchToken's thrift HistoryBranch); longer or unaligned ones take
+// the byte loop for what the prefetched words do not cover.
+struct TokenDesc { u32 so, sl, fo, fl; };  // crr_workflow start / final token offsets and lengths
+__device__ __forceinline__ TokenDesc token_desc(const crr_workflow* wfp) {
+  return TokenDesc{wfp->start_token_off, wfp->start_token_len, wfp->final_token_off, wfp->final_token_len};
+}
+struct TokenWords {
+  static constexpr int kWords = 12;
+  u64 w[kWords];
+  u32 off, len, held;  // held: bytes in w (a multiple of 8)
+  __device__ __forceinline__ void issue(const TokenDesc& d, i32 token_src, const uint8_t* arena) {
+    off = 0; len = 0;
+    if (token_src == 1) { off = d.so; len = d.sl; }
+    if (token_src == 2) { off = d.fo; len = d.fl; }
+    held = (off & 7u) ? 0u : (len & ~7u);
+    held = held < 8u * kWords ? held : 8u * kWords;
+    const u64* tw = reinterpret_cast<const u64*>(arena + off);
+#pragma unroll
+    for (int j = 0; j < kWords; ++j) w[j] = (8u * j + 8u <= held) ? tw[j] : 0ull;
+  }
+};
+
 template <class IDS>
-__device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids, const Geo& G, const crr_workflow* wfp,
+__device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids, const Geo& G, const TokenWords& TW,
                                            const uint8_t* arena, const u32* tables, u32* out_len) {
   Crc K;
   K.init(tables);
@@ -1604,14 +1642,15 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
   K.field(12, 56);                                                       // VersionHistories (shared.go:91639)
   K.field(8, 10); K.be32(0);                                             //   CurrentVersionHistoryIndex
   K.list_header(20, 12, 1u);                                             //   Histories: list<struct> of 1
-  u32 toff = 0, tlen = 0;
-  if (R.token_src == 1) { toff = wfp->start_token_off; tlen = wfp->start_token_len; }
-  if (R.token_src == 2) { toff = wfp->final_token_off; tlen = wfp->final_token_len; }
+  const u32 tlen = TW.len;
   K.field(11, 10); K.be32(tlen);                                         //   VersionHistory.BranchToken (shared.go:92043)
   {
-    const uint8_t* tp = arena + toff;
-    u32 i = 0;
-    if ((toff & 7u) == 0) {
+#pragma unroll
+    for (int j = 0; j < TokenWords::kWords; ++j)
+      if (8u * j + 8u <= TW.held) K.push(TW.w[j], 8);
+    const uint8_t* tp = arena + TW.off;
+    u32 i = TW.held;
+    if ((TW.off & 7u) == 0) {
       const u64* tw = reinterpret_cast<const u64*>(tp);
       for (; i + 8 <= tlen; i += 8) K.push(tw[i >> 3], 8);
     }
@@ -1918,6 +1957,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 
   i64 batch_first_id = 0;
   i32 last_task_step = -1;
+  bool task_read = false;
+  TokenDesc tok{0, 0, 0, 0};  // read after the loop (failed workflows have no checksum: left zero)
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
 
@@ -1979,22 +2020,32 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       L.next_event_id = id + 1;
     }
   }
-  if (empty_at == n_ev) FAIL(CRR_ERR_EMPTY_HISTORY, n_ev);
-  if (wfp->final_token_len != 0xFFFFFFFFu) {  // rebuild finalisation (state_rebuilder.go:150-177)
-    L.token_src = 2;
-    if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, n_ev);
+  {
+    // what the tail reads from HBM -- the last TaskID, the token and rebuild fields of the descriptor --
+    // issued together, before the first use of any of them: one memory round trip, not a chain
+    if (last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
+    task_read = true;
+    tok.so = wfp->start_token_off; tok.sl = wfp->start_token_len;
+    tok.fo = wfp->final_token_off; tok.fl = wfp->final_token_len;
+    const u32 final_len = tok.fl;
     const i64 want_id = wfp->rebuild_last_event_id, want_ver = wfp->rebuild_last_event_version;
-    if (want_id < 0 || (want_ver < 0 && want_ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, n_ev);
-    if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
-  }
-  if (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:183)
-    T.refresh(L, G);
-    L.n_tasks = 0;  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
+    const u32 wf_flags = wfp->flags;
+    if (empty_at == n_ev) FAIL(CRR_ERR_EMPTY_HISTORY, n_ev);
+    if (final_len != 0xFFFFFFFFu) {  // rebuild finalisation (state_rebuilder.go:150-177)
+      L.token_src = 2;
+      if (L.vh_n == 0) FAIL(CRR_ERR_VH_EMPTY, n_ev);
+      if (want_id < 0 || (want_ver < 0 && want_ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, n_ev);
+      if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
+    }
+    if (wf_flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:183)
+      T.refresh(L, G);
+      L.n_tasks = 0;  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
+    }
   }
 done_events:
 #undef CHECK
 #undef FAIL
-  if (last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
+  if (!task_read && last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
   if (L.status == CRR_OK && K.on && L.n_tasks > G.task_cap) L.status = CRR_ERR_CAPACITY;
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
@@ -2002,6 +2053,10 @@ done_events:
     T.retry_push(in, out, w);
     return;
   }
+  // the checksum's branch-token words go out before the row write-back, whose work hides their latency
+  const bool want_crc = L.status == CRR_OK && !(CRR_EXP & 1);
+  TokenWords TW;
+  TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
   if (L.vh_n > 0) {
     crr_vh_item* it = G.vh(L.vh_n - 1);
     it->event_id = L.vh_last_id;
@@ -2045,7 +2100,7 @@ done_events:
   R.payload_len = 0;
   R.n_tasks = L.n_tasks;
   R.reserved = 0;
-  if (L.status == CRR_OK && !(CRR_EXP & 1)) R.checksum = payload_crc(R, T, G, wfp, in.arena, crc_tables, &R.payload_len);
+  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
 }
 
@@ -2080,7 +2135,7 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
                 "per-wave arenas must fit in the lane arena");
   __shared__ u32 crc_tables[8 * 256];
   __shared__ BlockArena<TIER> arena;
-  build_crc_tables(crc_tables);
+  build_crc_tables<kBlock>(crc_tables);
   const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
   const u32 tail_end = WAVE_TAIL ? tail_count_end(in) : in.n_wf;  // [tail_end, n_wf): replay_big_kernel
   const u32 wave_blocks = WAVE_TAIL ? (tail_end - n_lane + kWavesPerBlock - 1) / kWavesPerBlock : 0;
@@ -2100,15 +2155,20 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
     return;
   }
-  const u32 w = lo + (blockIdx.x - wave_blocks) * blockDim.x + threadIdx.x;  // lanes [lo, hi)
+  const u32 w = lo + (blockIdx.x - wave_blocks) * kBlock + threadIdx.x;  // lanes [lo, hi); launched with kBlock
   if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
-  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  // the descriptor in one round trip: the phase test reads its flags after the geometry is loaded
   const i64 lane = threadIdx.x & 63;
   Geo G;
   load_geo(G, wfp, out, 64);
+  const i64 ev_begin0 = wfp->ev_begin;
+  const i32 ev_count0 = wfp->ev_count;
+  const u32 wf_flags = wfp->flags;
+  asm volatile("" ::"v"(ev_begin0), "v"(ev_count0), "v"(wf_flags));  // all issued before the phase test's wait
+  if (((wf_flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   uniformize_geo(G, lane);
-  const i64 ev_begin = uniform64(wfp->ev_begin - lane) + lane;
+  const i64 ev_begin = uniform64(ev_begin0 - lane) + lane;
   LdsTables<TIER> T;
   T.init(&arena.lane, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
@@ -2321,8 +2381,10 @@ __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_out
   load_geo(G, wfp, out, wf_stride(in, w));
   const crr_exec_row R = out.exec[w];
   GlobalTables ids;
+  TokenWords TW;
+  TW.issue(token_desc(wfp), R.token_src, in.arena);
   u32 len = 0;
-  checksums[w] = payload_crc(R, ids, G, wfp, in.arena, crc_tables, &len);
+  checksums[w] = payload_crc(R, ids, G, TW, in.arena, crc_tables, &len);
 }
 
 }  // namespace crr

@@ -2277,15 +2277,18 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
 __global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase,
                                                                                     u32 lo, u32 hi) {
   __shared__ u32 crc_tables[8 * 256];
-  build_crc_tables(crc_tables);
+  build_crc_tables<kBlock>(crc_tables);
   const u32 w = lo + blockIdx.x * kBlock + threadIdx.x;
   if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
-  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   const i64 lane = threadIdx.x & 63;
-  Geo G;
+  Geo G;  // the descriptor in one round trip, as in replay_lds
   load_geo(G, wfp, out, 64);
   i64 ev_begin = wfp->ev_begin;
+  const i32 ev_count0 = wfp->ev_count;
+  const u32 wf_flags = wfp->flags;
+  asm volatile("" ::"v"(ev_begin), "v"(ev_count0), "v"(wf_flags));
+  if (((wf_flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   if ((lo & 63u) == 0) {  // wavefront == one interleaved group: group-uniform geometry in SGPRs
     uniformize_geo(G, lane);
     ev_begin = uniform64(ev_begin - lane) + lane;

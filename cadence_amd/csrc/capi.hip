@@ -132,7 +132,9 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   if (!valid_inputs(in, out)) return -1;
   if (in->n_wf == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool timed = ensure_events();
+  // inside a crr_timing_begin region the ring's event pair is the only record: the per-call
+  // phase events (crr_last_kernel_ms) would add four event packets to every measured step
+  const bool timed = !g_ring.on && ensure_events();
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
   // fast-path grid: one block per 4 long (wave-tail) workflows, then one per 256 lane workflows
   const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;

@@ -511,7 +511,8 @@ float crr_last_kernel_ms(int which);
 /* Measured region for benchmarks: after crr_timing_begin, every crr_replay on this thread records
  * its phase-1 fast-path kernel with its own HIP event pair on the launch stream (up to 512 launches,
  * no synchronisation between launches).  crr_timing_read ends the region, waits for the events and
- * writes up to `cap` per-launch durations (ms); returns how many, or -1 on a HIP error. */
+ * writes up to `cap` per-launch durations (ms); returns how many, or -1 on a HIP error.  Inside the
+ * region crr_last_kernel_ms returns -1 (the per-call phase events are not recorded). */
 int crr_timing_begin(void);
 int crr_timing_read(float* ms, int cap);
 

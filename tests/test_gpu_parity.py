@@ -172,3 +172,27 @@ def test_retry_routes(engine):
                  known_domains=KNOWN)
     check(engine, interleave(lt))
     check(engine, interleave(lt, tiered=False))
+
+
+def test_measured_region_launches(engine):
+    """Launches inside crr_timing_begin/_read (the bench's measured region) record one ring event
+    pair each and skip the per-call phase events; the rows they leave are the oracle's."""
+    import torch
+    b = interleave(synth.activity_chain(4_096, 4, synth.SEED_C2))
+    db = engine.upload(b)
+    engine.launch(db)
+    torch.cuda.synchronize()
+    assert engine.last_kernel_ms()[2] > 0
+    engine.timing_begin()
+    for _ in range(3):
+        engine.launch(db)
+    assert engine.last_kernel_ms() == [-1.0, -1.0, -1.0]
+    ms = engine.timing_read()
+    assert len(ms) == 3 and all(m > 0 for m in ms)
+    got = engine.download(db)
+    want = _oracle().replay(b, 0)
+    d = diff_results(b, got, b, want)
+    assert not d, "\n".join(d)
+    engine.launch(db)
+    torch.cuda.synchronize()
+    assert engine.last_kernel_ms()[2] > 0

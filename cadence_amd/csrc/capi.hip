@@ -98,7 +98,22 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (in->flags & CRR_IN_WAVE_TAIL) {
     if (in->stride != 64 || in->wave_begin > in->n_wf) return false;
   }
+  if (in->flags & CRR_IN_TIERED) {
+    // the lane kernels keep a wavefront's geometry in SGPRs: every segment must start on a group
+    // (64-workflow) boundary, or its wavefronts would straddle two groups
+    const uint32_t n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
+    if (in->stride != 64) return false;
+    if (in->large_begin < n_lane && (in->large_begin & 63u)) return false;
+    if (in->wide_begin < n_lane && (in->wide_begin & 63u)) return false;
+  }
   return true;
+}
+
+// Every crr_replay leaves the retry-list counters (scratch[0..2]) zeroed; an error return after the
+// fast kernels were enqueued must reset them itself (the retry pass that would have is not launched).
+int fail_reset(const crr_outputs* out, hipStream_t s, hipError_t err) {
+  if (out->scratch) (void)hipMemsetAsync(out->scratch, 0, 3 * sizeof(uint32_t), s);
+  return (int)err;
 }
 
 }  // namespace
@@ -207,7 +222,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         launch_fast(s, small, tail, 0, n_lane);
       }
       hipError_t err = hipGetLastError();
-      if (err != hipSuccess) return (int)err;
+      if (err != hipSuccess) return fail_reset(out, s, err);
       if (timed && phase == 1) {
         (void)hipEventRecord(g_timing.ev[5], s);
         g_timing.valid[2] = true;
@@ -219,7 +234,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       hipLaunchKernelGGL(crr::replay_global_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, phase, 0);
     }
     hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return (int)err;
+    if (err != hipSuccess) return in->stride == 64 ? fail_reset(out, s, err) : (int)err;
     if (timed) {
       (void)hipEventRecord(g_timing.ev[2 * phase + 1], s);
       g_timing.valid[phase] = true;

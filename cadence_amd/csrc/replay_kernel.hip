@@ -2333,8 +2333,10 @@ union RetryArena {
 __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_outputs out, int phase) {
   __shared__ u32 crc_tables[8 * 256];
   __shared__ RetryArena arena;
-  const u32 n0 = __hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const u32 n1 = __hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // counts are bounded by n_wf (each workflow is handed back at most once per launch); the clamp
+  // keeps a stale or corrupted header from indexing past the lists
+  const u32 n0 = min(__hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
+  const u32 n1 = min(__hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
   if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
 #if CRR_EXP & 64  // diagnostics only: leave the handed-back workflows at CRR_INTERNAL_RETRY
   return;
@@ -2342,6 +2344,7 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   build_crc_tables(crc_tables);
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
+    if (w >= in.n_wf) continue;
     WaveTables<LdsRows<BigArena, -1>> T;
     T.S.M = &arena.wave;
     replay_wave_item(in, out, phase, w, T, crc_tables);
@@ -2358,8 +2361,8 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   const u32 chunk = min(64u, (n0 + gridDim.x - 1) / gridDim.x);
   for (u32 base = start * chunk; base < n0; base += gridDim.x * chunk) {
     const u32 i = base + threadIdx.x;
-    if (threadIdx.x < chunk && i < n0)
-      replay_lane_item(in, out, phase, out.scratch[retry_slot(in, 0, i)], &arena.lane, crc_tables);
+    const u32 w = (threadIdx.x < chunk && i < n0) ? out.scratch[retry_slot(in, 0, i)] : in.n_wf;
+    if (w < in.n_wf) replay_lane_item(in, out, phase, w, &arena.lane, crc_tables);
   }
   // every block has read both counts: the last one to finish resets them for the next launch
   if (threadIdx.x == 0) {

@@ -11,8 +11,14 @@ from __future__ import annotations
 
 import numpy as np
 
-EXEC_ROW_WORDS = 48          # sizeof(crr_exec_row) / 4
-W_STATUS, W_INCONS, W_NEXT_EVENT_ID, W_CHECKSUM = 0, 2, 8, 44
+from . import abi
+
+# word offsets of the digest's fields inside crr_exec_row (int32 words; next_event_id as an int64 word)
+EXEC_ROW_WORDS = abi.EXEC_ROW.itemsize // 4
+W_STATUS = abi.EXEC_ROW.fields["status"][1] // 4
+W_INCONS = abi.EXEC_ROW.fields["inconsistencies"][1] // 4
+W_CHECKSUM = abi.EXEC_ROW.fields["checksum"][1] // 4
+Q_NEXT_EVENT_ID = abi.EXEC_ROW.fields["next_event_id"][1] // 8
 DIGEST_LEN = 6
 GOLDEN = 0x9E3779B1
 
@@ -29,11 +35,13 @@ def workflow_mask(shard_ids: np.ndarray, rank: int, world: int) -> np.ndarray:
 def digest_torch(torch, exec_bytes, n_wf: int):
     """Device-side digest of a replayed shard from the raw exec-row buffer (int64[6]):
     [events replayed, workflows ok, workflows failed, sum(crc of ok), sum(crc*phi mod 2^32), inconsistencies]."""
-    rows = exec_bytes[: n_wf * EXEC_ROW_WORDS * 4].view(torch.int32).view(n_wf, EXEC_ROW_WORDS)
+    raw = exec_bytes[: n_wf * EXEC_ROW_WORDS * 4]
+    rows = raw.view(torch.int32).view(n_wf, EXEC_ROW_WORDS)
+    nxt = raw.view(torch.int64).view(n_wf, EXEC_ROW_WORDS // 2)[:, Q_NEXT_EVENT_ID]   # the whole int64 field
     ok = (rows[:, W_STATUS] == 0).to(torch.int64)
     crc = rows[:, W_CHECKSUM].to(torch.int64) & 0xFFFFFFFF
     return torch.stack([
-        ((rows[:, W_NEXT_EVENT_ID].to(torch.int64) - 1) * ok).sum(),
+        ((nxt - 1) * ok).sum(),
         ok.sum(),
         n_wf - ok.sum(),
         (crc * ok).sum(),
@@ -46,7 +54,7 @@ def digest_numpy(exec_rows: np.ndarray) -> np.ndarray:
     """Same digest from host exec rows (abi.EXEC_ROW)."""
     ok = (exec_rows["status"] == 0).astype(np.int64)
     crc = exec_rows["checksum"].astype(np.int64)
-    nxt = exec_rows["next_event_id"].astype(np.int64) & 0xFFFFFFFF
+    nxt = exec_rows["next_event_id"].astype(np.int64)
     return np.array([((nxt - 1) * ok).sum(), ok.sum(), len(exec_rows) - ok.sum(), (crc * ok).sum(),
                      ((crc * GOLDEN) & 0xFFFFFFFF).sum(), exec_rows["inconsistencies"].astype(np.int64).sum()],
                     dtype=np.int64)

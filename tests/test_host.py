@@ -132,10 +132,35 @@ def test_digest_numpy_matches_torch():
     rows = np.zeros(5, abi.EXEC_ROW)
     rows["status"] = [0, 0, 3, 0, 0]
     rows["checksum"] = [1, 0xFFFFFFFF, 7, 12345, 0x80000000]
-    rows["next_event_id"] = [30, 24, 5, 30, 2]
+    rows["next_event_id"] = [30, 24, 5, 2 ** 31 + 7, 2 ** 40 + 2]   # IDs past the low int32 word too
     rows["inconsistencies"] = [0, 1, 0, 2, 0]
     raw = torch.from_numpy(rows.view(np.uint8).copy())
-    assert (dist.digest_torch(torch, raw, 5).numpy() == dist.digest_numpy(rows)).all()
+    d = dist.digest_numpy(rows)
+    assert (dist.digest_torch(torch, raw, 5).numpy() == d).all()
+    assert d[0] == 29 + 23 + 2 ** 31 + 6 + 2 ** 40 + 1
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_replay_rejects_unaligned_tier_segments():
+    """crr_replay validates CRR_IN_TIERED segment starts (multiples of 64 below the lane count)
+    before any HIP call: an unaligned boundary returns -1 instead of replaying wrong rows."""
+    lib = ctypes.CDLL(LIB)
+    lib.crr_replay.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.crr_replay.restype = ctypes.c_int
+    dummy = ctypes.c_void_p(64)          # never dereferenced: validation fails first
+    ev = abi.CEvents(*([dummy.value] * len(abi.EVENT_COLUMNS)))
+    ci = abi.CInputs()
+    ci.ev = ev
+    for f in ("act_side", "start_side", "reset_keys", "arena", "wf"):
+        setattr(ci, f, dummy.value)
+    ci.n_wf, ci.stride, ci.flags = 1000, 64, abi.IN_TIERED
+    co = abi.COutputs(*([dummy.value] * len(abi.COutputs._fields_)))
+    for lb, wb in ((100, 1000), (128, 130), (3, 3)):
+        ci.large_begin, ci.wide_begin = lb, wb
+        assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1, (lb, wb)
+    ci.stride = 1                        # tier segments are a stride-64 layout only
+    ci.large_begin = ci.wide_begin = 1000
+    assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1
 
 
 HOST_LIB = os.path.join(ROOT, "cadence_amd", "libcadence_host.so")

@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1
@@ -152,6 +152,7 @@ ROW_RESETTABLE = 16
 
 WF_FLAG_NEW_RUN = 1
 WF_FLAG_REFRESH_TASKS = 2      # Rebuild's RefreshTasks state effects after the replay
+WF_FLAG_RESUME = 4             # ApplyEvents onto the loaded state held in the output rows (in place)
 IN_HAS_NEW_RUN = 1
 IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4
@@ -192,7 +193,8 @@ EXEC_ROW = np.dtype([
     ("decision_request_src", "<i4"), ("start_src", "<i4"),
     ("n_activity", "<i4"), ("n_timer", "<i4"), ("n_child", "<i4"), ("n_rc", "<i4"), ("n_signal", "<i4"),
     ("n_vh_items", "<i4"), ("n_reset_points", "<i4"), ("token_src", "<i4"),
-    ("checksum", "<u4"), ("payload_len", "<u4"), ("n_tasks", "<i4"), ("reserved", "<i4")])
+    ("checksum", "<u4"), ("payload_len", "<u4"), ("n_tasks", "<i4"), ("decision_start_to_close", "<i4"),
+    ("expiration_ns", "<i8"), ("src_next", "<i4"), ("reserved", "<i4")])
 
 ACTIVITY_ROW = np.dtype([
     ("schedule_id", "<i8"), ("version", "<i8"), ("scheduled_batch_id", "<i8"), ("scheduled_time", "<i8"),
@@ -200,7 +202,7 @@ ACTIVITY_ROW = np.dtype([
     ("last_hb_timeout_vis_s", "<i8"), ("sched_src", "<i4"), ("started_src", "<i4"),
     ("schedule_to_start", "<i4"), ("schedule_to_close", "<i4"), ("start_to_close", "<i4"),
     ("heartbeat", "<i4"), ("timer_task_status", "<i4"), ("key", "<u4"), ("flags", "<u4"),
-    ("reserved", "<i4", (3,))])
+    ("reserved", "<i4"), ("last_heartbeat_time", "<i8")])
 
 TIMER_ROW = np.dtype([
     ("started_id", "<i8"), ("version", "<i8"), ("expiry_time", "<i8"), ("task_status", "<i4"),

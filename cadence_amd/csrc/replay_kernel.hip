@@ -174,6 +174,7 @@ struct Lane {
   i32 status, fail_step;
   i32 n_tasks;                  // transfer / timer tasks generated (CRR_IN_EMIT_TASKS)
   i64 expiration_ns;            // executionInfo.ExpirationTime (0: unset)
+  i32 src_base;                 // provenance offset of this call's steps (the resumed row's src_next; 0 fresh)
 };
 
 // Where this lane's output rows live in HBM: row(table, slot) = base + slot * stride.
@@ -327,16 +328,16 @@ struct BestTimer {
     if (!have || seq_less(tt, ee, yy, t, e, y)) { have = true; t = tt; e = ee; y = yy; j = jj; created = cc; }
   }
 };
+// hb_t: max(StartedTime, LastHeartBeatUpdatedTime) (getActivityHeartbeatTimeout, timer_sequence.go:345-381)
 __device__ __forceinline__ void activity_candidates(BestTimer& B, i32 j, i64 sid, i64 sched_t, bool started,
-                                                    i64 start_t, i32 s2s, i32 s2c, i32 st2c, i32 hb, u32 tts) {
+                                                    i64 start_t, i64 hb_t, i32 s2s, i32 s2c, i32 st2c, i32 hb, u32 tts) {
   if (sid == CRR_EMPTY_EVENT_ID) return;
   B.offer(add_seconds(sched_t, s2c), sid, CRR_TIMEOUT_SCHEDULE_TO_CLOSE, j, (tts & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) != 0);
   if (!started) {
     B.offer(add_seconds(sched_t, s2s), sid, CRR_TIMEOUT_SCHEDULE_TO_START, j, (tts & CRR_TTS_CREATED_SCHEDULE_TO_START) != 0);
   } else {
     B.offer(add_seconds(start_t, st2c), sid, CRR_TIMEOUT_START_TO_CLOSE, j, (tts & CRR_TTS_CREATED_START_TO_CLOSE) != 0);
-    // LastHeartBeatUpdatedTime == StartedTime on the replay path (mutable_state_builder.go:2272-2273)
-    if (hb > 0) B.offer(add_seconds(start_t, hb), sid, CRR_TIMEOUT_HEARTBEAT, j, (tts & CRR_TTS_CREATED_HEARTBEAT) != 0);
+    if (hb > 0) B.offer(add_seconds(hb_t, hb), sid, CRR_TIMEOUT_HEARTBEAT, j, (tts & CRR_TTS_CREATED_HEARTBEAT) != 0);
   }
 }
 
@@ -356,6 +357,7 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
 // GlobalTables: pending maps as slot tables in the HBM output rows (any layout, unbounded).
 // ===================================================================================================
 struct GlobalTables {
+  static constexpr bool kResumable = true;  // rows live in HBM: a loaded state is continued in place
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
   // a map changed since its last batch epilogue (an unchanged one would reselect the same created
   // timer: a no-op, skipped -- each skipped pass is a scan of HBM rows)
@@ -419,6 +421,7 @@ struct GlobalTables {
     r->started_id = id;
     r->started_src = s;
     r->started_time = ts;
+    r->last_heartbeat_time = ts;  // LastHeartBeatUpdatedTime = StartedTime (:2272-2273)
     return CRR_OK;
   }
   // DeleteActivity (:1310-1339)
@@ -502,6 +505,28 @@ struct GlobalTables {
     (is_rc ? G.rc(j) : G.sig(j))->flags = 0;
     if (is_rc) --L.n_rc; else --L.n_sig;
   }
+  // mutableStateBuilder.Load (mutable_state_builder.go:306-349) over the loaded rows in slots 0..n-1:
+  // pendingActivityIDToEventID[ActivityID] = ScheduleID for every activity (:311-314; among duplicate
+  // ActivityIDs Go's map order picks one: here the latest scheduled), every row live
+  __device__ __forceinline__ void load(Lane& L, const Geo& G) {
+    hw_act = L.n_act; hw_timer = L.n_timer; hw_child = L.n_child; hw_rc = L.n_rc; hw_sig = L.n_sig;
+    dirty_act = dirty_timer = true;  // the loaded state's timer masks are re-examined by the first epilogue
+    for (i32 j = 0; j < hw_act; ++j) {
+      crr_activity_row* r = G.act(j);
+      const u32 key = r->key;
+      const i64 sid = r->schedule_id;
+      bool mapped = true;
+      for (i32 k = 0; k < hw_act; ++k) {
+        const crr_activity_row* o = G.act(k);
+        if (k != j && o->key == key && o->schedule_id > sid) mapped = false;
+      }
+      r->flags = (r->flags & ~CRR_ROW_MAPPED) | CRR_ROW_LIVE | (mapped ? CRR_ROW_MAPPED : 0u);
+    }
+    for (i32 j = 0; j < hw_timer; ++j) G.timer(j)->flags |= CRR_ROW_LIVE;
+    for (i32 j = 0; j < hw_child; ++j) G.child(j)->flags |= CRR_ROW_LIVE;
+    for (i32 j = 0; j < hw_rc; ++j) G.rc(j)->flags |= CRR_ROW_LIVE;
+    for (i32 j = 0; j < hw_sig; ++j) G.sig(j)->flags |= CRR_ROW_LIVE;
+  }
   // reset points: rows in HBM, append-only
   __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
@@ -522,7 +547,8 @@ struct GlobalTables {
         const crr_activity_row* r = G.act(j);
         if (!(r->flags & CRR_ROW_LIVE)) continue;
         activity_candidates(B, j, r->schedule_id, r->scheduled_time, r->started_id != CRR_EMPTY_EVENT_ID,
-                            r->started_time, r->schedule_to_start, r->schedule_to_close, r->start_to_close,
+                            r->started_time, max(r->started_time, r->last_heartbeat_time), r->schedule_to_start,
+                            r->schedule_to_close, r->start_to_close,
                             r->heartbeat, (u32)r->timer_task_status);
       }
       if (B.have && !B.created) {
@@ -646,6 +672,8 @@ struct LdsArena {
 template <class TIER>
 struct LdsTables {
   CRR_TIER_SLOTS
+  static constexpr bool kResumable = false;  // rows are rebuilt from this call's events: no loaded state
+  __device__ __forceinline__ void load(Lane&, const Geo&) {}
   using Arena = LdsArena<TIER>;
   Arena* M;
   int t;  // threadIdx.x
@@ -854,6 +882,7 @@ struct LdsTables {
         if (!(f & CRR_ROW_LIVE)) continue;
         const int4 to = M->a_to[j][t];
         activity_candidates(B, j, M->a_sid[j][t], M->a_sched_t[j][t], (f & LF_STARTED) != 0, M->a_start_t[j][t],
+                            M->a_start_t[j][t],
                             to.x, to.y, to.z, to.w, f >> LF_TTS_SHIFT);
       }
       if (B.have && !B.created) {
@@ -941,7 +970,8 @@ struct LdsTables {
       r.timer_task_status = (i32)tts;
       r.key = M->a_key[i][t];
       r.flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
-      r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
+      r.reserved = 0;
+      r.last_heartbeat_time = r.started_time;  // StartedTime (:2272-2273), Go's zero time until started
       *G.act(i) = r;
     }
     for (i32 i = 0; i < L.n_timer; ++i) {  // ReplicateTimerStartedEvent image
@@ -1081,6 +1111,7 @@ struct HbmRows {
 
 template <class ST>
 struct WaveTables {
+  static constexpr bool kResumable = !ST::kLds;  // HbmRows continue a loaded state in place
   ST S;
   i32 lane;
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
@@ -1167,6 +1198,7 @@ struct WaveTables {
       r.started_id = id;
       r.started_src = s;
       r.started_time = ts;
+      r.last_heartbeat_time = ts;
     }
     return CRR_OK;
   }
@@ -1252,6 +1284,30 @@ struct WaveTables {
     }
     if (is_rc) --L.n_rc; else --L.n_sig;
   }
+  // Load over HbmRows (GlobalTables::load): lane j % 64 writes row j; the fields read across lanes (key,
+  // ScheduleID) are not written here
+  __device__ __forceinline__ void load(Lane& L, const Geo& G) {
+    hw_act = L.n_act; hw_timer = L.n_timer; hw_child = L.n_child; hw_rc = L.n_rc; hw_sig = L.n_sig;
+    dirty_act = dirty_timer = true;
+    if constexpr (!ST::kLds) {
+      for (i32 j = lane; j < hw_act; j += 64) {
+        crr_activity_row& r = S.act(j);
+        const u32 key = r.key;
+        const i64 sid = r.schedule_id;
+        bool mapped = true;
+        for (i32 k = 0; k < hw_act; ++k) {
+          const crr_activity_row& o = S.act(k);
+          if (k != j && o.key == key && o.schedule_id > sid) mapped = false;
+        }
+        r.flags = (r.flags & ~CRR_ROW_MAPPED) | CRR_ROW_LIVE | (mapped ? CRR_ROW_MAPPED : 0u);
+      }
+      for (i32 j = lane; j < hw_timer; j += 64) S.timer(j).flags |= CRR_ROW_LIVE;
+      for (i32 j = lane; j < hw_child; j += 64) S.child(j).flags |= CRR_ROW_LIVE;
+      for (i32 j = lane; j < hw_rc; j += 64) S.rc(j).flags |= CRR_ROW_LIVE;
+      for (i32 j = lane; j < hw_sig; j += 64) S.sig(j).flags |= CRR_ROW_LIVE;
+      wave_sync_global();
+    }
+  }
   __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
     if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
@@ -1323,6 +1379,7 @@ struct WaveTables {
         const crr_activity_row& r = S.act(j);
         if (!(r.flags & CRR_ROW_LIVE)) continue;
         activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
+                            max(r.started_time, r.last_heartbeat_time),
                             r.schedule_to_start, r.schedule_to_close, r.start_to_close, r.heartbeat,
                             (u32)r.timer_task_status);
       }
@@ -1798,7 +1855,8 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
         row.key = ev.key;
         row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
-        row.reserved[0] = row.reserved[1] = row.reserved[2] = 0;
+        row.reserved = 0;
+        row.last_heartbeat_time = CRR_ZERO_TIME;
         CHECK(T.act_insert(L, G, row));
         K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks
         break;
@@ -1952,15 +2010,56 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = 0;
   L.inconsistencies = 0;
   L.status = CRR_OK; L.fail_step = -1;
-  L.n_tasks = 0; L.expiration_ns = 0;
+  L.n_tasks = 0; L.expiration_ns = 0; L.src_base = 0;
   const TaskSink K{EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0, T.task_writer()};
 
   i64 batch_first_id = 0;
   i32 last_task_step = -1;
   bool task_read = false;
   TokenDesc tok{0, 0, 0, 0};  // read after the loop (failed workflows have no checksum: left zero)
-#define FAIL(code, step) do { L.status = (code); L.fail_step = (step); goto done_events; } while (0)
+#define FAIL(code, step) do { L.status = (code); L.fail_step = (step) + L.src_base; goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
+
+  if (wfp->flags & CRR_WF_FLAG_RESUME) {
+    if constexpr (P::kResumable) {
+      // the loaded state (mutableStateBuilder.Load, mutable_state_builder.go:306-349) from the rows
+      const crr_exec_row X = out.exec[w];
+      L.state = X.state; L.close_status = X.close_status;
+      L.next_event_id = X.next_event_id; L.last_first_event_id = X.last_first_event_id;
+      L.last_event_task_id = X.last_event_task_id; L.last_processed_event = X.last_processed_event;
+      L.completion_event_batch_id = X.completion_event_batch_id;
+      L.decision_version = X.decision_version; L.decision_schedule_id = X.decision_schedule_id;
+      L.decision_started_id = X.decision_started_id; L.decision_attempt = X.decision_attempt;
+      L.decision_started_ts = X.decision_started_ts; L.decision_scheduled_ts = X.decision_scheduled_ts;
+      L.decision_orig_scheduled_ts = X.decision_orig_scheduled_ts;
+      L.decision_timeout = X.decision_timeout; L.decision_request_src = X.decision_request_src;
+      L.signal_count = X.signal_count; L.decision_start_to_close = X.decision_start_to_close;
+      L.start_src = X.start_src;
+      L.flags = X.flags & (CRR_EXEC_CANCEL_REQUESTED | CRR_EXEC_RESET_POINTS_SET);
+      L.current_version = CRR_EMPTY_VERSION;  // Load: e.currentVersion = common.EmptyVersion (:324)
+      L.token_src = X.token_src;
+      L.n_act = X.n_activity; L.n_timer = X.n_timer; L.n_child = X.n_child; L.n_rc = X.n_rc; L.n_sig = X.n_signal;
+      L.n_rp = X.n_reset_points;
+      L.vh_n = X.n_vh_items;
+      L.expiration_ns = X.expiration_ns;
+      L.src_base = X.src_next;
+      if (L.n_act > G.act_cap || L.n_timer > G.timer_cap || L.n_child > G.child_cap || L.n_rc > G.rc_cap ||
+          L.n_sig > G.sig_cap || L.n_rp > G.rp_cap || L.vh_n > G.vh_cap || L.vh_n < 0 || L.n_act < 0 ||
+          L.n_timer < 0 || L.n_child < 0 || L.n_rc < 0 || L.n_sig < 0 || L.n_rp < 0) {
+        L.n_act = L.n_timer = L.n_child = L.n_rc = L.n_sig = L.n_rp = L.vh_n = 0;
+        FAIL(CRR_ERR_CAPACITY, 0);
+      }
+      if (L.vh_n > 0) {
+        const crr_vh_item last = *G.vh(L.vh_n - 1);
+        L.vh_last_id = last.event_id;
+        L.vh_last_ver = last.version;
+      }
+      T.load(L, G);
+    } else {
+      L.status = CRR_INTERNAL_RETRY;  // rows rebuilt from events cannot hold a loaded state: general path
+      goto done_events;
+    }
+  }
 
   src.start();
   for (i32 s = 0; s < n_ev; ++s) {
@@ -2005,11 +2104,12 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     {
       int rc;
       const i32 tu = uniform32(t);
+      const i32 ps = s + L.src_base;  // provenance step of the event (rows' *_src)
       if (__builtin_amdgcn_ballot_w64(t != tu) == 0)
-        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
+        rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
                          K, wfp->retention_days);
       else
-        rc = apply_event(in, out, L, G, T, ev, s, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
+        rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
                          K, wfp->retention_days);
       if (rc) FAIL(rc, s);
     }
@@ -2099,6 +2199,9 @@ done_events:
   R.checksum = 0;
   R.payload_len = 0;
   R.n_tasks = L.n_tasks;
+  R.decision_start_to_close = L.decision_start_to_close;
+  R.expiration_ns = L.expiration_ns;
+  R.src_next = L.src_base + n_ev;
   R.reserved = 0;
   if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;

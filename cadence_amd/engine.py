@@ -129,13 +129,22 @@ class ReplayEngine:
         elif batch.stride == 64 and fits_small_tier(batch):
             ci.flags |= abi.IN_LDS_SMALL
         co = abi.COutputs()
+        init_host = None
+        if batch.init is not None:   # loaded states (CRR_WF_FLAG_RESUME): the rows the replay continues in place
+            from .result import allocate_host
+            init_host = allocate_host(batch)
         T["exec"] = torch.zeros(max(batch.n_wf, 1) * abi.EXEC_ROW.itemsize, dtype=torch.uint8, device=dev)
+        if init_host is not None and batch.n_wf:
+            T["exec"][:batch.n_wf * abi.EXEC_ROW.itemsize].copy_(torch.from_numpy(init_host.exec.view(np.uint8)))
         co.exec = T["exec"].data_ptr()
         for name, dt, *_ in abi.TABLES:
             rows = max(batch.table_rows.get(name, 0), 1)
             if name == "tasks" and not batch.emit_tasks:
                 rows = 1   # not written without CRR_IN_EMIT_TASKS
             T["out_" + name] = torch.zeros(rows * dt.itemsize, dtype=torch.uint8, device=dev)
+            if init_host is not None and name != "tasks":
+                src = init_host.tables[name].view(np.uint8).reshape(-1)
+                T["out_" + name][:src.size].copy_(torch.from_numpy(src))
             setattr(co, name, T["out_" + name].data_ptr())
         T["scratch"] = torch.zeros(2 * batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)
         co.scratch = T["scratch"].data_ptr()

@@ -48,6 +48,12 @@ class HistoryBatch:
     # CRR_IN_TIERED: (large_begin, wide_begin, big_begin) -- lane workflows ordered by expected
     # live-set size; long-tail workflows no fast per-wave arena is expected to hold from big_begin on
     tiers: Optional[Tuple[int, int, int]] = None
+    # CRR_WF_FLAG_RESUME: the loaded mutable states (batch order) the output rows start from
+    init: Optional["LoadedStates"] = None
+    # per-workflow key id -> string tables (batch order): (begin, count, off, len, arena), the strings of
+    # loaded rows for the oracle; interners: the host's per-workflow string -> key maps (batch order)
+    key_dict: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]] = None
+    interners: Optional[List[Dict[str, int]]] = None
 
     def wf_strides(self) -> np.ndarray:
         """Column / row stride of every workflow."""
@@ -77,9 +83,75 @@ def _zeros_cols(n):
     return {name: np.zeros(n, dtype=t) for name, t in abi.EVENT_COLUMNS}
 
 
+@dataclasses.dataclass
+class LoadedStates:
+    """Loaded mutable states (``mutableStateBuilder.Load``) as the engine's row images, one per workflow
+    of a batch (batch order): ``exec`` rows (all zero, counts 0, for a workflow that is not resumed),
+    each table's live rows concatenated in workflow order (counts = the exec rows' n_* fields) and the
+    resume mask.  ``ReplayResult.to_loaded`` builds one from a replay's output."""
+    exec: np.ndarray                      # abi.EXEC_ROW [n]
+    rows: Dict[str, np.ndarray]           # table -> live rows, workflow-major
+    mask: np.ndarray                      # bool [n]: resume this workflow
+    interners: Optional[List[Dict[str, int]]] = None
+
+    def counts(self, name: str) -> np.ndarray:
+        n_f = {t[0]: t[4] for t in abi.TABLES}[name]
+        return np.maximum(self.exec[n_f].astype(np.int64), 0)
+
+    def permuted(self, perm: np.ndarray) -> "LoadedStates":
+        rows = {}
+        for name in self.rows:
+            c = self.counts(name)
+            off = np.cumsum(c) - c
+            cp = c[perm]
+            idx = np.repeat(off[perm], cp) + (np.arange(int(cp.sum())) - np.repeat(np.cumsum(cp) - cp, cp))
+            rows[name] = self.rows[name][idx]
+        its = [self.interners[i] for i in perm] if self.interners is not None else None
+        return LoadedStates(self.exec[perm].copy(), rows, self.mask[perm].copy(), its)
+
+
+def write_init(batch: "HistoryBatch", exec_rows: np.ndarray, tables: Dict[str, np.ndarray]):
+    """Place the batch's loaded states into output buffers (host images of crr_outputs): the exec
+    rows of resumed workflows and their live rows in slots 0..n-1 of their slot tables."""
+    init = batch.init
+    if init is None:
+        return
+    m = init.mask
+    exec_rows[m] = init.exec[m]
+    st = batch.wf_strides()
+    for name, _dt, base_f, _cap_f, _n_f in abi.TABLES:
+        if name not in init.rows:
+            continue
+        c = init.counts(name)
+        tot = int(c.sum())
+        if tot == 0:
+            continue
+        wf_idx = np.repeat(np.arange(batch.n_wf), c)
+        slot = np.arange(tot) - np.repeat(np.cumsum(c) - c, c)
+        idx = batch.wf[base_f].astype(np.int64)[wf_idx] + slot * st[wf_idx]
+        tables[name][idx] = init.rows[name]
+
+
+def key_dict_from_interners(interners: List[Dict[str, int]]):
+    """(begin, count, off, len, arena) of the per-workflow key id -> string tables."""
+    strs, begin, count = [], np.zeros(len(interners), np.uint32), np.zeros(len(interners), np.uint32)
+    for w, ids in enumerate(interners):
+        inv = [""] * len(ids)
+        for k, v in ids.items():
+            inv[v] = k
+        begin[w] = len(strs)
+        count[w] = len(inv)
+        strs.extend(inv)
+    enc = [x.encode() for x in strs]
+    lens = np.array([len(e) for e in enc] or [0], np.uint32)
+    offs = (np.cumsum(lens) - lens).astype(np.uint32)
+    arena = np.frombuffer(b"".join(enc) or b"\0", np.uint8).copy()
+    return begin, count, offs, lens, arena
+
+
 class _Interner:
-    def __init__(self):
-        self.ids = {"": 0}
+    def __init__(self, ids: Optional[Dict[str, int]] = None):
+        self.ids = ids if ids is not None else {"": 0}
 
     def __call__(self, s) -> int:
         s = "" if s is None else str(s)
@@ -99,12 +171,18 @@ def _domain_status(name, known_domains) -> int:
 
 
 def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
-            new_run_index: Optional[Dict[int, int]] = None) -> HistoryBatch:
+            new_run_index: Optional[Dict[int, int]] = None, loaded: Optional[LoadedStates] = None,
+            interners: Optional[List[Dict[str, int]]] = None) -> HistoryBatch:
     """Flatten object histories into a canonical HistoryBatch.
 
     ``known_domains``: domain names the domain cache resolves (None: all resolve).
     CAN events reference their new-run history through attrs["new_run"] = workflow index.
+    ``loaded``: ApplyEvents continues these loaded states (``loaded.mask``; CRR_WF_FLAG_RESUME) --
+    the histories are then the new batches only; their keys are interned with ``loaded.interners``
+    (or ``interners``) so they match the loaded rows' keys.
     """
+    if loaded is not None and interners is None:
+        interners = loaded.interners
     n_ev = sum(len(b) for h in histories for b in h.batches)
     cols = _zeros_cols(n_ev)
     key_off = np.zeros(n_ev, np.uint32)
@@ -127,8 +205,10 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         key_len[i] = len(s.encode())
 
     i = 0
+    interners_out: List[Dict[str, int]] = []
     for w, h in enumerate(histories):
-        intern = _Interner()
+        intern = _Interner(interners[w] if interners is not None else None)
+        interners_out.append(intern.ids)
         begin = i
         empty_at = -1
         n_act = n_timer = n_child = n_rc = n_sig = n_dtc = 0
@@ -264,6 +344,8 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
             r["final_token_off"] = 0
             r["final_token_len"] = abi.NO_TOKEN
         r["flags"] = (abi.WF_FLAG_NEW_RUN if h.is_new_run else 0) | (abi.WF_FLAG_REFRESH_TASKS if h.refresh_tasks else 0)
+        if loaded is not None and loaded.mask[w]:
+            r["flags"] |= abi.WF_FLAG_RESUME
         caps["act_cap"][w] = n_act
         caps["timer_cap"][w] = n_timer
         caps["child_cap"][w] = n_child
@@ -273,6 +355,10 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         caps["task_cap"][w] = n_tasks
         r["retention_days"] = h.retention_days
         caps["rp_cap"][w] = max_prev * max(1, sum(1 for e in h.events if e.event_type == ET.WorkflowExecutionStarted)) + n_dtc
+    if loaded is not None:   # the loaded rows plus this call's inserts
+        for name, _dt, _b, cap_f, n_f in abi.TABLES:
+            if name != "tasks":
+                caps[cap_f] += np.where(loaded.mask, loaded.exec[n_f], 0).astype(np.int64)
     batch = HistoryBatch(
         cols=cols,
         act_side=np.array(act_side or [(0,) * 8], dtype=abi.ACTIVITY_SIDE),
@@ -283,6 +369,10 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         key_off=key_off, key_len=key_len,
         key_arena=np.frombuffer(bytes(key_arena) or b"\0", dtype=np.uint8).copy())
     assign_canonical_tables(batch, caps)
+    batch.interners = interners_out
+    batch.key_dict = key_dict_from_interners(interners_out)
+    if loaded is not None:
+        batch.init = loaded
     return batch
 
 
@@ -333,6 +423,12 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     longs = order[is_long]
     bounds = live_set_bounds(batch) if (tiered and n) else None
     tier = tier_classes(batch, bounds) if (tiered and n) else np.zeros(n, np.int64)
+    if tiered and n:
+        # a loaded state is continued in place over its HBM rows: the wide (GlobalTables) segment, and
+        # in the long tail the replay_big_kernel segment (whose HBM-row pass continues it)
+        resumed = (batch.wf["flags"] & abi.WF_FLAG_RESUME) != 0
+        tier = np.where(resumed, 2, tier)
+        bounds = {k: np.where(resumed, np.iinfo(np.int32).max, v) for k, v in bounds.items()}
     n_big = 0
     if tiered:
         lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
@@ -410,11 +506,16 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
 
     wf = batch.wf[perm].copy()
     wf["ev_begin"] = dev_begin
+    kd = None
+    if batch.key_dict is not None:
+        kb, kc, ko, kl, ka = batch.key_dict
+        kd = (kb[perm].copy(), kc[perm].copy(), ko, kl, ka)
     out = HistoryBatch(cols=cols, act_side=act_side, start_side=start_side,
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
                        wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks,
-                       tiers=tiers)
+                       tiers=tiers, init=batch.init.permuted(perm) if batch.init is not None else None,
+                       key_dict=kd, interners=[batch.interners[i] for i in perm] if batch.interners else None)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)
         cap[:n_lane] = wf[cap_f][:n_lane]

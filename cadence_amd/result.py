@@ -7,7 +7,7 @@ from typing import Dict
 import numpy as np
 
 from . import abi
-from .flatten import HistoryBatch
+from .flatten import HistoryBatch, LoadedStates, write_init
 
 
 @dataclasses.dataclass
@@ -24,6 +24,29 @@ class ReplayResult:
             out[name] = self.tables[name][idx]
         return out
 
+    def to_loaded(self, batch: HistoryBatch, mask=None) -> LoadedStates:
+        """The replayed states as loaded states for a following ApplyEvents call (canonical workflow
+        order, as persisted and re-read by Load): the workflows in ``mask`` (default: status OK)."""
+        ex = to_canonical_order(batch, self).copy()
+        m = (ex["status"] == 0) if mask is None else np.asarray(mask, bool)
+        live = _live_canonical(batch, self)
+        rows = {}
+        for name, _dt, _b, _c, n_f in abi.TABLES:
+            if name == "tasks":
+                continue
+            c = np.maximum(ex[n_f].astype(np.int64), 0)
+            keep = np.repeat(m, c)
+            rows[name] = live[name][keep].copy()
+        ex[~m] = np.zeros(1, abi.EXEC_ROW)
+        ex["n_tasks"] = 0
+        its = None
+        if batch.interners is not None:
+            its = batch.interners if batch.perm is None else [None] * batch.n_wf
+            if batch.perm is not None:
+                for p, c in enumerate(batch.perm):
+                    its[c] = batch.interners[p]
+        return LoadedStates(ex, rows, m, its)
+
 
 def allocate_host(batch: HistoryBatch) -> ReplayResult:
     ex = np.zeros(max(batch.n_wf, 1), dtype=abi.EXEC_ROW)[:batch.n_wf]
@@ -31,6 +54,7 @@ def allocate_host(batch: HistoryBatch) -> ReplayResult:
     for name, dt, *_ in abi.TABLES:
         rows = batch.table_rows.get(name, 0) if (name != "tasks" or batch.emit_tasks) else 0
         tables[name] = np.zeros(max(rows, 1), dtype=dt)
+    write_init(batch, ex, tables)
     return ReplayResult(ex, tables)
 
 

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define CRR_ABI_VERSION 3
+#define CRR_ABI_VERSION 4
 
 /* ---- constants restated from the reference ------------------------------------------------ */
 /* common/constants.go:30-58 */
@@ -253,6 +253,18 @@ typedef struct crr_workflow {
  * (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): clear every pending activity's
  * TimerTaskStatus and user timer's TaskStatus, then CreateNextActivityTimer / CreateNextUserTimer. */
 #define CRR_WF_FLAG_REFRESH_TASKS 2
+/* ApplyEvents onto a LOADED mutable state (NewStateBuilder(shard, logger, mutableState, ...) with the
+ * state mutableStateBuilder.Load (mutable_state_builder.go:306-349) built from persistence; the passive
+ * replication path ndc/history_replicator.go:385-460 -> stateBuilder.ApplyEvents :396).  On entry
+ * out.exec[w] and slots 0..n-1 of the workflow's slot tables hold the loaded state (the image this
+ * engine writes: live rows, any order); the call continues from it and rewrites them in place, as
+ * ApplyEvents mutates the caller-owned MutableState.  Read from the exec row: every WorkflowExecutionInfo
+ * field of the row, the n_* counts, token_src (1: the descriptor's start token is the loaded current
+ * branch token), decision_start_to_close, expiration_ns and src_next (the provenance offset: step s of
+ * this call is written as src_next + s).  As in Load, currentVersion starts at EmptyVersion and every
+ * loaded activity is mapped by its ActivityID (duplicates: the latest scheduled one).  Capacities must
+ * cover the loaded rows plus this call's inserts. */
+#define CRR_WF_FLAG_RESUME 4
 
 typedef struct crr_inputs {
     crr_events               ev;
@@ -290,7 +302,9 @@ typedef struct crr_inputs {
                                    CRR_IN_LDS_SMALL (which it overrides): speed only, never results */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
-/* WorkflowExecutionInfo numeric image + engine status (192 B). */
+/* WorkflowExecutionInfo numeric image + engine status (208 B).  "step" / "*_src" values below are
+ * provenance references: src_next of the resumed state (0 for a replay from scratch) + the step index
+ * of the event in this call's history. */
 typedef struct crr_exec_row {
     int32_t  status;                 /* crr_status_code */
     int32_t  fail_step;              /* step index of the failing event, or -1 */
@@ -311,8 +325,12 @@ typedef struct crr_exec_row {
     uint32_t checksum;               /* crc32.ChecksumIEEE of the thriftrw payload (crc.go:46) */
     uint32_t payload_len;            /* bytes the checksum was computed over (0x59 preamble included) */
     int32_t  n_tasks;                /* task rows written (CRR_IN_EMIT_TASKS) */
+    int32_t  decision_start_to_close;/* executionInfo.DecisionStartToCloseTimeout (transient decisions) */
+    int64_t  expiration_ns;          /* executionInfo.ExpirationTime, Unix ns (0: unset) */
+    int32_t  src_next;               /* provenance space: the *_src / fail_step values of this row are
+                                        < src_next (= the resumed row's src_next + this call's events) */
     int32_t  reserved;
-} crr_exec_row;
+} crr_exec_row;                      /* 208 B */
 
 #define CRR_EXEC_CANCEL_REQUESTED  1u
 #define CRR_EXEC_RESET_POINTS_SET  2u   /* AutoResetPoints != nil */
@@ -329,7 +347,8 @@ typedef struct crr_activity_row {
     int32_t  timer_task_status;
     uint32_t key;                                /* interned ActivityID */
     uint32_t flags;                              /* CRR_ROW_* */
-    int32_t  reserved[3];
+    int32_t  reserved;
+    int64_t  last_heartbeat_time;                /* LastHeartBeatUpdatedTime (== started_time on replay) */
 } crr_activity_row;
 
 /* persistence.TimerInfo numeric image (40 B). */

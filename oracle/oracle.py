@@ -33,6 +33,8 @@ def lib():
         vp = ctypes.c_void_p
         L.oracle_replay.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int]
         L.oracle_replay.restype = ctypes.c_int
+        L.oracle_replay2.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int]
+        L.oracle_replay2.restype = ctypes.c_int
         L.oracle_payload.argtypes = [vp, vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int]
         L.oracle_payload.restype = ctypes.c_int
         L.oracle_crc32.argtypes = [vp, ctypes.c_size_t]
@@ -96,11 +98,16 @@ def replay(batch: HistoryBatch, n_threads: int = 0) -> ReplayResult:
     """Replay every workflow of ``batch`` on the host (oracle)."""
     if batch.key_off is None:
         raise ValueError("oracle needs per-event key strings (batch.key_off / key_len / key_arena)")
-    res = allocate_host(batch)
+    res = allocate_host(batch)          # loaded states (CRR_WF_FLAG_RESUME) already in place
     hi = _HostInputs(batch)
     co = _outputs(res)
-    rc = lib().oracle_replay(ctypes.byref(hi.c), _ptr(hi.key_off), _ptr(hi.key_len), _ptr(hi.key_arena),
-                             ctypes.byref(co), int(n_threads))
+    if batch.key_dict is not None:
+        kd = [np.ascontiguousarray(a) for a in batch.key_dict]
+        rc = lib().oracle_replay2(ctypes.byref(hi.c), _ptr(hi.key_off), _ptr(hi.key_len), _ptr(hi.key_arena),
+                                  *[_ptr(a) for a in kd], ctypes.byref(co), int(n_threads))
+    else:
+        rc = lib().oracle_replay(ctypes.byref(hi.c), _ptr(hi.key_off), _ptr(hi.key_len), _ptr(hi.key_arena),
+                                 ctypes.byref(co), int(n_threads))
     if rc != 0:
         raise RuntimeError(f"oracle_replay failed: {rc}")
     return res

@@ -55,16 +55,34 @@ struct KeyStrings {  // per-event key strings (ActivityID / TimerID / BinaryChec
   const char* arena;
 };
 
+// Per-workflow key id -> string (the host interner's inverse): the strings of a loaded state's rows
+// (ActivityID / TimerID / BinaryChecksum), which no event of this call carries.
+struct KeyDict {
+  const uint32_t* begin = nullptr;
+  const uint32_t* count = nullptr;
+  const uint32_t* off = nullptr;
+  const uint32_t* len = nullptr;
+  const char* arena = nullptr;
+  bool ok() const { return begin != nullptr; }
+  std::string str(uint32_t w, uint32_t key) const {
+    const uint32_t i = begin[w] + key;
+    return key < count[w] ? std::string(arena + off[i], len[i]) : std::string();
+  }
+};
+
 // per-workflow column/row stride: the long-history tail of a CRR_IN_WAVE_TAIL batch is contiguous
 inline i64 stride_of(const crr_inputs* in, const crr_workflow* wf) {
   return ((in->flags & CRR_IN_WAVE_TAIL) && (uint32_t)(wf - in->wf) >= in->wave_begin) ? 1 : (i64)in->stride;
 }
 
+// Steps are provenance steps: this call's event k is step sb + k, where sb is the resumed state's
+// src_next (0 for a replay from scratch), so every *_src / fail_step value matches the engine's.
 struct WfView {
   const crr_inputs* in;
   const crr_workflow* wf;
   const KeyStrings* ks;
-  i64 idx(int step) const { return wf->ev_begin + (i64)step * stride_of(in, wf); }
+  int sb;
+  i64 idx(int step) const { return wf->ev_begin + (i64)(step - sb) * stride_of(in, wf); }
   int type(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_MASK; }
   bool first(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_BATCH_FIRST; }
   bool last(int step) const { return in->ev.etype[idx(step)] & CRR_ETYPE_BATCH_LAST; }
@@ -547,18 +565,20 @@ class Replayer {
   Replayer(const crr_inputs* in, const KeyStrings* ks, const Outcome* phase0)
       : in_(in), ks_(ks), phase0_(phase0) {}
 
-  // Replays workflow `w` from a fresh NewMutableStateBuilderWithVersionHistories (:245-254).
-  Outcome replay(uint32_t w, MutableState& ms) {
+  // Replays workflow `w` from a fresh NewMutableStateBuilderWithVersionHistories (:245-254), or, for a
+  // CRR_WF_FLAG_RESUME workflow, from the state `ms` already holds (load_state: mutableStateBuilder.Load)
+  // with provenance steps starting at `sb`.
+  Outcome replay(uint32_t w, MutableState& ms, int sb = 0) {
     const crr_workflow* wf = &in_->wf[w];
-    WfView v{in_, wf, ks_};
-    ms.currentVersion = wf->init_version;  // domainEntry.GetFailoverVersion() (:207)
+    WfView v{in_, wf, ks_, sb};
+    if (!(wf->flags & CRR_WF_FLAG_RESUME)) ms.currentVersion = wf->init_version;  // GetFailoverVersion() (:207)
     ms.now_ns = wf->now_ns;
     ms.emit_tasks = (in_->flags & CRR_IN_EMIT_TASKS) != 0;
     Outcome out;
-    int k = 0;
-    const int n = wf->ev_count;
+    int k = sb;
+    const int n = sb + wf->ev_count;
     for (;;) {
-      if (k == wf->empty_batch_at) {  // an ApplyEvents call with an empty batch (state_builder.go:98-100)
+      if (k - sb == wf->empty_batch_at) {  // an ApplyEvents call with an empty batch (state_builder.go:98-100)
         out.status = CRR_ERR_EMPTY_HISTORY;
         out.fail_step = k;
         return out;
@@ -989,7 +1009,7 @@ uint32_t crc32_ieee_bitwise(const uint8_t* p, size_t n) {
 
 // ---- row export ------------------------------------------------------------------------------------
 void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const Outcome& oc,
-                 const crr_outputs* out) {
+                 const crr_outputs* out, int src_next) {
   const crr_workflow* wf = &in->wf[w];
   const i64 st = stride_of(in, wf);
   crr_exec_row& r = out->exec[w];
@@ -1019,6 +1039,9 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
   r.decision_request_src = x.decision_request_src;
   r.start_src = x.start_src;
   r.token_src = ms.vh.token_src;
+  r.decision_start_to_close = x.decision_start_to_close_timeout;
+  r.expiration_ns = ms.expiration_ns;
+  r.src_next = src_next;
 
   // pending activities sorted by ScheduleID
   std::vector<const ActivityInfo*> acts;
@@ -1036,6 +1059,7 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
     o.schedule_to_start = a.schedule_to_start; o.schedule_to_close = a.schedule_to_close;
     o.start_to_close = a.start_to_close; o.heartbeat = a.heartbeat;
     o.timer_task_status = a.timer_task_status; o.key = a.key;
+    o.last_heartbeat_time = a.last_heartbeat_updated_time;
     auto m = ms.pendingActivityIDToEventID.find(a.activity_id);
     bool mapped = m != ms.pendingActivityIDToEventID.end() && m->second == a.schedule_id;
     o.flags = CRR_ROW_LIVE | (mapped ? CRR_ROW_MAPPED : 0u) | (a.cancel_requested ? CRR_ROW_CANCEL_REQUESTED : 0u) |
@@ -1103,9 +1127,98 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
   }
 }
 
+// mutableStateBuilder.Load (mutable_state_builder.go:306-349) from the engine's row image of a loaded
+// state (out->exec[w] and slots 0..n-1 of the workflow's tables).  Returns the provenance base (src_next).
+int load_state(const crr_inputs* in, uint32_t w, const crr_outputs* out, const KeyDict& kd, MutableState& ms) {
+  const crr_workflow* wf = &in->wf[w];
+  const i64 st = stride_of(in, wf);
+  const crr_exec_row X = out->exec[w];
+  ExecutionInfo& x = ms.exec;
+  x.state = X.state; x.close_status = X.close_status;
+  x.next_event_id = X.next_event_id; x.last_first_event_id = X.last_first_event_id;
+  x.last_event_task_id = X.last_event_task_id; x.last_processed_event = X.last_processed_event;
+  x.completion_event_batch_id = X.completion_event_batch_id;
+  x.decision_version = X.decision_version; x.decision_schedule_id = X.decision_schedule_id;
+  x.decision_started_id = X.decision_started_id; x.decision_request_src = X.decision_request_src;
+  x.decision_timeout = X.decision_timeout; x.decision_attempt = X.decision_attempt;
+  x.decision_started_ts = X.decision_started_ts; x.decision_scheduled_ts = X.decision_scheduled_ts;
+  x.decision_orig_scheduled_ts = X.decision_orig_scheduled_ts;
+  x.signal_count = X.signal_count;
+  x.cancel_requested = (X.flags & CRR_EXEC_CANCEL_REQUESTED) != 0;
+  x.decision_start_to_close_timeout = X.decision_start_to_close;
+  x.start_src = X.start_src;
+  x.auto_reset_points_set = (X.flags & CRR_EXEC_RESET_POINTS_SET) != 0;
+  ms.expiration_ns = X.expiration_ns;
+  ms.currentVersion = CRR_EMPTY_VERSION;  // e.currentVersion = common.EmptyVersion (:324)
+  ms.vh.token_src = X.token_src;
+  for (int i = 0; i < X.n_vh_items; ++i) {
+    const crr_vh_item& it = out->vh[wf->vh_base + (i64)i * st];
+    ms.vh.items.push_back({it.event_id, it.version});
+  }
+  // e.pendingActivityInfoIDs = state.ActivityInfos; then pendingActivityIDToEventID[ActivityID] =
+  // ScheduleID for every info (:311-314).  Go iterates a map: among duplicate ActivityIDs the winner is
+  // arbitrary; this restatement (and the engine) let the latest scheduled one win.
+  std::vector<i64> sids;
+  for (int i = 0; i < X.n_activity; ++i) {
+    const crr_activity_row& o = out->act[wf->act_base + (i64)i * st];
+    ActivityInfo a;
+    a.version = o.version; a.schedule_id = o.schedule_id; a.scheduled_batch_id = o.scheduled_batch_id;
+    a.scheduled_time = o.scheduled_time; a.started_id = o.started_id; a.started_time = o.started_time;
+    a.activity_id = kd.str(w, o.key); a.key = o.key;
+    a.sched_src = o.sched_src; a.started_src = o.started_src;
+    a.schedule_to_start = o.schedule_to_start; a.schedule_to_close = o.schedule_to_close;
+    a.start_to_close = o.start_to_close; a.heartbeat = o.heartbeat;
+    a.cancel_requested = (o.flags & CRR_ROW_CANCEL_REQUESTED) != 0;
+    a.cancel_request_id = o.cancel_request_id;
+    a.last_heartbeat_updated_time = o.last_heartbeat_time;
+    a.timer_task_status = o.timer_task_status;
+    a.has_retry_policy = (o.flags & CRR_ROW_HAS_RETRY) != 0;
+    a.last_hb_timeout_vis_s = o.last_hb_timeout_vis_s;
+    ms.pendingActivityInfoIDs[a.schedule_id] = a;
+    sids.push_back(a.schedule_id);
+  }
+  std::sort(sids.begin(), sids.end());
+  for (i64 sid : sids) ms.pendingActivityIDToEventID[ms.pendingActivityInfoIDs[sid].activity_id] = sid;
+  for (int i = 0; i < X.n_timer; ++i) {  // e.pendingTimerInfoIDs = state.TimerInfos (+ StartedID -> TimerID)
+    const crr_timer_row& o = out->timer[wf->timer_base + (i64)i * st];
+    TimerInfo t;
+    t.version = o.version; t.timer_id = kd.str(w, o.key); t.key = o.key;
+    t.started_id = o.started_id; t.expiry_time = o.expiry_time; t.task_status = o.task_status; t.src = o.src;
+    ms.pendingTimerInfoIDs[t.timer_id] = t;
+    ms.pendingTimerEventIDToID[t.started_id] = t.timer_id;
+  }
+  for (int i = 0; i < X.n_child; ++i) {
+    const crr_child_row& o = out->child[wf->child_base + (i64)i * st];
+    ChildExecutionInfo c;
+    c.version = o.version; c.initiated_id = o.initiated_id; c.initiated_batch_id = o.initiated_batch_id;
+    c.started_id = o.started_id; c.src = o.src; c.started_src = o.started_src;
+    ms.pendingChildExecutionInfoIDs[c.initiated_id] = c;
+  }
+  auto load_init = [&](const crr_initiated_row* rows, i64 base, int n, std::unordered_map<i64, InitiatedInfo>& m) {
+    for (int i = 0; i < n; ++i) {
+      const crr_initiated_row& o = rows[base + (i64)i * st];
+      InitiatedInfo r;
+      r.version = o.version; r.initiated_batch_id = o.initiated_batch_id; r.initiated_id = o.initiated_id; r.src = o.src;
+      m[r.initiated_id] = r;
+    }
+  };
+  load_init(out->rc, wf->rc_base, X.n_rc, ms.pendingRequestCancelInfoIDs);
+  load_init(out->sig, wf->sig_base, X.n_signal, ms.pendingSignalInfoIDs);
+  for (int i = 0; i < X.n_reset_points; ++i) {  // executionInfo.AutoResetPoints.Points
+    const crr_reset_point_row& o = out->rp[wf->rp_base + (i64)i * st];
+    ResetPoint p;
+    p.src = o.src; p.prev_index = o.prev_index; p.key = o.key;
+    p.checksum = o.prev_index < 0 ? kd.str(w, o.key) : std::string();
+    p.resettable = (o.flags & CRR_ROW_RESETTABLE) != 0;
+    x.reset_points.push_back(p);
+  }
+  return X.src_next;
+}
+
 struct RunCtx {
   const crr_inputs* in;
   const KeyStrings* ks;
+  const KeyDict* kd;
   const crr_outputs* out;
   std::vector<Outcome>* phase0;
 };
@@ -1120,10 +1233,12 @@ void run_range(const RunCtx& c, uint32_t lo, uint32_t hi, int phase, std::atomic
       bool is_new_run = (c.in->wf[w].flags & CRR_WF_FLAG_NEW_RUN) != 0;
       if ((phase == 0) != is_new_run) continue;
       MutableState ms;
+      int sb = 0;
+      if (c.in->wf[w].flags & CRR_WF_FLAG_RESUME) sb = load_state(c.in, w, c.out, *c.kd, ms);
       Replayer rep(c.in, c.ks, phase == 0 ? nullptr : c.phase0->data());
-      Outcome oc = rep.replay(w, ms);
+      Outcome oc = rep.replay(w, ms, sb);
       if (phase == 0) (*c.phase0)[w] = oc;
-      export_rows(c.in, w, ms, oc, c.out);
+      export_rows(c.in, w, ms, oc, c.out, sb + c.in->wf[w].ev_count);
     }
   }
 }
@@ -1134,12 +1249,18 @@ extern "C" {
 
 // Replays every workflow of `in` (host pointers) into `out` (host pointers, same row layout as the
 // device engine).  key_off/key_len/key_arena give the per-event key strings.  n_threads <= 0: all.
-int oracle_replay(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len, const char* key_arena,
-                  const crr_outputs* out, int n_threads) {
+// Workflows flagged CRR_WF_FLAG_RESUME continue the loaded state their rows in `out` hold (in place);
+// dict_* give each workflow's key id -> string table for those rows (required when any resumes).
+int oracle_replay2(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len, const char* key_arena,
+                   const uint32_t* dict_begin, const uint32_t* dict_count, const uint32_t* dict_off,
+                   const uint32_t* dict_len, const char* dict_arena, const crr_outputs* out, int n_threads) {
   if (!in || !out) return -1;
   KeyStrings ks{key_off, key_len, key_arena};
+  KeyDict kd{dict_begin, dict_count, dict_off, dict_len, dict_arena};
+  for (uint32_t w = 0; w < in->n_wf; ++w)
+    if ((in->wf[w].flags & CRR_WF_FLAG_RESUME) && !kd.ok()) return -2;
   std::vector<Outcome> phase0(in->n_wf);
-  RunCtx c{in, &ks, out, &phase0};
+  RunCtx c{in, &ks, &kd, out, &phase0};
   if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
   for (int phase = 0; phase < 2; ++phase) {
     std::atomic<uint32_t> next{0};
@@ -1152,6 +1273,11 @@ int oracle_replay(const crr_inputs* in, const uint32_t* key_off, const uint32_t*
     }
   }
   return 0;
+}
+
+int oracle_replay(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len, const char* key_arena,
+                  const crr_outputs* out, int n_threads) {
+  return oracle_replay2(in, key_off, key_len, key_arena, nullptr, nullptr, nullptr, nullptr, nullptr, out, n_threads);
 }
 
 // Writes the checksum payload bytes of workflow `w` after replay (for golden-vector tests).

@@ -1,0 +1,69 @@
+"""GPU: ApplyEvents onto loaded mutable states (CRR_WF_FLAG_RESUME) through the C ABI.
+
+Batches 1..k of every history are replayed on the device, downloaded, re-uploaded as the loaded
+states, and batches k+1..n are replayed onto them.  The device rows equal the oracle's for the same
+split (every workflow, every field, bit-exact), and equal the one-shot device replay wherever Load
+reproduces the in-memory state (tests/resume_cases.py).
+"""
+import numpy as np
+import pytest
+
+from cadence_amd import synth_mixed
+from cadence_amd.flatten import flatten, interleave
+from cadence_amd.result import diff_results, to_canonical_order
+
+from resume_cases import KNOWN, compare_split_with_one_shot, load_stable, loaded_from, split_histories
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from cadence_amd.engine import ReplayEngine
+    return ReplayEngine(0)
+
+
+def _oracle():
+    from oracle import oracle
+    return oracle
+
+
+def _device_split(engine, hs, seed, layout, last_only=False):
+    one_b = layout(flatten(hs, known_domains=KNOWN))
+    one = engine.replay(one_b)
+    pre, suf, mask = split_histories(hs, seed, last_only)
+    pre_b = layout(flatten(pre, known_domains=KNOWN))
+    pre_r = engine.replay(pre_b)                       # device prefix -> downloaded rows
+    d = diff_results(pre_b, pre_r, pre_b, _oracle().replay(pre_b, 0))
+    assert not d, "\n".join(d)
+    loaded = loaded_from(pre_b, pre_r, mask)           # re-uploaded as the loaded states
+    suf_b = layout(flatten(suf, known_domains=KNOWN, loaded=loaded))
+    suf_r = engine.replay(suf_b)
+    want = _oracle().replay(suf_b, 0)                  # the oracle given the same split
+    d = diff_results(suf_b, suf_r, suf_b, want)
+    assert not d, "\n".join(d)
+    n = compare_split_with_one_shot(one_b, one, to_canonical_order(pre_b, pre_r), suf_b, suf_r, load_stable(loaded))
+    return loaded, n
+
+
+@pytest.mark.parametrize("layout", ["interleaved", "canonical", "lanes_only"])
+def test_resume_mixed_all_layouts(engine, layout):
+    lay = {"interleaved": interleave, "canonical": lambda b: b,
+           "lanes_only": lambda b: interleave(b, long_threshold=None)}[layout]
+    hs = synth_mixed.mixed_histories(3000, 61, multi_version=True, invalid_rate=0.1, can_rate=0.3)
+    loaded, n = _device_split(engine, hs, 5, lay)
+    assert loaded.mask.sum() > 1500 and n > 1200
+
+
+def test_resume_long_histories_wavefront_path(engine):
+    """Long resumed histories take the long-tail segment (replay_big_kernel: HBM-row wavefront pass)."""
+    hs = synth_mixed.long_tail_histories(150, 62, max_len=4000, run_cap=2000, multi_version=True, caps=None)
+    loaded, n = _device_split(engine, hs, 6, interleave)
+    assert n > 50
+
+
+def test_resume_passive_replication_last_batch(engine):
+    """One replication task per workflow: the last batch applied onto the loaded state."""
+    hs = synth_mixed.mixed_histories(4000, 63, multi_version=True)
+    loaded, n = _device_split(engine, hs, 7, interleave, last_only=True)
+    assert n > 2500

@@ -333,3 +333,20 @@ def test_rebuild_refresh_tasks_reselects_timers():  # mutable_state_task_refresh
     assert [int(a["timer_task_status"]) for a in live["act"]] == [0, abi.TTS_SCHEDULE_TO_START]
     assert [int(t["task_status"]) for t in live["timer"]] == [0, 1]
     assert r.exec[0]["checksum"] == plain.exec[0]["checksum"]   # the checksum does not cover timer masks
+
+
+# ---- service/history/execution/state_builder_test.go:143-1749: the dispatch table ----------------------
+def test_state_builder_dispatch_table_kats():
+    """All 45 state_builder_test.go cases (tests/kat_state_builder.py): one ApplyEvents batch onto the
+    case's loaded state, the Replicate* effects and Generate* tasks each Go test expects."""
+    import kat_state_builder as K
+    kats = K.cases()
+    assert len(kats) == 44            # + TestApplyEventsNewEventsNotHandled below
+    batch, idx, nr = K.build_batch(kats)
+    res = oracle.replay(batch, 1)
+    fails = K.check_all(kats, batch, res, idx, nr)
+    assert not fails, "\n".join(fails)
+
+
+def test_event_type_count():  # state_builder_test.go:1744-1749 TestApplyEventsNewEventsNotHandled
+    assert len(ET) == 42 == abi.EV_TYPE_COUNT

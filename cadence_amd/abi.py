@@ -202,7 +202,7 @@ ACTIVITY_ROW = np.dtype([
     ("last_hb_timeout_vis_s", "<i8"), ("sched_src", "<i4"), ("started_src", "<i4"),
     ("schedule_to_start", "<i4"), ("schedule_to_close", "<i4"), ("start_to_close", "<i4"),
     ("heartbeat", "<i4"), ("timer_task_status", "<i4"), ("key", "<u4"), ("flags", "<u4"),
-    ("reserved", "<i4"), ("last_heartbeat_time", "<i8")])
+    ("attempt", "<i4"), ("last_heartbeat_time", "<i8")])
 
 TIMER_ROW = np.dtype([
     ("started_id", "<i8"), ("version", "<i8"), ("expiry_time", "<i8"), ("task_status", "<i4"),

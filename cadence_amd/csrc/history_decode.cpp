@@ -10,6 +10,7 @@
 // thrift binary: field header = type byte + big-endian i16 id, i32/i64 big-endian, binary = be32
 // length + bytes, list = element type + be32 count, struct = fields until a 0 byte.
 #include "cadence_decode.h"
+#include "host_flatten.h"
 
 #include <algorithm>
 #include <cstring>
@@ -21,9 +22,7 @@
 
 namespace {
 
-using i64 = int64_t;
-using i32 = int32_t;
-using u32 = uint32_t;
+using namespace crr_host;
 
 enum : uint8_t { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10,
                  T_STRING = 11, T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15 };
@@ -106,28 +105,6 @@ struct Reader {
     skip(got);
     return false;
   }
-};
-
-// ---- the fields one event contributes ----------------------------------------------------------------
-struct Attr {
-  i64 ref = 0;
-  i32 aux = 0;
-  std::string key;           // ActivityID / TimerID / BinaryChecksum
-  bool has_key = false;
-  std::string domain;        // attributes.Domain / ParentWorkflowDomain
-  // ActivityTaskScheduled
-  i32 s2s = 0, s2c = 0, st2c = 0, hb = 0, has_retry = 0, expiration = 0;
-  // WorkflowExecutionStarted
-  i32 task_s2c = 0, exec_s2c = 0, backoff = 0, initiator = CRR_INITIATOR_NIL, attempt = 0;
-  i64 expiration_ts = 0;
-  int prev_mode = -1;        // -1: PrevAutoResetPoints nil, -2: Points nil, 0: list
-  std::vector<std::string> prev;
-};
-
-struct Event {
-  i64 id = 0, ts = 0, ver = 0, task = 0;
-  i32 type = 0;
-  Attr a;
 };
 
 // Attribute field id (in HistoryEvent) -> event type: 40 + 10 * type for every type
@@ -328,31 +305,6 @@ void read_event(Reader& r, Event& e) {
   }
 }
 
-// tasks the task generator adds per event type (state_builder.go:157-625), an upper bound
-constexpr int8_t kTasksPerEvent[CRR_EV_TYPE_COUNT] = {
-    3, 2, 2, 2, 1, 1, 0, 1, 1, 1,   // 0 Started(+backoff) 1-3 closes 4 DTSched 5 DTStarted 6 DTCompleted 7-8 DT fail 9 ATSched
-    0, 0, 0, 0, 0, 0, 0, 0, 0, 0,   // 10-19
-    0, 0, 2, 1, 0, 0, 0, 0, 2, 2,   // 22 Canceled 23 RCInitiated 28 Terminated 29 ContinuedAsNew
-    1, 0, 0, 0, 0, 0, 0, 0, 1, 0,   // 30 StartChildInitiated 38 SignalInitiated
-    0, 1};                          // 41 Upsert
-
-// ---- per-chunk output --------------------------------------------------------------------------------
-struct Chunk {
-  std::vector<uint8_t> etype;
-  std::vector<i64> id, ver, ts, task, ref;
-  std::vector<u32> key;
-  std::vector<i32> aux;
-  std::vector<u32> key_off, key_len;
-  std::string key_arena;
-  std::vector<crr_activity_side> act;
-  std::vector<crr_start_side> start;
-  std::vector<u32> reset_keys;
-  std::vector<uint8_t> arena;
-  std::vector<crr_workflow> wf;
-  int err = CRR_DECODE_OK;
-  int64_t err_blob = -1;
-};
-
 struct Ctx {
   const uint8_t* const* blobs;
   const uint64_t* lens;
@@ -361,54 +313,16 @@ struct Ctx {
   const std::unordered_set<std::string>* known;  // null: every name resolves
 };
 
-int domain_status(const Ctx& c, const std::string& name) {
-  if (name.empty()) return CRR_DOMAIN_NOT_SET;
-  if (!c.known || c.known->count(name)) return CRR_DOMAIN_RESOLVED;
-  return CRR_DOMAIN_UNKNOWN;
-}
-
-// NewHistoryBranchTokenByBranchID (dataManagerInterfaces.go:2899-2910): 0x59 + thrift binary
-// HistoryBranch{10 TreeID string, 20 BranchID string, 30 Ancestors list<struct> = []}.
-void branch_token(std::vector<uint8_t>& out, const char* tree, const char* branch) {
-  auto be32 = [&](u32 v) { for (int s = 24; s >= 0; s -= 8) out.push_back((uint8_t)(v >> s)); };
-  const size_t nt = tree ? strlen(tree) : 0, nb = branch ? strlen(branch) : 0;
-  out.push_back(0x59);
-  out.push_back(T_STRING); out.push_back(0); out.push_back(10); be32((u32)nt);
-  out.insert(out.end(), tree, tree + nt);
-  out.push_back(T_STRING); out.push_back(0); out.push_back(20); be32((u32)nb);
-  out.insert(out.end(), branch, branch + nb);
-  out.push_back(T_LIST); out.push_back(0); out.push_back(30); out.push_back(T_STRUCT); be32(0);
-  out.push_back(T_STOP);
-}
-
 void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
   const crr_wf_source& src = c.wfs[w];
-  std::unordered_map<std::string, u32> intern;
-  intern.emplace(std::string(), 0u);
-  auto key_of = [&](const std::string& s) -> u32 {
-    auto it = intern.find(s);
-    if (it != intern.end()) return it->second;
-    const u32 v = (u32)intern.size();
-    intern.emplace(s, v);
-    return v;
-  };
-  crr_workflow d;
-  std::memset(&d, 0, sizeof(d));
-  const i64 begin = (i64)k.etype.size();
-  i32 empty_at = -1;
-  i64 n_act = 0, n_timer = 0, n_child = 0, n_rc = 0, n_sig = 0, n_dtc = 0, n_started = 0, vh_items = 0;
-  i64 max_prev = 0;
-  i64 n_tasks = 0;  // upper bound of the tasks ApplyEvents generates (flatten.TASKS_PER_EVENT)
-  bool have_ver = false;
-  i64 last_ver = 0;
+  WfFlattener f(k, c.known);
   Event e;
   for (uint32_t b = 0; b < src.blob_count; ++b) {
     const uint32_t bi = src.blob_begin + b;
     if (bi >= c.n_blobs) throw DecodeError{CRR_DECODE_BAD_ARGUMENT};
     k.err_blob = bi;
     const uint64_t len = c.lens[bi];
-    i32 n_in_batch = 0;
-    const i64 batch_begin = (i64)k.etype.size();
+    f.batch_begin();
     if (len > 0) {
       Reader r{c.blobs[bi], c.blobs[bi] + len};
       if (r.u8() != 0x59) throw DecodeError{CRR_DECODE_BAD_PREAMBLE};  // version0Thriftrw.go:53-58
@@ -425,127 +339,26 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
         for (i32 i = 0; i < n; ++i) {
           e = Event();
           read_event(r, e);
-          const i32 t = e.type;
-          const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
-          k.etype.push_back((uint8_t)(valid ? t : CRR_EV_PAD - 1));
-          k.id.push_back(e.id);
-          k.ver.push_back(e.ver);
-          k.ts.push_back(e.ts);
-          k.task.push_back(e.task);
-          if (!have_ver || e.ver > last_ver) { ++vh_items; last_ver = e.ver; have_ver = true; }
-          n_tasks += valid ? kTasksPerEvent[t] : 0;
-          i64 ref = 0;
-          u32 key = 0;
-          i32 aux = 0;
-          const std::string* ks = nullptr;
-          Attr& a = e.a;
-          switch (valid ? t : -1) {
-            case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
-              crr_start_side ss;
-              std::memset(&ss, 0, sizeof(ss));
-              if (a.prev_mode == -1) { ss.prev_reset_key_off = 0; ss.prev_reset_count = -1; }
-              else if (a.prev_mode == -2) { ss.prev_reset_key_off = 0; ss.prev_reset_count = -2; }
-              else {
-                ss.prev_reset_key_off = (u32)k.reset_keys.size();
-                ss.prev_reset_count = (i32)a.prev.size();
-                for (const auto& p : a.prev) k.reset_keys.push_back(key_of(p));
-                max_prev = std::max<i64>(max_prev, (i64)a.prev.size());
-              }
-              ss.decision_start_to_close = a.task_s2c;
-              ss.workflow_timeout = a.exec_s2c;
-              ss.first_decision_backoff = a.backoff;
-              ss.initiator = a.initiator;
-              ss.attempt = a.attempt;
-              ss.expiration_ns = a.expiration_ts;
-              // ParentWorkflowDomainID is not on the thrift wire: the name lookup (state_builder.go:137-147)
-              ss.parent_domain_status = domain_status(c, a.domain);
-              k.start.push_back(ss);
-              aux = (i32)k.start.size() - 1;
-              ++n_started;
-              break;
-            }
-            case CRR_EV_DECISION_TASK_SCHEDULED: ref = a.ref; aux = a.aux; break;
-            case CRR_EV_DECISION_TASK_STARTED: ref = a.ref; break;
-            case CRR_EV_DECISION_TASK_COMPLETED: ref = a.ref; ks = &a.key; key = key_of(a.key); ++n_dtc; break;
-            case CRR_EV_DECISION_TASK_TIMED_OUT: aux = a.aux; break;
-            case CRR_EV_ACTIVITY_TASK_SCHEDULED: {
-              ks = &a.key;
-              key = key_of(a.key);
-              crr_activity_side as;
-              std::memset(&as, 0, sizeof(as));
-              as.schedule_to_start = a.s2s; as.schedule_to_close = a.s2c; as.start_to_close = a.st2c;
-              as.heartbeat = a.hb; as.has_retry_policy = a.has_retry; as.expiration_interval = a.expiration;
-              as.domain_status = domain_status(c, a.domain);
-              k.act.push_back(as);
-              aux = (i32)k.act.size() - 1;
-              ++n_act;
-              break;
-            }
-            case CRR_EV_ACTIVITY_TASK_STARTED: case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED:
-            case CRR_EV_ACTIVITY_TASK_TIMED_OUT: case CRR_EV_ACTIVITY_TASK_CANCELED:
-              ref = a.ref; break;
-            case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED: ks = &a.key; key = key_of(a.key); break;
-            case CRR_EV_TIMER_STARTED: ks = &a.key; key = key_of(a.key); ref = a.ref; ++n_timer; break;
-            case CRR_EV_TIMER_FIRED: case CRR_EV_TIMER_CANCELED: ks = &a.key; key = key_of(a.key); break;
-            case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: aux = domain_status(c, a.domain); ++n_child; break;
-            case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED: aux = domain_status(c, a.domain); ++n_rc; break;
-            case CRR_EV_SIGNAL_EXTERNAL_INITIATED: aux = domain_status(c, a.domain); ++n_sig; break;
-            case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:
-            case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED:
-            case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
-            case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED: case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
-            case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED: case CRR_EV_SIGNAL_EXTERNAL_FAILED:
-            case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:
-              ref = a.ref; break;
-            case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: aux = src.new_run_wf; break;
-            default: break;
-          }
-          k.ref.push_back(ref);
-          k.key.push_back(key);
-          k.aux.push_back(aux);
-          k.key_off.push_back((u32)k.key_arena.size());
-          k.key_len.push_back(ks ? (u32)ks->size() : 0u);
-          if (ks) k.key_arena.append(*ks);
-          ++n_in_batch;
+          e.a.new_run = src.new_run_wf;  // ParentWorkflowDomainID is not on the thrift wire: name lookups only
+          f.add(e);
         }
       }
     }
-    if (n_in_batch == 0) {  // an empty batch: ApplyEvents' history-size-zero error (state_builder.go:98-100)
-      if (empty_at < 0) empty_at = (i32)(batch_begin - begin);
-      continue;
-    }
-    n_tasks += 2;  // the batch's timer epilogue
-    k.etype[batch_begin] |= CRR_ETYPE_BATCH_FIRST;
-    k.etype.back() |= CRR_ETYPE_BATCH_LAST;
+    f.batch_end();
   }
   k.err_blob = -1;
-  const i64 n = (i64)k.etype.size() - begin;
-  if (src.blob_count == 0) empty_at = 0;
-  d.ev_begin = begin;
-  d.ev_count = (i32)n;
-  d.empty_batch_at = empty_at;
-  d.init_version = src.init_version;
-  d.now_ns = src.now_ns;
-  d.start_token_off = (u32)k.arena.size();
-  branch_token(k.arena, src.run_id ? src.run_id : "", src.branch_id ? src.branch_id : "");
-  d.start_token_len = (u32)(k.arena.size() - d.start_token_off);
-  if (src.final_token) {
-    d.final_token_off = (u32)k.arena.size();
-    d.final_token_len = src.final_token_len;
-    k.arena.insert(k.arena.end(), src.final_token, src.final_token + src.final_token_len);
-    d.rebuild_last_event_id = src.rebuild_last_event_id;
-    d.rebuild_last_event_version = src.rebuild_last_event_version;
-  } else {
-    d.final_token_off = 0;
-    d.final_token_len = 0xFFFFFFFFu;
-  }
-  d.act_cap = (i32)n_act; d.timer_cap = (i32)n_timer; d.child_cap = (i32)n_child;
-  d.rc_cap = (i32)n_rc; d.sig_cap = (i32)n_sig; d.vh_cap = (i32)vh_items;
-  d.rp_cap = (i32)(max_prev * std::max<i64>(1, n_started) + n_dtc);
-  d.flags = src.flags;
-  d.task_cap = (i32)n_tasks;
-  d.retention_days = src.retention_days;
-  k.wf.push_back(d);
+  WfMeta m;
+  m.init_version = src.init_version;
+  m.now_ns = src.now_ns;
+  m.run_id = src.run_id;
+  m.branch_id = src.branch_id;
+  m.final_token = src.final_token;
+  m.final_token_len = src.final_token_len;
+  m.rebuild_last_event_id = src.rebuild_last_event_id;
+  m.rebuild_last_event_version = src.rebuild_last_event_version;
+  m.flags = src.flags;
+  m.retention_days = src.retention_days;
+  f.finish(m, src.blob_count);
 }
 
 void decode_range(const Ctx& c, uint32_t w0, uint32_t w1, Chunk* k) {
@@ -558,15 +371,7 @@ void decode_range(const Ctx& c, uint32_t w0, uint32_t w1, Chunk* k) {
   }
 }
 
-template <class T>
-void append(std::vector<T>& dst, const std::vector<T>& src) { dst.insert(dst.end(), src.begin(), src.end()); }
-
 }  // namespace
-
-struct crr_decoded {
-  Chunk all;
-  uint64_t table_rows[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-};
 
 extern "C" {
 
@@ -602,45 +407,9 @@ crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* b
       return nullptr;
     }
   }
-  // concatenate with offset fix-ups (event indices, side-record indices, key / token / reset-key offsets)
+  // concatenate with offset fix-ups and canonical slot-table bases
   auto* out = new crr_decoded();
-  Chunk& a = out->all;
-  for (auto& k : chunks) {
-    const i64 ev0 = (i64)a.etype.size();
-    const i32 act0 = (i32)a.act.size(), st0 = (i32)a.start.size();
-    const u32 rk0 = (u32)a.reset_keys.size(), ar0 = (u32)a.arena.size(), ka0 = (u32)a.key_arena.size();
-    for (size_t i = 0; i < k.etype.size(); ++i) {
-      const int t = k.etype[i] & CRR_ETYPE_MASK;
-      if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) k.aux[i] += act0;
-      else if (t == CRR_EV_WORKFLOW_EXECUTION_STARTED) k.aux[i] += st0;
-      k.key_off[i] += ka0;
-    }
-    for (auto& s : k.start)
-      if (s.prev_reset_count >= 0) s.prev_reset_key_off += rk0;
-    for (auto& d : k.wf) {
-      d.ev_begin += ev0;
-      d.start_token_off += ar0;
-      if (d.final_token_len != 0xFFFFFFFFu) d.final_token_off += ar0;
-    }
-    append(a.etype, k.etype); append(a.id, k.id); append(a.ver, k.ver); append(a.ts, k.ts);
-    append(a.task, k.task); append(a.ref, k.ref); append(a.key, k.key); append(a.aux, k.aux);
-    append(a.key_off, k.key_off); append(a.key_len, k.key_len); a.key_arena += k.key_arena;
-    append(a.act, k.act); append(a.start, k.start); append(a.reset_keys, k.reset_keys);
-    append(a.arena, k.arena); append(a.wf, k.wf);
-    Chunk().etype.swap(k.etype);  // release chunk memory early
-  }
-  // canonical slot-table bases: prefix sums of the per-workflow capacities
-  int64_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (auto& d : a.wf) {
-    const i32 caps[8] = {d.act_cap, d.timer_cap, d.child_cap, d.rc_cap, d.sig_cap, d.vh_cap, d.rp_cap, d.task_cap};
-    int64_t* bases[8] = {&d.act_base, &d.timer_base, &d.child_base, &d.rc_base, &d.sig_base, &d.vh_base, &d.rp_base,
-                         &d.task_base};
-    for (int j = 0; j < 8; ++j) {
-      *bases[j] = base[j];
-      base[j] += std::max(caps[j], 0);
-    }
-  }
-  for (int j = 0; j < 8; ++j) out->table_rows[j] = (uint64_t)base[j];
+  concat_chunks(chunks, out->all, out->table_rows);
   return out;
 }
 

@@ -555,7 +555,7 @@ struct GlobalTables {
         crr_activity_row* r = G.act(B.j);
         r->timer_task_status |= timer_mask(B.y);
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r->last_hb_timeout_vis_s = unix_seconds(B.t);
-        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);  // timer_sequence.go:190-196
+        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, r->attempt, -1);  // timer_sequence.go:190-196
       }
     }
     dirty_act = false;
@@ -970,7 +970,7 @@ struct LdsTables {
       r.timer_task_status = (i32)tts;
       r.key = M->a_key[i][t];
       r.flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
-      r.reserved = 0;
+      r.attempt = 0;
       r.last_heartbeat_time = r.started_time;  // StartedTime (:2272-2273), Go's zero time until started
       *G.act(i) = r;
     }
@@ -1384,12 +1384,14 @@ struct WaveTables {
                             (u32)r.timer_task_status);
       }
       wave_min(B);
+      i32 attempt = 0;
       if (B.have && !B.created && own(B.j)) {
         crr_activity_row& r = S.act(B.j);
         r.timer_task_status |= timer_mask(B.y);
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r.last_hb_timeout_vis_s = unix_seconds(B.t);
+        attempt = r.attempt;
       }
-      if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
+      if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, (i32)bcast(B.j, (u32)attempt), -1);
     }
     dirty_act = false;
     if (L.n_timer > 0 && dirty_timer) {
@@ -1855,7 +1857,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
         row.key = ev.key;
         row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
-        row.reserved = 0;
+        row.attempt = 0;
         row.last_heartbeat_time = CRR_ZERO_TIME;
         CHECK(T.act_insert(L, G, row));
         K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks

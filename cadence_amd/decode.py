@@ -70,6 +70,8 @@ def lib():
         L.crr_decoded_get_view.restype = ctypes.c_int
         L.crr_decoded_free.argtypes = [vp]
         L.crr_decoded_free.restype = None
+        L.crr_synth_histories.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.crr_synth_histories.restype = vp
         _lib = L
     return _lib
 
@@ -146,6 +148,11 @@ def decode_histories(sources: Sequence[WorkflowSource], known_domains: Optional[
                                ctypes.byref(err), ctypes.byref(err_blob))
     if not h:
         raise DeserializationError(err.value, err_blob.value)
+    return batch_from_handle(L, h)
+
+
+def batch_from_handle(L, h) -> HistoryBatch:
+    """Copy a crr_decoded result into a canonical HistoryBatch and free it."""
     try:
         v = CDecodedView()
         L.crr_decoded_get_view(h, ctypes.byref(v))

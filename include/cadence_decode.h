@@ -81,6 +81,30 @@ crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* b
 int  crr_decoded_get_view(const crr_decoded* d, crr_decoded_view* view);
 void crr_decoded_free(crr_decoded* d);
 
+/* ---- synthetic histories (benchmark / test infrastructure, not part of the replay boundary) ---------
+ * Seeded random-walk histories flattened like decoded ones (cadence_amd/csrc/synth_native.cpp):
+ * CRR_SYNTH_MIXED: n workflows of 10..2*mean_len-10 events over every event type (configs 3 and 5);
+ * CRR_SYNTH_LONG_TAIL: n logical workflows with Zipf(alpha) lengths in [min_len, max_len], continued
+ * as new every run_cap events (each run a workflow, each CAN event's new-run history its next run's
+ * first batch; config 4).  The result is freed with crr_decoded_free. */
+#define CRR_SYNTH_MIXED     0
+#define CRR_SYNTH_LONG_TAIL 1
+typedef struct crr_synth_params {
+    uint32_t kind;                 /* CRR_SYNTH_* */
+    uint32_t n;
+    uint64_t seed;
+    int32_t  mean_len;             /* mixed */
+    int32_t  multi_version;        /* failover version bumps at batch boundaries (VersionHistories items) */
+    double   invalid_rate;         /* histories that end in an injected ApplyEvents error */
+    double   can_rate;             /* mixed: CAN-closed histories given a new-run history */
+    double   unknown_domain_rate;  /* attribute domain names the domain cache cannot resolve */
+    int32_t  min_len, max_len, run_cap;   /* long tail */
+    int32_t  caps[5];              /* concurrently pending activity / timer / child / rc / signal caps (<= 0: none) */
+    double   alpha;                /* long tail: Zipf exponent */
+} crr_synth_params;
+
+crr_decoded* crr_synth_histories(const crr_synth_params* params, int n_threads, int* err);
+
 #ifdef __cplusplus
 }
 #endif

@@ -347,7 +347,7 @@ typedef struct crr_activity_row {
     int32_t  timer_task_status;
     uint32_t key;                                /* interned ActivityID */
     uint32_t flags;                              /* CRR_ROW_* */
-    int32_t  reserved;
+    int32_t  attempt;                            /* ActivityInfo.Attempt (0 on the replay path) */
     int64_t  last_heartbeat_time;                /* LastHeartBeatUpdatedTime (== started_time on replay) */
 } crr_activity_row;
 

@@ -43,6 +43,29 @@ struct VH {
     *out = items.front();
     return CRR_OK;
   }
+  // ContainsItem (:228-245)
+  bool contains(const Item& it) const {
+    i64 prev = CRR_FIRST_EVENT_ID - 1;
+    for (const Item& c : items) {
+      if (it.version == c.version) {
+        if (prev < it.event_id && it.event_id <= c.event_id) return true;
+      } else if (it.version < c.version) {
+        return false;
+      }
+      prev = c.event_id;
+    }
+    return false;
+  }
+  // GetEventVersion (:313-335)
+  int event_version(i64 event_id, i64* out) const {
+    Item last;
+    int e = last_item(&last);
+    if (e) return e;
+    if (event_id < CRR_FIRST_EVENT_ID || event_id > last.event_id) return CRR_ERR_NDC_BAD_INDEX;
+    for (const Item& c : items)
+      if (event_id <= c.event_id) { *out = c.version; return CRR_OK; }
+    return CRR_ERR_NDC_BAD_INDEX;
+  }
   int duplicate_until_lca(const Item& lca, VH* out) const {  // :142-172
     VH v;
     for (const Item& it : items) {
@@ -153,6 +176,49 @@ int verify_events_order(const VH& local, i64 first_id, bool* do_continue, Item* 
 }
 
 }  // namespace
+
+// Single VersionHistory queries over caller items (restating versionHistory_test.go's unit cases):
+//   op 1 DuplicateUntilLCAItem(a, b) -> status, items in out; op 2 IsLCAAppendable(a, b) -> 0/1;
+//   op 3 GetFirstItem, op 4 GetLastItem -> status, item in out[0]; op 5 ContainsItem(a, b) -> 0/1;
+//   op 6 GetEventVersion(a) -> status, version in out[0].version; op 7 AddOrUpdateItem(a, b) -> status, items.
+// Returns the status (or the boolean), *n_out the items written to out.
+extern "C" int oracle_vh_query(int op, const crr_vh_item* items, int n, int64_t a, int64_t b, crr_vh_item* out,
+                               int* n_out) {
+  VH v;
+  for (int i = 0; i < n; ++i) v.items.push_back({items[i].event_id, items[i].version});
+  *n_out = 0;
+  Item it{a, b}, r{0, 0};
+  switch (op) {
+    case 1: {
+      VH d;
+      int e = v.duplicate_until_lca(it, &d);
+      if (e) return e;
+      for (const Item& x : d.items) out[(*n_out)++] = {x.event_id, x.version};
+      return CRR_OK;
+    }
+    case 2: return !v.items.empty() && v.items.back() == it;  // IsLCAAppendable (:278-290)
+    case 3: case 4: {
+      int e = op == 3 ? v.first_item(&r) : v.last_item(&r);
+      if (!e) { out[0] = {r.event_id, r.version}; *n_out = 1; }
+      return e;
+    }
+    case 5: return v.contains(it);
+    case 6: {
+      i64 ver = 0;
+      int e = v.event_version(a, &ver);
+      if (!e) { out[0] = {a, ver}; *n_out = 1; }
+      return e;
+    }
+    case 7: {
+      if (a < 0 || (b < 0 && b != CRR_EMPTY_VERSION)) return CRR_ERR_VH_INVALID_ITEM;  // NewVersionHistoryItem
+      int e = v.add_or_update(it);
+      if (e) return e;
+      for (const Item& x : v.items) out[(*n_out)++] = {x.event_id, x.version};
+      return CRR_OK;
+    }
+    default: return -1;
+  }
+}
 
 extern "C" int oracle_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* results, crr_vh_item* out_items) {
   for (uint32_t k = 0; k < in->n_tasks; ++k) {

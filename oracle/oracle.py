@@ -43,8 +43,12 @@ def lib():
         L.oracle_vh_add_or_update.restype = ctypes.c_int
         L.oracle_update_state.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int]
         L.oracle_update_state.restype = ctypes.c_int
-        L.oracle_activity_timer_sequence.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int]
+        L.oracle_activity_timer_sequence.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int]
         L.oracle_activity_timer_sequence.restype = ctypes.c_int
+        L.oracle_user_timer_sequence.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int]
+        L.oracle_user_timer_sequence.restype = ctypes.c_int
+        L.oracle_vh_query.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, vp, vp]
+        L.oracle_vh_query.restype = ctypes.c_int
         L.oracle_ndc_prepare.argtypes = [vp, vp, vp]
         L.oracle_ndc_prepare.restype = ctypes.c_int
         _lib = L
@@ -149,15 +153,28 @@ def update_state(state, close, new_state, new_close):
 
 
 def activity_timer_sequence(rows: np.ndarray):
-    """LoadAndSortActivityTimers; rows are abi.ACTIVITY_ROW with last_hb_timeout_vis_s holding
-    LastHeartBeatUpdatedTime.  Returns [(timestamp, event_id, type, created)]."""
+    """LoadAndSortActivityTimers over abi.ACTIVITY_ROW images (last_heartbeat_time = LastHeartBeatUpdatedTime).
+    Returns [(timestamp, event_id, timer type, created, attempt)]."""
     rows = np.ascontiguousarray(rows, dtype=abi.ACTIVITY_ROW)
     cap = 4 * max(len(rows), 1)
     ts = np.zeros(cap, np.int64)
     eid = np.zeros(cap, np.int64)
     ty = np.zeros(cap, np.int32)
     cr = np.zeros(cap, np.int32)
-    n = lib().oracle_activity_timer_sequence(_ptr(rows), len(rows), _ptr(ts), _ptr(eid), _ptr(ty), _ptr(cr), cap)
+    at = np.zeros(cap, np.int32)
+    n = lib().oracle_activity_timer_sequence(_ptr(rows), len(rows), _ptr(ts), _ptr(eid), _ptr(ty), _ptr(cr), _ptr(at), cap)
+    return [(int(ts[i]), int(eid[i]), int(ty[i]), bool(cr[i]), int(at[i])) for i in range(n)]
+
+
+def user_timer_sequence(rows: np.ndarray):
+    """LoadAndSortUserTimers over abi.TIMER_ROW images: [(timestamp, event_id, timer type, created)]."""
+    rows = np.ascontiguousarray(rows, dtype=abi.TIMER_ROW)
+    cap = max(len(rows), 1)
+    ts = np.zeros(cap, np.int64)
+    eid = np.zeros(cap, np.int64)
+    ty = np.zeros(cap, np.int32)
+    cr = np.zeros(cap, np.int32)
+    n = lib().oracle_user_timer_sequence(_ptr(rows), len(rows), _ptr(ts), _ptr(eid), _ptr(ty), _ptr(cr), cap)
     return [(int(ts[i]), int(eid[i]), int(ty[i]), bool(cr[i])) for i in range(n)]
 
 
@@ -174,3 +191,15 @@ def ndc_prepare(batch):
     out = np.zeros(batch.n_out_items, abi.VH_ITEM)
     lib().oracle_ndc_prepare(ctypes.byref(ci), _ptr(res), _ptr(out))
     return res[:n], out
+
+
+VH_DUPLICATE_UNTIL_LCA, VH_IS_LCA_APPENDABLE, VH_FIRST, VH_LAST, VH_CONTAINS, VH_EVENT_VERSION, VH_ADD_OR_UPDATE = range(1, 8)
+
+
+def vh_query(op, items, a=0, b=0):
+    """One VersionHistory operation (versionHistory.go) on ``items`` [(event_id, version)]: (result, items out)."""
+    arr = np.array([tuple(x) for x in items] or [(0, 0)], abi.VH_ITEM)
+    out = np.zeros(len(items) + 2, abi.VH_ITEM)
+    n = ctypes.c_int(0)
+    r = lib().oracle_vh_query(int(op), _ptr(arr), len(items), int(a), int(b), _ptr(out), ctypes.byref(n))
+    return r, [(int(x["event_id"]), int(x["version"])) for x in out[:n.value]]

@@ -463,6 +463,7 @@ struct TimerSequenceID {
   i64 timestamp;
   i32 timer_type;
   bool created;
+  i32 attempt;  // the activity's Attempt (0 for user timers)
 };
 // Less (timer_sequence.go:461-493): order by timestamp, event ID, timer type.  Sequence IDs in one
 // list are pairwise distinct, so any sort yields the same first element as Go's sort.Sort.
@@ -483,21 +484,21 @@ std::vector<TimerSequenceID> LoadAndSortActivityTimers(const MutableState& ms) {
     if (ai.schedule_id == CRR_EMPTY_EVENT_ID) continue;  // every getter returns nil
     // getActivityScheduleToCloseTimeout (:296-316)
     v.push_back({ai.schedule_id, add_seconds(ai.scheduled_time, ai.schedule_to_close), CRR_TIMEOUT_SCHEDULE_TO_CLOSE,
-                 (ai.timer_task_status & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) > 0});
+                 (ai.timer_task_status & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) > 0, ai.attempt});
     // getActivityScheduleToStartTimeout (:269-294)
     if (ai.started_id == CRR_EMPTY_EVENT_ID) {
       v.push_back({ai.schedule_id, add_seconds(ai.scheduled_time, ai.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START,
-                   (ai.timer_task_status & CRR_TTS_CREATED_SCHEDULE_TO_START) > 0});
+                   (ai.timer_task_status & CRR_TTS_CREATED_SCHEDULE_TO_START) > 0, ai.attempt});
     } else {
       // getActivityStartToCloseTimeout (:318-343)
       v.push_back({ai.schedule_id, add_seconds(ai.started_time, ai.start_to_close), CRR_TIMEOUT_START_TO_CLOSE,
-                   (ai.timer_task_status & CRR_TTS_CREATED_START_TO_CLOSE) > 0});
+                   (ai.timer_task_status & CRR_TTS_CREATED_START_TO_CLOSE) > 0, ai.attempt});
       // getActivityHeartbeatTimeout (:345-381)
       if (ai.heartbeat > 0) {
         i64 lastHeartbeat = ai.started_time;
         if (ai.last_heartbeat_updated_time > lastHeartbeat) lastHeartbeat = ai.last_heartbeat_updated_time;
         v.push_back({ai.schedule_id, add_seconds(lastHeartbeat, ai.heartbeat), CRR_TIMEOUT_HEARTBEAT,
-                     (ai.timer_task_status & CRR_TTS_CREATED_HEARTBEAT) > 0});
+                     (ai.timer_task_status & CRR_TTS_CREATED_HEARTBEAT) > 0, ai.attempt});
       }
     }
   }
@@ -510,7 +511,7 @@ std::vector<TimerSequenceID> LoadAndSortUserTimers(const MutableState& ms) {
   v.reserve(ms.pendingTimerInfoIDs.size());
   for (const auto& kv : ms.pendingTimerInfoIDs) {
     const TimerInfo& ti = kv.second;
-    v.push_back({ti.started_id, ti.expiry_time, CRR_TIMEOUT_START_TO_CLOSE, ti.task_status == CRR_TIMER_TASK_STATUS_CREATED});
+    v.push_back({ti.started_id, ti.expiry_time, CRR_TIMEOUT_START_TO_CLOSE, ti.task_status == CRR_TIMER_TASK_STATUS_CREATED, 0});
   }
   std::sort(v.begin(), v.end(), seq_less);
   return v;
@@ -535,7 +536,7 @@ Err CreateNextActivityTimer(MutableState& ms) {
   ai.timer_task_status |= timer_type_to_mask(first.timer_type);
   if (first.timer_type == CRR_TIMEOUT_HEARTBEAT) ai.last_hb_timeout_vis_s = unix_seconds(first.timestamp);
   // UpdateActivity (:1292-1307) cannot fail: the info is pending.  AddTimerTasks (:190-196):
-  ms.AddTask(CRR_TASK_ACTIVITY_TIMEOUT, first.timer_type, ms.currentVersion, first.timestamp, first.event_id, 0, -1);
+  ms.AddTask(CRR_TASK_ACTIVITY_TIMEOUT, first.timer_type, ms.currentVersion, first.timestamp, first.event_id, ai.attempt, -1);
   return Err{};
 }
 // CreateNextUserTimer (:127-160)
@@ -1060,6 +1061,7 @@ void export_rows(const crr_inputs* in, uint32_t w, const MutableState& ms, const
     o.start_to_close = a.start_to_close; o.heartbeat = a.heartbeat;
     o.timer_task_status = a.timer_task_status; o.key = a.key;
     o.last_heartbeat_time = a.last_heartbeat_updated_time;
+    o.attempt = a.attempt;
     auto m = ms.pendingActivityIDToEventID.find(a.activity_id);
     bool mapped = m != ms.pendingActivityIDToEventID.end() && m->second == a.schedule_id;
     o.flags = CRR_ROW_LIVE | (mapped ? CRR_ROW_MAPPED : 0u) | (a.cancel_requested ? CRR_ROW_CANCEL_REQUESTED : 0u) |
@@ -1171,6 +1173,7 @@ int load_state(const crr_inputs* in, uint32_t w, const crr_outputs* out, const K
     a.cancel_requested = (o.flags & CRR_ROW_CANCEL_REQUESTED) != 0;
     a.cancel_request_id = o.cancel_request_id;
     a.last_heartbeat_updated_time = o.last_heartbeat_time;
+    a.attempt = o.attempt;
     a.timer_task_status = o.timer_task_status;
     a.has_retry_policy = (o.flags & CRR_ROW_HAS_RETRY) != 0;
     a.last_hb_timeout_vis_s = o.last_hb_timeout_vis_s;
@@ -1336,20 +1339,41 @@ int oracle_update_state(int* state, int* close_status, int new_state, int new_cl
 }
 
 // LoadAndSortActivityTimers over caller rows (timer_sequence.go:219-254); returns count written.
+// attempt[] receives each sequence ID's Attempt (the ActivityInfo's, getActivity*Timeout).
 int oracle_activity_timer_sequence(const crr_activity_row* rows, int n, int64_t* ts, int64_t* eid, int32_t* type,
-                                   int32_t* created, int cap) {
+                                   int32_t* created, int32_t* attempt, int cap) {
   MutableState ms;
   for (int i = 0; i < n; ++i) {
     ActivityInfo a;
     a.schedule_id = rows[i].schedule_id; a.scheduled_time = rows[i].scheduled_time;
     a.started_id = rows[i].started_id; a.started_time = rows[i].started_time;
-    a.last_heartbeat_updated_time = rows[i].last_hb_timeout_vis_s;  // caller passes LastHeartBeatUpdatedTime here
+    a.last_heartbeat_updated_time = rows[i].last_heartbeat_time;
     a.schedule_to_start = rows[i].schedule_to_start; a.schedule_to_close = rows[i].schedule_to_close;
     a.start_to_close = rows[i].start_to_close; a.heartbeat = rows[i].heartbeat;
     a.timer_task_status = rows[i].timer_task_status;
+    a.attempt = rows[i].attempt;
     ms.pendingActivityInfoIDs[a.schedule_id * 64 + i] = a;  // distinct map keys even for EmptyEventID rows
   }
   std::vector<TimerSequenceID> v = LoadAndSortActivityTimers(ms);
+  int m = (int)std::min<size_t>(v.size(), (size_t)cap);
+  for (int i = 0; i < m; ++i) {
+    ts[i] = v[i].timestamp; eid[i] = v[i].event_id; type[i] = v[i].timer_type; created[i] = v[i].created;
+    attempt[i] = v[i].attempt;
+  }
+  return (int)v.size();
+}
+
+// LoadAndSortUserTimers over caller rows (timer_sequence.go:201-217, getUserTimerTimeout :256-267).
+int oracle_user_timer_sequence(const crr_timer_row* rows, int n, int64_t* ts, int64_t* eid, int32_t* type,
+                               int32_t* created, int cap) {
+  MutableState ms;
+  for (int i = 0; i < n; ++i) {
+    TimerInfo t;
+    t.version = rows[i].version; t.started_id = rows[i].started_id; t.expiry_time = rows[i].expiry_time;
+    t.task_status = rows[i].task_status; t.timer_id = std::to_string(i);
+    ms.pendingTimerInfoIDs[t.timer_id] = t;
+  }
+  std::vector<TimerSequenceID> v = LoadAndSortUserTimers(ms);
   int m = (int)std::min<size_t>(v.size(), (size_t)cap);
   for (int i = 0; i < m; ++i) { ts[i] = v[i].timestamp; eid[i] = v[i].event_id; type[i] = v[i].timer_type; created[i] = v[i].created; }
   return (int)v.size();

@@ -547,3 +547,153 @@ def check_all(kats: List[Kat], batch, res, idx, nr_idx):
             except AssertionError as ex:
                 failures.append(f"{k.name} ({k.cite}): {ex!r}")
     return failures
+
+
+# ---- service/history/execution/timer_sequence_test.go:74-231: CreateNextUserTimer / CreateNextActivityTimer
+# Each Go test hands the timer sequence a mock whose pending infos are given and whose GetCurrentVersion
+# is 999.  Restated: a loaded state holding those infos, one batch [MarkerRecorded] of version 999 (so
+# UpdateCurrentVersion makes currentVersion 999), whose per-batch epilogue (state_builder.go:634-640)
+# runs CreateNextActivityTimer / CreateNextUserTimer.
+TS = "service/history/execution/timer_sequence_test.go"
+CUR = 999
+
+
+def _marker_state(**kw):
+    return State(exec=running(next_event_id=1000, last_first_event_id=999, src_next=999, vh=[(999, 5)]), **kw)
+
+
+def _seq_act(tts, started=False, hb=1):
+    st = NOW + 200_000_000 if started else abi.ZERO_TIME
+    return dict(schedule_id=234, version=123, scheduled_batch_id=230, scheduled_time=NOW,
+                started_id=345 if started else abi.EMPTY_EVENT_ID, started_time=st, cancel_request_id=abi.EMPTY_EVENT_ID,
+                sched_src=3, started_src=4 if started else -1, schedule_to_start=10, schedule_to_close=1000,
+                start_to_close=100, heartbeat=hb, timer_task_status=tts, key=1, flags=abi.ROW_LIVE | abi.ROW_MAPPED,
+                attempt=12, last_heartbeat_time=abi.ZERO_TIME)
+
+
+def _seq_timer(status):
+    return dict(started_id=456, version=123, expiry_time=NOW + 100 * SEC, task_status=status, key=1, src=5)
+
+
+def _timer_kat(name, line, state, want_tasks, after):
+    def check(e, live, tasks, ctx):
+        assert int(e["status"]) == 0 and int(e["current_version"]) == CUR
+        got = [(int(t["kind"]), int(t["aux"]), int(t["version"]), int(t["visibility_ts"]), int(t["event_id"]),
+                int(t["attempt"])) for t in tasks]
+        assert got == want_tasks, got
+        after(live)
+    return Kat(name, f"{TS}:{line}", [[event(ET.MarkerRecorded, i=1000, v=CUR)]], state, check)
+
+
+def timer_cases() -> List[Kat]:
+    K = []
+    K.append(_timer_kat("CreateNextUserTimer_AlreadyCreated", 74, _marker_state(timers=[_seq_timer(1)], keys=["some random timer ID"]),
+                        [], lambda live: _eq(int(live["timer"][0]["task_status"]), 1)))
+    # UpdateUserTimer(TaskStatus = Created) + AddTimerTasks(UserTimerTask{ExpiryTime, StartedID, currentVersion})
+    K.append(_timer_kat("CreateNextUserTimer_NotCreated", 91, _marker_state(timers=[_seq_timer(0)], keys=["some random timer ID"]),
+                        [(TK.UserTimer, 0, CUR, NOW + 100 * SEC, 456, 0)],
+                        lambda live: _eq(int(live["timer"][0]["task_status"]), 1)))
+    both = abi.TTS_SCHEDULE_TO_CLOSE | abi.TTS_SCHEDULE_TO_START
+    K.append(_timer_kat("CreateNextActivityTimer_AlreadyCreated", 121,
+                        _marker_state(acts=[_seq_act(both)], keys=["some random activity ID"]), [],
+                        lambda live: _eq(int(live["act"][0]["timer_task_status"]), both)))
+    # UpdateActivity(TimerTaskStatus = CreatedScheduleToStart) + ActivityTimeoutTask{ScheduledTime + 10 s,
+    # ScheduleToStart, ScheduleID, Attempt 12, currentVersion}
+    K.append(_timer_kat("CreateNextActivityTimer_NotCreated", 146,
+                        _marker_state(acts=[_seq_act(0)], keys=["some random activity ID"]),
+                        [(TK.ActivityTimeout, abi.TimeoutType.ScheduleToStart, CUR, NOW + 10 * SEC, 234, 12)],
+                        lambda live: _eq(int(live["act"][0]["timer_task_status"]), abi.TTS_SCHEDULE_TO_START)))
+    hb_vis = NOW + 200_000_000 + 1 * SEC
+
+    def hb_after(live):
+        a = live["act"][0]
+        _eq(int(a["timer_task_status"]), abi.TTS_HEARTBEAT)
+        _eq(int(a["last_hb_timeout_vis_s"]), hb_vis // SEC)     # LastHeartbeatTimeoutVisibilityInSeconds = .Unix()
+    K.append(_timer_kat("CreateNextActivityTimer_HeartbeatTimer", 188,
+                        _marker_state(acts=[_seq_act(0, started=True)], keys=["some random activity ID"]),
+                        [(TK.ActivityTimeout, abi.TimeoutType.Heartbeat, CUR, hb_vis, 234, 12)], hb_after))
+    # LoadAndSortActivityTimers_Multiple (:567-644): the first of the sorted sequence is activity 2345's
+    # ScheduleToStart (now + 11 s, attempt 21); CreateNextActivityTimer creates exactly that one
+    a1 = dict(_seq_act(0, started=True, hb=0), last_heartbeat_time=NOW + 400_000_000)
+    a2 = dict(_seq_act(0, hb=6), schedule_id=2345, schedule_to_start=11, schedule_to_close=1001, start_to_close=101,
+              attempt=21, key=2, last_heartbeat_time=NOW + 800_000_000)
+    K.append(_timer_kat("LoadAndSortActivityTimers_Multiple_first", 567,
+                        _marker_state(acts=[a1, a2], keys=["some random activity ID", "other random activity ID"]),
+                        [(TK.ActivityTimeout, abi.TimeoutType.ScheduleToStart, CUR, NOW + 11 * SEC, 2345, 21)],
+                        lambda live: _eq([int(a["timer_task_status"]) for a in live["act"]], [0, abi.TTS_SCHEDULE_TO_START])))
+    # LoadAndSortUserTimers_Multiple (:263-302): 456 (created) sorts before 4567 -> nothing to create
+    t2 = dict(started_id=4567, version=1234, expiry_time=NOW + 200 * SEC, task_status=0, key=2, src=6)
+    K.append(_timer_kat("LoadAndSortUserTimers_Multiple_first", 263,
+                        _marker_state(timers=[_seq_timer(1), t2], keys=["some random timer ID", "other random timer ID"]),
+                        [], lambda live: _eq([int(t["task_status"]) for t in live["timer"]], [1, 0])))
+    return K
+
+
+# ---- service/history/execution/mutable_state_builder_test.go: transient decisions on the replay path ----
+# prepareTransientDecisionCompletionFirstBatchReplicated (:634-788) replicates Started(1), DecisionTask-
+# Scheduled(2), DecisionTaskStarted(3), DecisionTaskFailed, then a transient DecisionTaskScheduled(5,
+# attempt 123) + DecisionTaskStarted(6).  The tests then drive the ACTIVE path (AddDecisionTask*Event,
+# AddDecisionTaskScheduledEventAsHeartbeat) and assert on the history builder's transient / flushed
+# events -- code the replay path never runs.  Restated here is what the replay path does with the same
+# histories: the replicated failure after a failover (event version 13 > 12) schedules the transient
+# decision with the new currentVersion and NextEventID (ReplicateTransientDecisionTaskScheduled,
+# mutable_state_decision_task_manager.go:168-197: "the schedule ID for this decision is guaranteed to be
+# wrong ... ReplicateDecisionTaskScheduledEvent will overwrite everything"), and a replicated
+# DecisionTaskScheduled after it overwrites every decision field.
+MSB = "service/history/execution/mutable_state_builder_test.go"
+
+
+def _prepare(version=12):
+    ts = NOW
+    return [[event(ET.WorkflowExecutionStarted, i=1, v=version, ts=ts, execution_start_to_close_timeout_seconds=222,
+                   task_start_to_close_timeout_seconds=11),
+             event(ET.DecisionTaskScheduled, i=2, v=version, ts=ts, start_to_close_timeout_seconds=11, attempt=0)],
+            [event(ET.DecisionTaskStarted, i=3, v=version, ts=ts, scheduled_event_id=2)],
+            [event(ET.DecisionTaskFailed, i=4, v=version, ts=ts)],
+            [event(ET.DecisionTaskScheduled, i=5, v=version, ts=ts, start_to_close_timeout_seconds=11, attempt=123),
+             event(ET.DecisionTaskStarted, i=6, v=version, ts=ts, scheduled_event_id=5)]]
+
+
+def _failover_case(name, line, t, **attrs):
+    def check(e, live, tasks, ctx):
+        assert int(e["status"]) == 0
+        # the started transient decision had Attempt forced to 0 (:223); FailDecision(true) -> 1
+        assert int(e["decision_attempt"]) == 1
+        assert (int(e["decision_schedule_id"]), int(e["decision_version"])) == (7, 13)   # NextEventID, currentVersion
+        assert int(e["decision_scheduled_ts"]) == ctx["now_ns"] and int(e["decision_timeout"]) == 11
+        assert int(e["current_version"]) == 13 and int(e["next_event_id"]) == 8
+        assert [(int(x["event_id"]), int(x["version"])) for x in live["vh"]] == [(6, 12), (7, 13)]
+        assert tasks_of(tasks)[-1] == (TK.Decision, 7)
+    return Kat(name, f"{MSB}:{line}", _prepare() + [[event(t, i=7, v=13, **attrs)]], None, check)
+
+
+def msb_cases() -> List[Kat]:
+    K = []
+
+    def completed(e, live, tasks, ctx):   # :106-134 ReplicateDecisionCompleted after the transient completion
+        assert int(e["status"]) == 0 and int(e["decision_schedule_id"]) == abi.EMPTY_EVENT_ID
+        assert int(e["last_processed_event"]) == 6 and int(e["decision_attempt"]) == 0
+    K.append(Kat("TransientDecisionCompletionFirstBatchReplicated_ReplicateDecisionCompleted", f"{MSB}:106",
+                 _prepare() + [[event(ET.DecisionTaskCompleted, i=7, v=12, scheduled_event_id=5, started_event_id=6)]],
+                 None, completed))
+    K.append(_failover_case("TransientDecisionCompletionFirstBatchReplicated_FailoverDecisionTimeout", 136,
+                            ET.DecisionTaskTimedOut, timeout_type=0))
+    K.append(_failover_case("TransientDecisionCompletionFirstBatchReplicated_FailoverDecisionFailed", 154,
+                            ET.DecisionTaskFailed))
+
+    def sched_changed(e, live, tasks, ctx):   # :535-567: the transient decision after a failure at version 2001
+        assert int(e["status"]) == 0
+        assert int(e["decision_attempt"]) == 1 and int(e["decision_version"]) == 2001
+        assert int(e["decision_schedule_id"]) == 7 and int(e["current_version"]) == 2001
+    K.append(Kat("TransientDecisionTaskSchedule_CurrentVersionChanged", f"{MSB}:535",
+                 _prepare(2000) + [[event(ET.DecisionTaskFailed, i=7, v=2001)]], None, sched_changed))
+
+    def start_changed(e, live, tasks, ctx):   # :569-632: a replicated DecisionTaskScheduled overwrites the transient one
+        assert int(e["status"]) == 0
+        assert (int(e["decision_schedule_id"]), int(e["decision_attempt"]), int(e["decision_version"])) == (8, 2, 2001)
+        assert int(e["decision_started_id"]) == abi.EMPTY_EVENT_ID and int(e["decision_timeout"]) == 11
+    K.append(Kat("TransientDecisionTaskStart_CurrentVersionChanged", f"{MSB}:569",
+                 _prepare(2000) + [[event(ET.DecisionTaskFailed, i=7, v=2000)],
+                                   [event(ET.DecisionTaskScheduled, i=8, v=2001, start_to_close_timeout_seconds=11,
+                                          attempt=2)]], None, start_changed))
+    return K

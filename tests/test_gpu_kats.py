@@ -1,5 +1,5 @@
-"""GPU: the reference's dispatch-table spec (state_builder_test.go:143-1744, restated in
-tests/kat_state_builder.py) replayed by the HIP engine through the C ABI -- every case's expected
+"""GPU: the reference's dispatch-table spec (state_builder_test.go:143-1744) and timer-sequence
+creation tests (timer_sequence_test.go:74-231), restated in tests/kat_state_builder.py, replayed by the HIP engine through the C ABI -- every case's expected
 Replicate* effects and Generate* tasks, in the canonical and the wave-interleaved layouts, and
 bit-exact against the oracle."""
 import pytest
@@ -12,12 +12,13 @@ import kat_state_builder as K
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("suite", ["state_builder", "timer_sequence", "mutable_state_builder"])
 @pytest.mark.parametrize("layout", ["canonical", "interleaved"])
-def test_device_dispatch_table_kats(layout):
+def test_device_dispatch_table_kats(layout, suite):
     from cadence_amd.engine import ReplayEngine
     from oracle import oracle
     eng = ReplayEngine(0)
-    kats = K.cases()
+    kats = {"state_builder": K.cases, "timer_sequence": K.timer_cases, "mutable_state_builder": K.msb_cases}[suite]()
     batch, idx, nr = K.build_batch(kats)
     if layout == "interleaved":
         ib = interleave(batch)

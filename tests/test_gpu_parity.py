@@ -196,3 +196,28 @@ def test_measured_region_launches(engine):
     engine.launch(db)
     torch.cuda.synchronize()
     assert engine.last_kernel_ms()[2] > 0
+
+
+def test_config4_long_tail_at_stated_size(engine):
+    """BASELINE config 4 at its stated size: histories up to 50k events, continue-as-new every <= 10k
+    (native generator), bounded and unbounded pending sets; length-bucketed (wave tail + big-arena
+    segment + retry), lanes-only and untiered layouts, every row against the oracle."""
+    from cadence_amd import synth_native
+    for caps in (synth_native.LONG_TAIL_CAPS, None):
+        b = synth_native.long_tail(400, seed=0xCAD00004, max_len=50_000, run_cap=10_000, caps=caps,
+                                   multi_version=True, invalid_rate=0.05)
+        assert b.wf["ev_count"].max() > 9_000 and b.n_events > 2_000_000
+        check(engine, interleave(b))
+        check(engine, interleave(b, tiered=False))
+    check(engine, interleave(b, long_threshold=None))
+
+
+def test_config3_native_mixed_shard(engine):
+    """Config 3 shape from the native generator (every event type, failover versions, injected errors,
+    continue-as-new), 200k workflows, tier segments, against the oracle; plus the all-valid default."""
+    from cadence_amd import synth_native
+    b = synth_native.mixed(200_000, seed=0xCAD00003, multi_version=True, invalid_rate=0.1, can_rate=0.3,
+                           unknown_domain_rate=0.005)
+    check(engine, interleave(b))
+    got = check(engine, interleave(synth_native.mixed(100_000)))
+    assert (got.exec["status"] == 0).all()

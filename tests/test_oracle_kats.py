@@ -92,60 +92,9 @@ def test_state_transition_unknown_state():
     assert oracle.update_state(int(S.Created), 0, 9, 0)[0] == Status.UNKNOWN_WORKFLOW_STATE
 
 
-# ---- service/history/execution/timer_sequence_test.go ------------------------------------------------
+# ---- service/history/execution/timer_sequence_test.go: see tests/test_timer_sequence_kats.py -------------
 NOW = 1_700_000_000_123_456_789
 SEC = 1_000_000_000
-
-
-def _ai(schedule_id=234, scheduled=NOW, started_id=abi.EMPTY_EVENT_ID, started=abi.ZERO_TIME, s2s=10, s2c=1000,
-        st2c=100, hb=1, last_hb=abi.ZERO_TIME, tts=0):
-    r = np.zeros(1, abi.ACTIVITY_ROW)
-    r["schedule_id"], r["scheduled_time"], r["started_id"], r["started_time"] = schedule_id, scheduled, started_id, started
-    r["schedule_to_start"], r["schedule_to_close"], r["start_to_close"], r["heartbeat"] = s2s, s2c, st2c, hb
-    r["last_hb_timeout_vis_s"] = last_hb
-    r["timer_task_status"] = tts
-    return r
-
-
-def test_load_and_sort_activity_timers_not_scheduled():  # timer_sequence_test.go:312-332
-    assert oracle.activity_timer_sequence(_ai(schedule_id=abi.EMPTY_EVENT_ID)) == []
-
-
-def test_load_and_sort_activity_timers_scheduled_not_started():  # :334-375
-    seq = oracle.activity_timer_sequence(_ai(tts=abi.TTS_SCHEDULE_TO_CLOSE | abi.TTS_SCHEDULE_TO_START))
-    assert seq == [(NOW + 10 * SEC, 234, abi.TimeoutType.ScheduleToStart, True),
-                   (NOW + 1000 * SEC, 234, abi.TimeoutType.ScheduleToClose, True)]
-
-
-def test_load_and_sort_activity_timers_started_with_heartbeat():  # :377-427
-    started = NOW + 200_000_000
-    seq = oracle.activity_timer_sequence(_ai(started_id=345, started=started,
-                                             tts=abi.TTS_SCHEDULE_TO_CLOSE | abi.TTS_START_TO_CLOSE | abi.TTS_HEARTBEAT))
-    assert seq == [(started + 1 * SEC, 234, abi.TimeoutType.Heartbeat, True),
-                   (started + 100 * SEC, 234, abi.TimeoutType.StartToClose, True),
-                   (NOW + 1000 * SEC, 234, abi.TimeoutType.ScheduleToClose, True)]
-
-
-def test_load_and_sort_activity_timers_started_without_heartbeat():  # :429-470
-    started = NOW + 200_000_000
-    seq = oracle.activity_timer_sequence(_ai(started_id=345, started=started, hb=0, tts=abi.TTS_START_TO_CLOSE))
-    assert seq == [(started + 100 * SEC, 234, abi.TimeoutType.StartToClose, True),
-                   (NOW + 1000 * SEC, 234, abi.TimeoutType.ScheduleToClose, False)]
-
-
-def test_load_and_sort_activity_timers_heartbeated():  # :472-522 (LastHeartBeatUpdatedTime after start)
-    started = NOW + 200_000_000
-    hbt = NOW + 400_000_000
-    seq = oracle.activity_timer_sequence(_ai(started_id=345, started=started, last_hb=hbt))
-    assert seq[0] == (hbt + 1 * SEC, 234, abi.TimeoutType.Heartbeat, False)
-
-
-def test_timer_sequence_less():  # :1070-1137 TestLess_CompareTime / CompareEventID / CompareType
-    a = _ai(schedule_id=10, s2s=5, s2c=5)         # ScheduleToStart and ScheduleToClose at the same time
-    b = _ai(schedule_id=9, s2s=5, s2c=6)
-    seq = oracle.activity_timer_sequence(np.concatenate([a, b]))
-    # same timestamp: smaller event ID first; same time and ID: smaller timer type first
-    assert [(s[1], int(s[2])) for s in seq[:3]] == [(9, 1), (10, 1), (10, 2)]
 
 
 # ---- end-to-end restatements --------------------------------------------------------------------------
@@ -350,3 +299,12 @@ def test_state_builder_dispatch_table_kats():
 
 def test_event_type_count():  # state_builder_test.go:1744-1749 TestApplyEventsNewEventsNotHandled
     assert len(ET) == 42 == abi.EV_TYPE_COUNT
+
+
+def test_mutable_state_builder_transient_decision_kats():   # mutable_state_builder_test.go:106-177, :535-632
+    import kat_state_builder as K
+    kats = K.msb_cases()
+    batch, idx, nr = K.build_batch(kats)
+    res = oracle.replay(batch, 1)
+    fails = K.check_all(kats, batch, res, idx, nr)
+    assert not fails, "\n".join(fails)

@@ -19,6 +19,8 @@ def main():
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--mixed", action="store_true", help="config-3-like mixed histories instead of chains")
+    p.add_argument("--native", action="store_true", help="mixed histories from the native generator (full size)")
+    p.add_argument("--tiered", type=int, default=1, help="0: no tier segments (CRR_IN_TIERED off)")
     p.add_argument("--calib", action="store_true", help="first stream known byte counts (tools/calib.py)")
     a = p.parse_args()
     if a.calib:   # in-process (never spawn or exec from a process the profiler has put on the GPU)
@@ -33,10 +35,15 @@ def main():
     from cadence_amd.engine import ReplayEngine
     from cadence_amd.flatten import interleave
     eng = ReplayEngine(0)
-    if a.mixed:
+    t0 = time.time()
+    if a.native:
+        from cadence_amd import synth_native
+        b = interleave(synth_native.mixed(a.wf), tiered=bool(a.tiered))
+    elif a.mixed:
         from cadence_amd import synth_mixed
         from cadence_amd.flatten import flatten
-        b = interleave(flatten(synth_mixed.mixed_histories(a.wf, 5), known_domains={"domain-a", "domain-b", "parent-domain"}))
+        b = interleave(flatten(synth_mixed.mixed_histories(a.wf, 5), known_domains={"domain-a", "domain-b", "parent-domain"}),
+                       tiered=bool(a.tiered))
     else:
         b = interleave(synth.activity_chain(a.wf, a.k, synth.SEED_C2, with_keys=False))
     db = eng.upload(b)
@@ -50,7 +57,7 @@ def main():
     res = eng.download(db)
     alg = synth.algorithmic_bytes(b, res)
     med = float(np.median(ms))
-    print(json.dumps({"lib": a.lib or "default", "workflows": b.n_wf, "events": b.n_events, "kernel_ms": ms,
+    print(json.dumps({"lib": a.lib or "default", "setup_s": time.time() - t0, "tiers": b.tiers, "workflows": b.n_wf, "events": b.n_events, "kernel_ms": ms,
                       "median_ms": med, "events_per_s": b.n_events / (med * 1e-3),
                       "alg_GBs": alg / (med * 1e-3) / 1e9, "alg_bytes": alg,
                       "ok": int((res.exec["status"] == 0).sum()),

@@ -23,6 +23,7 @@ def main():
     p.add_argument("--thresholds", default="none,256,64")
     p.add_argument("--unbounded", action="store_true", help="unbounded pending sets (random walk)")
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
+    p.add_argument("--native", action="store_true", help="native generator (synth_native.long_tail)")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -35,8 +36,13 @@ def main():
 
     t0 = time.time()
     kw = {"caps": None} if a.unbounded else {}
-    hs = synth_mixed.long_tail_histories(a.n, a.seed, max_len=a.max_len, run_cap=a.run_cap, **kw)
-    b = flatten(hs, known_domains={"domain-a", "domain-b", "parent-domain"})
+    if a.native:
+        from cadence_amd import synth_native
+        b = synth_native.long_tail(a.n, a.seed, max_len=a.max_len, run_cap=a.run_cap,
+                                   caps=None if a.unbounded else synth_native.LONG_TAIL_CAPS)
+    else:
+        hs = synth_mixed.long_tail_histories(a.n, a.seed, max_len=a.max_len, run_cap=a.run_cap, **kw)
+        b = flatten(hs, known_domains={"domain-a", "domain-b", "parent-domain"})
     gen_s = time.time() - t0
     cnt = b.wf["ev_count"]
     eng = ReplayEngine(0)

@@ -289,7 +289,8 @@ class CInputs(ctypes.Structure):
     _fields_ = [("ev", CEvents), ("act_side", ctypes.c_void_p), ("start_side", ctypes.c_void_p),
                 ("reset_keys", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("wf", ctypes.c_void_p),
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
-                ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
+                ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("compact_begin", ctypes.c_uint32),
+                ("compact2_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
                 ("big_begin", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
@@ -308,4 +309,4 @@ def check_layout(lib):
         got = lib.crr_sizeof(i)
         if got != dt.itemsize:
             raise RuntimeError(f"ABI layout mismatch for struct #{i}: C {got} vs numpy {dt.itemsize}")
-    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 32
+    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 40

@@ -12,6 +12,10 @@ __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, uin
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+template <bool EMIT>
+__global__ void replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+template <bool EMIT>
+__global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
@@ -62,7 +66,7 @@ bool ensure_events() {
 
 // Tier segments of one phase run concurrently: side streams fork from and join back into the
 // caller's stream with events (created once per thread and device).
-constexpr int kSide = 3;
+constexpr int kSide = 5;
 struct SideStreams {
   hipStream_t st[kSide] = {};
   hipEvent_t fork = nullptr, join[kSide] = {};
@@ -103,8 +107,8 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
     // (64-workflow) boundary, or its wavefronts would straddle two groups
     const uint32_t n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
     if (in->stride != 64) return false;
-    if (in->large_begin < n_lane && (in->large_begin & 63u)) return false;
-    if (in->wide_begin < n_lane && (in->wide_begin & 63u)) return false;
+    for (uint32_t b : {in->large_begin, in->compact_begin, in->compact2_begin, in->wide_begin})
+      if (b < n_lane && (b & 63u)) return false;
   }
   return true;
 }
@@ -189,17 +193,20 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         }
       };
       if (in->flags & CRR_IN_TIERED) {
-        // segments by expected live-set size: 1 entry per map | 2 | more (the wide tier, 64 per block);
-        // CRR_IN_LDS_SMALL picks the kernel whose per-wave arenas also take the long-history tail
-        const uint32_t lb = in->large_begin < n_lane ? in->large_begin : n_lane;
-        const uint32_t wb = in->wide_begin < lb ? lb : (in->wide_begin < n_lane ? in->wide_begin : n_lane);
-        const bool run_small = lb > 0 || (tail && small), run_large = wb > lb || (tail && !small), run_wide = wb < n_lane;
+        // segments by expected live-set size: 1 entry per map | 2 | compact tier 1 | compact tier 2 |
+        // more (HBM rows); CRR_IN_LDS_SMALL picks the kernel whose per-wave arenas take the long-history tail
+        auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
+        const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
+        const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
+        const bool run_small = lb > 0 || (tail && small), run_large = cb > lb || (tail && !small);
+        const bool run_c1 = c2 > cb, run_c2 = wb > c2, run_wide = wb < n_lane;
         const bool run_big = tail_end < in->n_wf;
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
-        const bool fork =
-            (int)run_small + (int)run_large + (int)run_wide + (int)run_big > 1 && ensure_side_streams();
+        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_wide + (int)run_big > 1 &&
+                          ensure_side_streams();
         hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
+        hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s;
         if (fork) {
           (void)hipEventRecord(g_side.fork, s);
           for (hipStream_t x : g_side.st) (void)hipStreamWaitEvent(x, g_side.fork, 0);
@@ -210,7 +217,15 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, wb, n_lane);
-        launch_fast(s_large, false, tail && !small, lb, wb);
+        if (run_c2) {
+          if (emit) hipLaunchKernelGGL((crr::replay_compact2_kernel<true>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
+          else hipLaunchKernelGGL((crr::replay_compact2_kernel<false>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
+        }
+        if (run_c1) {
+          if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
+          else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
+        }
+        launch_fast(s_large, false, tail && !small, lb, cb);
         launch_fast(s, true, tail && small, 0, lb);
         if (fork) {
           for (int i = 0; i < kSide; ++i) {

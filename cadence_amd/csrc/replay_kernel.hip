@@ -358,6 +358,7 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
 // ===================================================================================================
 struct GlobalTables {
   static constexpr bool kResumable = true;  // rows live in HBM: a loaded state is continued in place
+  __device__ __forceinline__ static bool fits(i64) { return true; }
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
   // a map changed since its last batch epilogue (an unchanged one would reselect the same created
   // timer: a no-op, skipped -- each skipped pass is a scan of HBM rows)
@@ -673,6 +674,7 @@ template <class TIER>
 struct LdsTables {
   CRR_TIER_SLOTS
   static constexpr bool kResumable = false;  // rows are rebuilt from this call's events: no loaded state
+  __device__ __forceinline__ static bool fits(i64) { return true; }
   __device__ __forceinline__ void load(Lane&, const Geo&) {}
   using Arena = LdsArena<TIER>;
   Arena* M;
@@ -1051,6 +1053,461 @@ struct LdsTables {
 };
 
 // ===================================================================================================
+// CompactTables: lane per workflow with larger LDS tiers for workflows whose live sets outgrow the
+// 2-slot LdsTables tier (mixed histories: several pending activities, timers, children ...).  Same
+// [slot][lane] SoA layout as LdsTables at ~40 % of its bytes per slot, so 4-8 slots per map fit at
+// 1-2 waves/SIMD instead of the HBM-row GlobalTables scans:
+//   * event IDs as u32 and event steps as 10-bit fields (a workflow with an ID >= 2^32 or more than
+//     1023 events is handed to the general path: speed only, never results);
+//   * per activity only what its timer candidates need: the earliest of its candidates (the head of
+//     its part of LoadAndSortActivityTimers' order, timer_sequence.go:219-381) is kept up to date
+//     when the activity is scheduled or started -- the only events that change its candidate set --
+//     so the per-batch epilogue compares one cached candidate per activity;
+//   * everything else of a row (times, timeouts, versions, batch IDs) is re-read from the source
+//     events and side records when the live rows are written at the end.
+// ===================================================================================================
+template <int A, int T, int C, int R, int S, int P, int LANES_ = kBlock>
+struct CTier {
+  static constexpr int A_SLOTS = A, T_SLOTS = T, C_SLOTS = C, R_SLOTS = R, S_SLOTS = S, P_SLOTS = P;
+  static constexpr int LANES = LANES_;
+};
+// activity flag word: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + LF_STARTED / LF_HB_VIS,
+// TimerTaskStatus << 8, the cached candidate's timer type << 12
+constexpr int CF_CAND_SHIFT = 12;
+// step fields: 10 bits each
+constexpr u32 kStepBits = 10, kStepMask = (1u << kStepBits) - 1u;
+constexpr i32 kMaxCompactSteps = (1 << kStepBits) - 1;  // step kStepMask encodes "none"
+
+template <class TIER>
+struct CompactArena {
+  CRR_TIER_SLOTS
+  u32 a_sid[A_SLOTS][LANES];
+  u32 a_key[A_SLOTS][LANES];
+  u32 a_fl[A_SLOTS][LANES];
+  u32 a_src[A_SLOTS][LANES];     // sched | started << 10 | cancel-requested << 20 (kStepMask: none)
+  i64 a_cand[A_SLOTS][LANES];    // timestamp of the activity's earliest timer candidate
+  i64 a_s2c[A_SLOTS][LANES];     // ScheduledTime + ScheduleToCloseTimeout
+  int2 a_to[A_SLOTS][LANES];     // StartToCloseTimeout, HeartbeatTimeout
+  u32 t_sid[T_SLOTS][LANES];
+  u32 t_key[T_SLOTS][LANES];
+  u32 t_fl[T_SLOTS][LANES];      // LIVE | TF_CREATED | src << 8
+  i64 t_exp[T_SLOTS][LANES];
+  u32 c_id[C_SLOTS][LANES];
+  u32 c_fl[C_SLOTS][LANES];      // LIVE | initiated src << 8 | started src << 18 (kStepMask: none)
+  u32 r_id[R_SLOTS][LANES];
+  u32 r_fl[R_SLOTS][LANES];      // LIVE | src << 8
+  u32 s_id[S_SLOTS][LANES];
+  u32 s_fl[S_SLOTS][LANES];
+  u32 p_key[P_SLOTS][LANES];
+  u32 p_fl[P_SLOTS][LANES];      // row flags (LIVE | RESETTABLE) | src << 8 | (prev_index + 1) << 18
+};
+
+template <class TIER>
+struct CompactTables {
+  CRR_TIER_SLOTS
+  static constexpr bool kResumable = false;  // rows are rebuilt from this call's events
+  using Arena = CompactArena<TIER>;
+  Arena* M;
+  int t;  // threadIdx.x
+  const crr_inputs* in;
+  i64 ev_begin;
+  bool retried = false;
+  __device__ __forceinline__ void load(Lane&, const Geo&) {}
+
+  __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin) {
+    M = arena;
+    t = threadIdx.x;
+    in = inputs;
+    ev_begin = begin;
+#pragma unroll
+    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < C_SLOTS; ++j) M->c_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < R_SLOTS; ++j) M->r_fl[j][t] = 0;
+#pragma unroll
+    for (int j = 0; j < S_SLOTS; ++j) M->s_fl[j][t] = 0;
+  }
+  // fits the compact encodings (u32 IDs, 10-bit steps); else the general path replays it
+  __device__ __forceinline__ static bool fits(i64 n_ev) { return n_ev <= kMaxCompactSteps; }
+  __device__ __forceinline__ static bool id_fits(i64 id) { return id >= 0 && id <= (i64)0xFFFFFFFFu; }
+  __device__ __forceinline__ i64 ix(i32 step) const { return ev_begin + (i64)step * 64; }
+  __device__ __forceinline__ i64 ev_id(i32 step) const { return in->ev.event_id[ix(step)]; }
+  __device__ __forceinline__ i64 ev_ver(i32 step) const { return in->ev.version[ix(step)]; }
+  __device__ __forceinline__ i64 ev_ts(i32 step) const { return in->ev.timestamp[ix(step)]; }
+  __device__ __forceinline__ i64 batch_first_id(i32 step) const {
+    while (step > 0 && !(in->ev.etype[ix(step)] & CRR_ETYPE_BATCH_FIRST)) --step;
+    return ev_id(step);
+  }
+  __device__ __forceinline__ static u32 step_field(u32 w, int k) { return (w >> (kStepBits * k)) & kStepMask; }
+
+  __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
+    if (!id_fits(sched)) return -1;
+    const u32 s32 = (u32)sched;
+    i32 hit = -1;
+#pragma unroll
+    for (int j = A_SLOTS - 1; j >= 0; --j)
+      if ((M->a_fl[j][t] & CRR_ROW_LIVE) && M->a_sid[j][t] == s32) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = A_SLOTS - 1; j >= 0; --j) {
+      const u32 f = M->a_fl[j][t];
+      if ((f & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && M->a_key[j][t] == key) hit = j;
+    }
+    return hit;
+  }
+  // the earliest of an activity's timer candidates (getActivity*Timeout, timer_sequence.go:269-381);
+  // candidates of one activity share its ScheduleID, so they order by (time, timer type)
+  __device__ __forceinline__ static void cand_min(i64& ct, i32& cy, i64 t2, i32 y2) {
+    if (t2 < ct || (t2 == ct && y2 < cy)) { ct = t2; cy = y2; }
+  }
+  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
+    if (!id_fits(row.schedule_id)) return CRR_INTERNAL_RETRY;
+    i32 m = find_act_mapped(row.key);
+    i32 j = -1;
+#pragma unroll
+    for (int k = A_SLOTS - 1; k >= 0; --k)
+      if (!(M->a_fl[k][t] & CRR_ROW_LIVE)) j = k;
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= G.act_cap) return CRR_ERR_CAPACITY;
+    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+    // not started: ScheduleToClose and ScheduleToStart
+    i64 ct = add_seconds(row.scheduled_time, row.schedule_to_close);
+    i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+    cand_min(ct, cy, add_seconds(row.scheduled_time, row.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+    M->a_sid[j][t] = (u32)row.schedule_id;
+    M->a_key[j][t] = row.key;
+    M->a_fl[j][t] = row.flags | ((u32)cy << CF_CAND_SHIFT);
+    M->a_src[j][t] = (u32)row.sched_src | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
+    M->a_cand[j][t] = ct;
+    M->a_s2c[j][t] = add_seconds(row.scheduled_time, row.schedule_to_close);
+    M->a_to[j][t] = make_int2(row.start_to_close, row.heartbeat);
+    ++L.n_act;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) return id_fits(sched) ? CRR_ERR_MISSING_ACTIVITY_INFO : CRR_INTERNAL_RETRY;
+    const u32 f = M->a_fl[j][t];
+    if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
+    // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime
+    const int2 to = M->a_to[j][t];
+    i64 ct = M->a_s2c[j][t];
+    i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+    cand_min(ct, cy, add_seconds(ts, to.x), CRR_TIMEOUT_START_TO_CLOSE);
+    if (to.y > 0) cand_min(ct, cy, add_seconds(ts, to.y), CRR_TIMEOUT_HEARTBEAT);
+    M->a_cand[j][t] = ct;
+    M->a_fl[j][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
+    const u32 w = M->a_src[j][t];
+    M->a_src[j][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) { ++L.inconsistencies; return; }
+    const u32 f = M->a_fl[j][t];
+    const u32 key = M->a_key[j][t];
+    M->a_fl[j][t] = 0;
+    --L.n_act;
+    if (f & CRR_ROW_MAPPED) return;
+    const i32 m = find_act_mapped(key);
+    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+    else ++L.inconsistencies;
+  }
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 /*id*/, i64 /*ver*/, i32 s) {
+    const i32 j = find_act_mapped(key);
+    if (j < 0) return;
+    M->a_fl[j][t] |= CRR_ROW_CANCEL_REQUESTED;
+    const u32 w = M->a_src[j][t];
+    M->a_src[j][t] = (w & ~(kStepMask << (2 * kStepBits))) | ((u32)s << (2 * kStepBits));
+  }
+
+  __device__ __forceinline__ i32 find_timer(u32 key) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = T_SLOTS - 1; j >= 0; --j)
+      if ((M->t_fl[j][t] & CRR_ROW_LIVE) && M->t_key[j][t] == key) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
+    if (!id_fits(row.started_id)) return CRR_INTERNAL_RETRY;
+    i32 j = find_timer(row.key);
+    if (j < 0) {
+#pragma unroll
+      for (int k = T_SLOTS - 1; k >= 0; --k)
+        if (!(M->t_fl[k][t] & CRR_ROW_LIVE)) j = k;
+      if (j < 0) return CRR_INTERNAL_RETRY;
+      if (j >= G.timer_cap) return CRR_ERR_CAPACITY;
+      ++L.n_timer;
+    }
+    M->t_sid[j][t] = (u32)row.started_id;
+    M->t_exp[j][t] = row.expiry_time;
+    M->t_key[j][t] = row.key;
+    M->t_fl[j][t] = CRR_ROW_LIVE | ((u32)row.src << 8);
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
+    const i32 j = find_timer(key);
+    if (j < 0) { ++L.inconsistencies; return; }
+    M->t_fl[j][t] = 0;
+    --L.n_timer;
+  }
+
+  template <int N>
+  __device__ __forceinline__ i32 find_init(const u32 (*ids)[LANES], const u32 (*fl)[LANES], i64 id) const {
+    if (!id_fits(id)) return -1;
+    const u32 i32id = (u32)id;
+    i32 hit = -1;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j)
+      if ((fl[j][t] & CRR_ROW_LIVE) && ids[j][t] == i32id) hit = j;
+    return hit;
+  }
+  template <int N>
+  __device__ __forceinline__ i32 free_init(const u32 (*fl)[LANES]) const {
+    i32 hit = -1;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j)
+      if (!(fl[j][t] & CRR_ROW_LIVE)) hit = j;
+    return hit;
+  }
+  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
+    if (!id_fits(row.initiated_id)) return CRR_INTERNAL_RETRY;
+    const i32 j = free_init<C_SLOTS>(M->c_fl);
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= G.child_cap) return CRR_ERR_CAPACITY;
+    M->c_id[j][t] = (u32)row.initiated_id;
+    M->c_fl[j][t] = CRR_ROW_LIVE | ((u32)row.src << 8) | (kStepMask << (8 + kStepBits));
+    ++L.n_child;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+    const i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
+    if (j < 0) return id_fits(init) ? CRR_ERR_MISSING_CHILD_INFO : CRR_INTERNAL_RETRY;
+    const u32 f = M->c_fl[j][t];
+    M->c_fl[j][t] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
+    const i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    M->c_fl[j][t] = 0;
+    --L.n_child;
+  }
+  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
+    if (!id_fits(row.initiated_id)) return CRR_INTERNAL_RETRY;
+    const i32 j = is_rc ? free_init<R_SLOTS>(M->r_fl) : free_init<S_SLOTS>(M->s_fl);
+    if (j < 0) return CRR_INTERNAL_RETRY;
+    if (j >= (is_rc ? G.rc_cap : G.sig_cap)) return CRR_ERR_CAPACITY;
+    const u32 f = CRR_ROW_LIVE | ((u32)row.src << 8);
+    if (is_rc) { M->r_id[j][t] = (u32)row.initiated_id; M->r_fl[j][t] = f; ++L.n_rc; }
+    else { M->s_id[j][t] = (u32)row.initiated_id; M->s_fl[j][t] = f; ++L.n_sig; }
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
+    const i32 j = is_rc ? find_init<R_SLOTS>(M->r_id, M->r_fl, init) : find_init<S_SLOTS>(M->s_id, M->s_fl, init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    if (is_rc) { M->r_fl[j][t] = 0; --L.n_rc; }
+    else { M->s_fl[j][t] = 0; --L.n_sig; }
+  }
+  __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+    if (L.n_rp >= P_SLOTS || row.prev_index >= (i32)kStepMask - 1) return CRR_INTERNAL_RETRY;
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    M->p_key[L.n_rp][t] = row.key;
+    M->p_fl[L.n_rp][t] = (row.flags & 0xFFu) | ((u32)row.src << 8) | ((u32)(row.prev_index + 1) << (8 + kStepBits));
+    ++L.n_rp;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < P_SLOTS; ++i)
+      if (i < L.n_rp && M->p_key[i][t] == key) hit = true;
+    return hit;
+  }
+  // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199) over the cached heads
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
+    if (L.n_act > 0) {
+      BestTimer B;
+#pragma unroll
+      for (int j = 0; j < A_SLOTS; ++j) {
+        const u32 f = M->a_fl[j][t];
+        if (!(f & CRR_ROW_LIVE)) continue;
+        const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
+        B.offer(M->a_cand[j][t], (i64)M->a_sid[j][t], y, j, ((f >> LF_TTS_SHIFT) & timer_mask(y)) != 0);
+      }
+      if (B.have && !B.created) {
+        M->a_fl[B.j][t] |= (timer_mask(B.y) << LF_TTS_SHIFT) | (B.y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
+        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
+      }
+    }
+    if (L.n_timer > 0) {
+      BestTimer B;
+#pragma unroll
+      for (int j = 0; j < T_SLOTS; ++j) {
+        const u32 f = M->t_fl[j][t];
+        if (!(f & CRR_ROW_LIVE)) continue;
+        B.offer(M->t_exp[j][t], (i64)M->t_sid[j][t], 0, j, (f & TF_CREATED) != 0);
+      }
+      if (B.have && !B.created) {
+        M->t_fl[B.j][t] |= TF_CREATED;
+        K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
+      }
+    }
+  }
+  __device__ __forceinline__ bool task_writer() const { return true; }
+  // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
+  __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
+#pragma unroll
+    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] &= ~(0xFu << LF_TTS_SHIFT);
+#pragma unroll
+    for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] &= ~TF_CREATED;
+    epilogue(L, G, TaskSink{false, false});
+  }
+
+  template <class V>
+  __device__ __forceinline__ static void swp(V& a, V& b) { V x = a; a = b; b = x; }
+  // selection sort of the live slots by event ID (slots 0..n-1 afterwards)
+  template <int N, class SwapFn>
+  __device__ __forceinline__ void sort_slots(u32 (*ids)[LANES], u32 (*fl)[LANES], i32 n, SwapFn swap_fn) {
+    for (i32 i = 0; i < n; ++i) {
+      i32 best = -1;
+      u32 bid = 0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        if (j < i || !(fl[j][t] & CRR_ROW_LIVE)) continue;
+        const u32 id = ids[j][t];
+        if (best < 0 || id < bid) { best = j; bid = id; }
+      }
+      if (best != i) {
+        swap_fn(i, best);
+        swp(ids[i][t], ids[best][t]);
+        swp(fl[i][t], fl[best][t]);
+      }
+    }
+  }
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+    sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
+      swp(M->a_key[i][t], M->a_key[b][t]); swp(M->a_src[i][t], M->a_src[b][t]);
+      swp(M->a_cand[i][t], M->a_cand[b][t]); swp(M->a_s2c[i][t], M->a_s2c[b][t]); swp(M->a_to[i][t], M->a_to[b][t]);
+    });
+    sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
+      swp(M->t_exp[i][t], M->t_exp[b][t]); swp(M->t_key[i][t], M->t_key[b][t]);
+    });
+    sort_slots<C_SLOTS>(M->c_id, M->c_fl, L.n_child, [&](int, int) {});
+    sort_slots<R_SLOTS>(M->r_id, M->r_fl, L.n_rc, [&](int, int) {});
+    sort_slots<S_SLOTS>(M->s_id, M->s_fl, L.n_sig, [&](int, int) {});
+
+    for (i32 i = 0; i < L.n_act; ++i) {  // ReplicateActivityTask{Scheduled,Started,CancelRequested} images
+      const u32 f = M->a_fl[i][t];
+      const u32 w = M->a_src[i][t];
+      const i32 ss = (i32)step_field(w, 0), st = (i32)step_field(w, 1), sc = (i32)step_field(w, 2);
+      const bool started = (f & LF_STARTED) != 0, cancel = (f & CRR_ROW_CANCEL_REQUESTED) != 0;
+      // the ActivityTaskScheduled event's own fields: timestamp, side record (timeouts)
+      const crr_activity_side as = in->act_side[in->ev.aux[ix(ss)]];
+      crr_activity_row r;
+      r.schedule_id = (i64)M->a_sid[i][t];
+      r.version = ev_ver(max(ss, max(started ? st : -1, cancel ? sc : -1)));  // last of Scheduled / Started / CancelRequested
+      r.scheduled_batch_id = batch_first_id(ss);
+      r.scheduled_time = ev_ts(ss);
+      r.started_id = started ? ev_id(st) : CRR_EMPTY_EVENT_ID;
+      r.started_time = started ? ev_ts(st) : CRR_ZERO_TIME;
+      r.cancel_request_id = cancel ? ev_id(sc) : CRR_EMPTY_EVENT_ID;
+      r.last_hb_timeout_vis_s = (f & LF_HB_VIS) ? unix_seconds(add_seconds(r.started_time, as.heartbeat)) : 0;
+      r.sched_src = ss;
+      r.started_src = started ? st : -1;
+      r.schedule_to_start = as.schedule_to_start; r.schedule_to_close = as.schedule_to_close;
+      r.start_to_close = as.start_to_close; r.heartbeat = as.heartbeat;
+      r.timer_task_status = (i32)((f >> LF_TTS_SHIFT) & 0xF);
+      r.key = M->a_key[i][t];
+      r.flags = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
+      r.attempt = 0;
+      r.last_heartbeat_time = r.started_time;
+      *G.act(i) = r;
+    }
+    for (i32 i = 0; i < L.n_timer; ++i) {  // ReplicateTimerStartedEvent image
+      const u32 f = M->t_fl[i][t];
+      const i32 src = (i32)((f >> 8) & kStepMask);
+      crr_timer_row r;
+      r.started_id = (i64)M->t_sid[i][t];
+      r.version = ev_ver(src);
+      r.expiry_time = M->t_exp[i][t];
+      r.task_status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+      r.key = M->t_key[i][t];
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.timer(i) = r;
+    }
+    for (i32 i = 0; i < L.n_child; ++i) {
+      const u32 f = M->c_fl[i][t];
+      const i32 src = (i32)((f >> 8) & kStepMask), sst = (i32)((f >> (8 + kStepBits)) & kStepMask);
+      const bool started = sst != (i32)kStepMask;
+      crr_child_row r;
+      r.initiated_id = (i64)M->c_id[i][t];
+      r.version = ev_ver(src);
+      r.initiated_batch_id = batch_first_id(src);
+      r.started_id = started ? ev_id(sst) : CRR_EMPTY_EVENT_ID;
+      r.src = src;
+      r.started_src = started ? sst : -1;
+      r.flags = CRR_ROW_LIVE;
+      r.reserved = 0;
+      *G.child(i) = r;
+    }
+    for (i32 i = 0; i < L.n_rc; ++i) {
+      const i32 src = (i32)((M->r_fl[i][t] >> 8) & kStepMask);
+      crr_initiated_row r;
+      r.initiated_id = (i64)M->r_id[i][t];
+      r.version = ev_ver(src);
+      r.initiated_batch_id = batch_first_id(src);
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.rc(i) = r;
+    }
+    for (i32 i = 0; i < L.n_sig; ++i) {
+      const i32 src = (i32)((M->s_fl[i][t] >> 8) & kStepMask);
+      crr_initiated_row r;
+      r.initiated_id = (i64)M->s_id[i][t];
+      r.version = ev_ver(src);
+      r.initiated_batch_id = batch_first_id(src);
+      r.src = src;
+      r.flags = CRR_ROW_LIVE;
+      *G.sig(i) = r;
+    }
+    for (i32 i = 0; i < L.n_rp; ++i) {
+      const u32 f = M->p_fl[i][t];
+      crr_reset_point_row r;
+      r.src = (i32)((f >> 8) & kStepMask);
+      r.prev_index = (i32)((f >> (8 + kStepBits)) & kStepMask) - 1;
+      r.key = M->p_key[i][t];
+      r.flags = f & 0xFFu;
+      *G.rp(i) = r;
+    }
+  }
+  __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return (i64)M->t_sid[i][t]; }
+  __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return (i64)M->a_sid[i][t]; }
+  __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return (i64)M->s_id[i][t]; }
+  __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return (i64)M->r_id[i][t]; }
+  __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return (i64)M->c_id[i][t]; }
+  // the general path replays a workflow this tier cannot hold: list 0 of the retry pass
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) {
+    const u64 m = __builtin_amdgcn_ballot_w64(true);
+    const u32 lane = threadIdx.x & 63;
+    const u32 leader = (u32)__builtin_ctzll(m);
+    const u32 below = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+    u32 base = 0;
+    if (lane == leader) base = atomicAdd(out.scratch, (u32)__builtin_popcountll(m));
+    base = (u32)__shfl((int)base, (int)leader, 64);
+    out.scratch[retry_slot(in, 0, base + below)] = w;
+  }
+};
+
+// ===================================================================================================
 // WaveTables: one wavefront replays one long history (length bucketing).  The
 // state machine runs wave-uniform (scalar registers); the pending maps are full rows that the 64
 // lanes search in parallel (one ballot per 64 slots), the per-batch timer candidates are built in
@@ -1112,6 +1569,7 @@ struct HbmRows {
 template <class ST>
 struct WaveTables {
   static constexpr bool kResumable = !ST::kLds;  // HbmRows continue a loaded state in place
+  __device__ __forceinline__ static bool fits(i64) { return true; }
   ST S;
   i32 lane;
   i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;
@@ -2022,6 +2480,10 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step) + L.src_base; goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
 
+  if (!P::fits(n_ev)) {
+    L.status = CRR_INTERNAL_RETRY;  // beyond the policy's encodings (CompactTables' 10-bit steps)
+    goto done_events;
+  }
   if (wfp->flags & CRR_WF_FLAG_RESUME) {
     if constexpr (P::kResumable) {
       // the loaded state (mutableStateBuilder.Load, mutable_state_builder.go:306-349) from the rows
@@ -2414,6 +2876,48 @@ __global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outp
   replay_lane_item(in, out, phase, w, &arena, crc_tables);
 }
 #endif
+// Compact LDS tiers (CRR_IN_TIERED segments [compact_begin, compact2_begin) and [compact2_begin,
+// wide_begin)): lane per workflow, 64 lanes per block; slot counts per map chosen by the host's live-set
+// bounds (flatten.COMPACT_TIERS).  A workflow that outgrows its tier goes to the retry pass (list 0).
+using CompactTier1 = CTier<4, 3, 2, 1, 1, 4, 64>;
+using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
+template <class TIER, bool EMIT>
+__device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  __shared__ CompactArena<TIER> arena;
+  build_crc_tables<64>(crc_tables);
+  const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
+  if (w >= hi) return;
+  const crr_workflow* wfp = in.wf + w;
+  const i64 lane = threadIdx.x & 63;
+  Geo G;  // the descriptor in one round trip, as in replay_lds
+  load_geo(G, wfp, out, 64);
+  i64 ev_begin = wfp->ev_begin;
+  const i32 ev_count0 = wfp->ev_count;
+  const u32 wf_flags = wfp->flags;
+  asm volatile("" ::"v"(ev_begin), "v"(ev_count0), "v"(wf_flags));
+  if (((wf_flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  if ((lo & 63u) == 0) {  // wavefront == one interleaved group: group-uniform geometry in SGPRs
+    uniformize_geo(G, lane);
+    ev_begin = uniform64(ev_begin - lane) + lane;
+  }
+  CompactTables<TIER> T;
+  T.init(&arena, &in, ev_begin);
+  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
+  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
+}
+template <bool EMIT>
+__global__ void __launch_bounds__(64) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_compact<CompactTier1, EMIT>(in, out, phase, lo, hi);
+}
+template <bool EMIT>
+__global__ void __launch_bounds__(64) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_compact<CompactTier2, EMIT>(in, out, phase, lo, hi);
+}
+template __global__ void replay_compact1_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact1_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
 // Long-tail workflows the host expects to outgrow the fast kernels' per-wave arenas
 // (CRR_IN_TIERED, [big_begin, n_wf)): one wavefront each with the 57 KB row arena, then HBM rows;
 // launched next to the fast kernels, so the longest of them is not replayed after them.

@@ -45,9 +45,10 @@ class HistoryBatch:
     wave_begin: Optional[int] = None
     # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
     emit_tasks: bool = False
-    # CRR_IN_TIERED: (large_begin, wide_begin, big_begin) -- lane workflows ordered by expected
-    # live-set size; long-tail workflows no fast per-wave arena is expected to hold from big_begin on
-    tiers: Optional[Tuple[int, int, int]] = None
+    # CRR_IN_TIERED: (large_begin, compact_begin, compact2_begin, wide_begin, big_begin) -- lane
+    # workflows ordered by expected live-set size (TIER_SLOTS); long-tail workflows no fast per-wave
+    # arena is expected to hold from big_begin on
+    tiers: Optional[Tuple[int, int, int, int, int]] = None
     # CRR_WF_FLAG_RESUME: the loaded mutable states (batch order) the output rows start from
     init: Optional["LoadedStates"] = None
     # per-workflow key id -> string tables (batch order): (begin, count, off, len, arena), the strings of
@@ -427,7 +428,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
         # a loaded state is continued in place over its HBM rows: the wide (GlobalTables) segment, and
         # in the long tail the replay_big_kernel segment (whose HBM-row pass continues it)
         resumed = (batch.wf["flags"] & abi.WF_FLAG_RESUME) != 0
-        tier = np.where(resumed, 2, tier)
+        tier = np.where(resumed, WIDE, tier)
         bounds = {k: np.where(resumed, np.iinfo(np.int32).max, v) for k, v in bounds.items()}
     n_big = 0
     if tiered:
@@ -442,11 +443,13 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     tiers = None
     if tiered:
         lane_tier = tier[perm[:n_lane]]
-        n0, n01 = int((lane_tier == 0).sum()), int((lane_tier <= 1).sum())
         # segment boundaries on group boundaries, rounded down (a mixed group takes the larger tier)
-        lb = n_lane if n0 == n_lane else n0 // wave * wave
-        wb = n_lane if n01 == n_lane else n01 // wave * wave
-        tiers = (lb, max(wb, lb), n - n_big)
+        bnd = []
+        for k in range(WIDE):
+            c = int((lane_tier <= k).sum())
+            b = n_lane if c == n_lane else c // wave * wave
+            bnd.append(max(b, bnd[-1]) if bnd else b)
+        tiers = (*bnd, n - n_big)
     inv = np.empty(n, np.int64)
     inv[perm] = np.arange(n)
     n_groups = (n_lane + wave - 1) // wave
@@ -575,6 +578,12 @@ def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, 
 
 SMALL_TIER = {"act": 1, "timer": 1, "child": 1, "rc": 1, "sig": 1, "rp": 1}
 LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # CRR_LDS_* defaults
+# replay_kernel.hip CompactTier1 / CompactTier2 (u32 event IDs, 10-bit event steps: <= 1023 events)
+COMPACT1_TIER = {"act": 4, "timer": 3, "child": 2, "rc": 1, "sig": 1, "rp": 4}
+COMPACT2_TIER = {"act": 8, "timer": 6, "child": 3, "rc": 3, "sig": 3, "rp": 8}
+COMPACT_MAX_EVENTS = 1023
+TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER]   # tier classes 0..3; WIDE: HBM rows
+WIDE = len(TIER_SLOTS)
 
 
 def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
@@ -656,21 +665,35 @@ WAVE_LARGE_TIER = {"act": 64, "timer": 48, "child": 24, "rc": 16, "sig": 16, "rp
 
 
 def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:
-    """Per workflow: 0 if its live sets are expected to fit the 1-slot tier, 1 the 2-slot tier, else 2."""
+    """Per workflow: the smallest LDS tier (TIER_SLOTS index) its live sets are expected to fit, WIDE
+    (HBM rows) when none does.  The compact tiers also need <= COMPACT_MAX_EVENTS events and event IDs
+    below 2^32 (their encodings; the kernel hands anything else to the general path anyway)."""
     b = live_set_bounds(batch) if bounds is None else bounds
-    small = np.ones(batch.n_wf, bool)
-    large = np.ones(batch.n_wf, bool)
-    for k in SMALL_TIER:
-        small &= b[k] <= SMALL_TIER[k]
-        large &= b[k] <= LARGE_TIER[k]
-    return np.where(small, 0, np.where(large, 1, 2)).astype(np.int64)
+    cls = np.full(batch.n_wf, WIDE, np.int64)
+    cnt = batch.wf["ev_count"].astype(np.int64)
+    compact_ok = cnt <= COMPACT_MAX_EVENTS
+    if batch.n_events:
+        st = batch.wf_strides()
+        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + (
+            np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)) * np.repeat(st, cnt)
+        big_id = np.zeros(batch.n_wf, bool)
+        np.logical_or.at(big_id, np.repeat(np.arange(batch.n_wf), cnt), batch.cols["event_id"][idx] > 0xFFFFFFFF)
+        compact_ok &= ~big_id
+    for k in range(WIDE - 1, -1, -1):
+        fit = np.ones(batch.n_wf, bool)
+        for m, cap in TIER_SLOTS[k].items():
+            fit &= b[m] <= cap
+        if k >= 2:
+            fit &= compact_ok
+        cls = np.where(fit, k, cls)
+    return cls
 
 
 def fits_small_tier(batch: HistoryBatch, lanes: bool = True) -> bool:
     """Whether the 3-blocks/CU LDS tier holds every workflow's live sets (lane part: 1 entry per
     map, unless ``lanes`` is False; wave tail: the small per-wave arena)."""
     nl = batch.n_wf if batch.wave_begin is None else batch.wave_begin
-    te = batch.tiers[2] if batch.tiers is not None else batch.n_wf   # [te, n): replay_big_kernel
+    te = batch.tiers[-1] if batch.tiers is not None else batch.n_wf   # [te, n): replay_big_kernel
     if not lanes and nl == te:
         return True
     b = live_set_bounds(batch)

@@ -279,10 +279,18 @@ typedef struct crr_inputs {
     uint32_t                 wave_begin;   /* CRR_IN_WAVE_TAIL: workflows [wave_begin, n_wf) are long
                                               histories laid out contiguously (stride 1), replayed one
                                               per wavefront; [0, wave_begin) use `stride` */
-    uint32_t                 large_begin;  /* CRR_IN_TIERED: lane workflows [0, large_begin) are expected */
-    uint32_t                 wide_begin;   /* to hold <= 1 pending entry per map, [large_begin,
-                                              wide_begin) <= 2, [wide_begin, lanes) more (multiples of
-                                              64 except at the end); */
+    /* CRR_IN_TIERED: lane workflows [0, lanes) ordered by expected live-set size in segments replayed
+       by the LDS tier that holds them (each boundary a multiple of 64 or the lane count):
+         [0, large_begin)               <= 1 pending entry per map             (1-slot LDS tier)
+         [large_begin, compact_begin)   <= 2 activities / timers / reset points (2-slot LDS tier)
+         [compact_begin, compact2_begin) compact tier 1 (4 / 3 / 2 / 1 / 1 / 4 slots)
+         [compact2_begin, wide_begin)    compact tier 2 (8 / 6 / 3 / 3 / 3 / 8 slots)
+         [wide_begin, lanes)             more: the workflow's own HBM rows
+       (activity / timer / child / request-cancel / signal / reset-point slots; flatten.py) */
+    uint32_t                 large_begin;
+    uint32_t                 compact_begin;
+    uint32_t                 compact2_begin;
+    uint32_t                 wide_begin;
     uint32_t                 big_begin;    /* long-tail workflows [big_begin, n_wf) are expected to outgrow
                                               the fast kernels' per-wave arenas (replayed concurrently
                                               with the 57-KB arena); n_wf: none */

@@ -166,7 +166,7 @@ def test_retry_routes(engine):
     assert (peak > 8).sum() > 10                       # retried, outgrow it
     check(engine, interleave(b, long_threshold=None, tiered=False))   # fast tier, then the retry pass
     tb = interleave(b, long_threshold=None)                            # tier segments: small | large | wide
-    assert 0 < tb.tiers[0] <= tb.tiers[1] < tb.n_wf
+    assert 0 < tb.tiers[0] <= tb.tiers[1] <= tb.tiers[2] <= tb.tiers[3] < tb.n_wf
     check(engine, tb)
     lt = flatten(synth_mixed.long_tail_histories(120, 9, max_len=3000, run_cap=1200, caps=None),
                  known_domains=KNOWN)

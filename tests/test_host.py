@@ -155,11 +155,11 @@ def test_replay_rejects_unaligned_tier_segments():
         setattr(ci, f, dummy.value)
     ci.n_wf, ci.stride, ci.flags = 1000, 64, abi.IN_TIERED
     co = abi.COutputs(*([dummy.value] * len(abi.COutputs._fields_)))
-    for lb, wb in ((100, 1000), (128, 130), (3, 3)):
-        ci.large_begin, ci.wide_begin = lb, wb
-        assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1, (lb, wb)
+    for bnd in ((100, 1000, 1000, 1000), (128, 130, 1000, 1000), (3, 3, 3, 3), (128, 128, 192, 200)):
+        ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin = bnd
+        assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1, bnd
     ci.stride = 1                        # tier segments are a stride-64 layout only
-    ci.large_begin = ci.wide_begin = 1000
+    ci.large_begin = ci.compact_begin = ci.compact2_begin = ci.wide_begin = 1000
     assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1
 
 
@@ -184,21 +184,22 @@ def test_interleave_tier_segments():
     hs = synth_mixed.mixed_histories(1000, 33, mean_len=50)
     b = flatten(hs)
     cls = tier_classes(b)
-    assert len(np.unique(cls)) == 3
+    assert len(np.unique(cls)) >= 4
     ib = interleave(b, long_threshold=70)
-    lb, wb, bb = ib.tiers
+    *bnd, bb = ib.tiers
     nl = ib.wave_begin
     c = cls[ib.perm[:nl]]
     assert (np.diff(c) >= 0).all()
-    assert lb % 64 == 0 and (wb % 64 == 0 or wb == nl) and lb <= wb <= nl
-    assert (c[:lb] == 0).all() and (c[lb:wb] <= 1).all()
+    assert all(b % 64 == 0 or b == nl for b in bnd) and list(bnd) == sorted(bnd) and bnd[-1] <= nl
+    for k, b in enumerate(bnd):      # segment k holds classes <= k (a mixed group takes the larger tier)
+        assert (c[:b] <= k).all()
     assert ib.c_flags() & abi.IN_TIERED
     cnt = ib.wf["ev_count"]
     assert nl <= bb <= ib.n_wf
     assert (np.diff(cnt[nl:bb]) <= 0).all() and (np.diff(cnt[bb:]) <= 0).all()
-    for k in range(3):
+    for k in range(5):
         seg = cnt[:nl][c == k]
         assert (np.diff(seg) <= 0).all()
     # one tier only: no segments beyond the lanes
     ic = interleave(synth.activity_chain(1000, 2, 3))
-    assert ic.tiers == (ic.n_wf, ic.n_wf, ic.n_wf)
+    assert ic.tiers == (ic.n_wf,) * 5

@@ -17,6 +17,8 @@ __global__ void replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase
 template <bool EMIT>
 __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+template <bool EMIT>
+__global__ void replay_tail_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
@@ -66,7 +68,7 @@ bool ensure_events() {
 
 // Tier segments of one phase run concurrently: side streams fork from and join back into the
 // caller's stream with events (created once per thread and device).
-constexpr int kSide = 5;
+constexpr int kSide = 6;
 struct SideStreams {
   hipStream_t st[kSide] = {};
   hipEvent_t fork = nullptr, join[kSide] = {};
@@ -198,15 +200,16 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
         const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
         const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
-        const bool run_small = lb > 0 || (tail && small), run_large = cb > lb || (tail && !small);
+        const bool run_small = lb > 0, run_large = cb > lb, run_tail = tail && tail_end > n_lane;
         const bool run_c1 = c2 > cb, run_c2 = wb > c2, run_wide = wb < n_lane;
         const bool run_big = tail_end < in->n_wf;
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
-        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_wide + (int)run_big > 1 &&
+        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_wide + (int)run_big +
+                              (int)run_tail > 1 &&
                           ensure_side_streams();
         hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
-        hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s;
+        hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s, s_tail = fork ? g_side.st[5] : s;
         if (fork) {
           (void)hipEventRecord(g_side.fork, s);
           for (hipStream_t x : g_side.st) (void)hipStreamWaitEvent(x, g_side.fork, 0);
@@ -214,6 +217,10 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_big)  // the longest histories first
           hipLaunchKernelGGL(crr::replay_big_kernel, dim3(in->n_wf - tail_end), dim3(64), 0, s_big, *in, *out, phase,
                              tail_end, in->n_wf);
+        if (run_tail) {  // the long-history tail, one wavefront each
+          if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+        }
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, wb, n_lane);
@@ -225,8 +232,8 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
           else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
         }
-        launch_fast(s_large, false, tail && !small, lb, cb);
-        launch_fast(s, true, tail && small, 0, lb);
+        launch_fast(s_large, false, false, lb, cb);
+        launch_fast(s, true, false, 0, lb);
         if (fork) {
           for (int i = 0; i < kSide; ++i) {
             (void)hipEventRecord(g_side.join[i], g_side.st[i]);

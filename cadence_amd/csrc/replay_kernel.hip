@@ -27,9 +27,15 @@
 
 // Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
 // checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
-// record loads, bit 16 the start side record loads.
+// record loads, bit 16 the start side record loads.  Bit 128 keeps outputs valid and counts shader
+// cycles per event type in the one-wavefront-per-workflow path (crr_debug_cycles).
 #ifndef CRR_EXP
 #define CRR_EXP 0
+#endif
+#if CRR_EXP & 128
+// [part][event type]: part 0 prologue, 1 dispatch, 2 batch epilogue, 3 events; [4][0..2] workflow
+// cycles, workflows, cycles from the end of the event loop (finalize + checksum + row write)
+__device__ unsigned long long crr_dbg[5 * 64];
 #endif
 #ifndef CRR_LDS_ACT
 #define CRR_LDS_ACT 2
@@ -1542,7 +1548,7 @@ __device__ __forceinline__ void wave_sync_global() {  // ... and its global-memo
 
 template <class ARENA, int LIST>
 struct LdsRows {
-  static constexpr bool kLds = true;
+  static constexpr bool kLds = true, kReg = false;
   static constexpr int kList = LIST;  // scratch list a workflow that outgrows the arena is handed to
   static constexpr i32 A = ARENA::A, T = ARENA::T, C = ARENA::C, R = ARENA::R, S = ARENA::S, P = ARENA::P;
   ARENA* M;
@@ -1553,8 +1559,30 @@ struct LdsRows {
   __device__ __forceinline__ crr_initiated_row& sig(i32 j) const { return M->sig[j]; }
   __device__ __forceinline__ crr_reset_point_row& rp(i32 j) const { return M->rp[j]; }
 };
+// Rows in registers: slot j < 64 is held by lane j (every accessor returns the calling lane's own
+// row; WaveTables reads another slot only through bcast, a readlane from its owner).  No LDS and no
+// memory round trip per lookup: a find is a compare and a ballot.  A workflow that outgrows 64
+// slots of a map is replayed again over HBM rows by the caller (kList < 0).  Built with
+// CRR_TAIL_LDS=0 only: measured slower than the LDS arena on the long tail (the 70 row registers are
+// copied around the loop's merge points, ~4x the VALU instructions per event, and spill).
+struct RegRows {
+  static constexpr bool kLds = false, kReg = true;
+  static constexpr int kList = -1;
+  static constexpr i32 A = 64, T = 64, C = 64, R = 64, S = 64, P = 64;
+  mutable crr_activity_row a;
+  mutable crr_timer_row t;
+  mutable crr_child_row c;
+  mutable crr_initiated_row r, s;
+  mutable crr_reset_point_row p;
+  __device__ __forceinline__ crr_activity_row& act(i32) const { return a; }
+  __device__ __forceinline__ crr_timer_row& timer(i32) const { return t; }
+  __device__ __forceinline__ crr_child_row& child(i32) const { return c; }
+  __device__ __forceinline__ crr_initiated_row& rc(i32) const { return r; }
+  __device__ __forceinline__ crr_initiated_row& sig(i32) const { return s; }
+  __device__ __forceinline__ crr_reset_point_row& rp(i32) const { return p; }
+};
 struct HbmRows {
-  static constexpr bool kLds = false;
+  static constexpr bool kLds = false, kReg = false;
   static constexpr int kList = -1;    // never outgrown
   static constexpr i32 A = 0x3fffffff, T = A, C = A, R = A, S = A, P = A;
   Geo G;
@@ -1568,7 +1596,7 @@ struct HbmRows {
 
 template <class ST>
 struct WaveTables {
-  static constexpr bool kResumable = !ST::kLds;  // HbmRows continue a loaded state in place
+  static constexpr bool kResumable = !ST::kLds && !ST::kReg;  // HbmRows continue a loaded state in place
   __device__ __forceinline__ static bool fits(i64) { return true; }
   ST S;
   i32 lane;
@@ -1747,7 +1775,7 @@ struct WaveTables {
   __device__ __forceinline__ void load(Lane& L, const Geo& G) {
     hw_act = L.n_act; hw_timer = L.n_timer; hw_child = L.n_child; hw_rc = L.n_rc; hw_sig = L.n_sig;
     dirty_act = dirty_timer = true;
-    if constexpr (!ST::kLds) {
+    if constexpr (kResumable) {
       for (i32 j = lane; j < hw_act; j += 64) {
         crr_activity_row& r = S.act(j);
         const u32 key = r.key;
@@ -1925,8 +1953,32 @@ struct WaveTables {
     }
     wave_sync_global();
   }
+  // RegRows: each lane's live row -> HBM slot rank (number of smaller live IDs, from the other
+  // lanes' IDs by readlane); the checksum then reads the IDs back from the HBM rows
+  template <class R, class IdOf>
+  __device__ __forceinline__ void scatter_reg(const R& r, i32 hw, R* (Geo::*dst)(i32) const, const Geo& G,
+                                              IdOf id_of) const {
+    const bool live = lane < hw && (r.flags & CRR_ROW_LIVE);
+    const i64 id = id_of(r);
+    u64 m = __builtin_amdgcn_ballot_w64(live);
+    i32 rank = 0;
+    while (m) {
+      const i32 l = (i32)__builtin_ctzll(m);
+      m &= m - 1;
+      rank += readlane64(id, l) < id ? 1 : 0;
+    }
+    if (live) *(G.*dst)(rank) = r;
+  }
   __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
-    if constexpr (ST::kLds) {
+    if constexpr (ST::kReg) {
+      scatter_reg(S.a, hw_act, &Geo::act, G, [](const crr_activity_row& r) { return r.schedule_id; });
+      scatter_reg(S.t, hw_timer, &Geo::timer, G, [](const crr_timer_row& r) { return r.started_id; });
+      scatter_reg(S.c, hw_child, &Geo::child, G, [](const crr_child_row& r) { return r.initiated_id; });
+      scatter_reg(S.r, hw_rc, &Geo::rc, G, [](const crr_initiated_row& r) { return r.initiated_id; });
+      scatter_reg(S.s, hw_sig, &Geo::sig, G, [](const crr_initiated_row& r) { return r.initiated_id; });
+      if (lane < L.n_rp) *G.rp(lane) = S.p;
+      wave_sync_global();
+    } else if constexpr (ST::kLds) {
       i64* ids = S.M->ids;
       constexpr i32 oT = ST::A, oC = oT + ST::T, oR = oC + ST::C, oS = oR + ST::R;
       scatter<crr_activity_row>(A_(), hw_act, ids, &Geo::act, G, [](const crr_activity_row& r) { return r.schedule_id; });
@@ -2454,6 +2506,15 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   const i32 n_ev = wfp->ev_count;
   const i32 empty_at = wfp->empty_batch_at;
   const i64 now_ns = wfp->now_ns;
+  // read once: a descriptor field read inside the loop is reloaded every event (stores in between may
+  // alias it), and its wait drains the prefetched columns with it
+  const i32 retention_days = wfp->retention_days;
+#if CRR_EXP & 128
+  constexpr bool kDbg = std::is_same<SRC, WaveSource>::value;
+  const i32 dbg_lane = (i32)(threadIdx.x & 63);
+  u64 dbg_p = 0, dbg_d = 0, dbg_e = 0, dbg_n = 0, dbg_c0 = 0, dbg_c1 = 0, dbg_c2 = 0, dbg_t0 = 0, dbg_t1 = 0;
+  if constexpr (kDbg) dbg_t0 = __builtin_readcyclecounter();
+#endif
 
   // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
   Lane L;
@@ -2527,6 +2588,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 
   src.start();
   for (i32 s = 0; s < n_ev; ++s) {
+#if CRR_EXP & 128
+    if constexpr (kDbg) dbg_c0 = __builtin_readcyclecounter();
+#endif
     // one loop exit for the whole prologue: the checks become a select chain (no divergent branch
     // per check), and on success vh_last = (id, ver) in every case (new item, same version, first).
     const Ev ev = src.next(s);
@@ -2565,24 +2629,40 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     // common case: histories of one workflow type replay in lockstep) the type is wave-uniform
     // and the switch runs on a scalar register -- scalar branches, no exec-mask tree; otherwise
     // the per-lane switch.
+#if CRR_EXP & 128
+    if constexpr (kDbg) dbg_c1 = __builtin_readcyclecounter();
+#endif
     {
       int rc;
       const i32 tu = uniform32(t);
       const i32 ps = s + L.src_base;  // provenance step of the event (rows' *_src)
-      if (__builtin_amdgcn_ballot_w64(t != tu) == 0)
+      if (std::is_same<SRC, WaveSource>::value || __builtin_amdgcn_ballot_w64(t != tu) == 0)  // WaveSource: readlane, uniform
         rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
-                         K, wfp->retention_days);
+                         K, retention_days);
       else
         rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
-                         K, wfp->retention_days);
+                         K, retention_days);
       if (rc) FAIL(rc, s);
     }
+#if CRR_EXP & 128
+    if constexpr (kDbg) dbg_c2 = __builtin_readcyclecounter();
+#endif
 
     if (et & CRR_ETYPE_BATCH_LAST) {
       if (!(CRR_EXP & 2)) T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
       L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
+#if CRR_EXP & 128
+    if constexpr (kDbg) {
+      const u64 c3 = __builtin_readcyclecounter();
+      const bool mine = dbg_lane == t;
+      dbg_p += mine ? dbg_c1 - dbg_c0 : 0;
+      dbg_d += mine ? dbg_c2 - dbg_c1 : 0;
+      dbg_e += mine ? c3 - dbg_c2 : 0;
+      dbg_n += mine ? 1 : 0;
+    }
+#endif
   }
   {
     // what the tail reads from HBM -- the last TaskID, the token and rebuild fields of the descriptor --
@@ -2609,6 +2689,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 done_events:
 #undef CHECK
 #undef FAIL
+#if CRR_EXP & 128
+  if constexpr (kDbg) dbg_t1 = __builtin_readcyclecounter();
+#endif
   if (!task_read && last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
   if (L.status == CRR_OK && K.on && L.n_tasks > G.task_cap) L.status = CRR_ERR_CAPACITY;
@@ -2669,6 +2752,20 @@ done_events:
   R.reserved = 0;
   if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
+#if CRR_EXP & 128
+  if constexpr (kDbg) {
+    atomicAdd(&crr_dbg[dbg_lane], (unsigned long long)dbg_p);
+    atomicAdd(&crr_dbg[64 + dbg_lane], (unsigned long long)dbg_d);
+    atomicAdd(&crr_dbg[128 + dbg_lane], (unsigned long long)dbg_e);
+    atomicAdd(&crr_dbg[192 + dbg_lane], (unsigned long long)dbg_n);
+    const u64 c4 = __builtin_readcyclecounter();
+    if (dbg_lane == 0) {
+      atomicAdd(&crr_dbg[256], (unsigned long long)(c4 - dbg_t0));
+      atomicAdd(&crr_dbg[257], 1ull);
+      atomicAdd(&crr_dbg[258], (unsigned long long)(c4 - dbg_t1));
+    }
+  }
+#endif
 }
 
 // ---- kernels ---------------------------------------------------------------------------------------
@@ -2798,7 +2895,7 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 // Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
 // the list counters, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
-template <class ST>
+template <class ST, bool EMIT = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  WaveTables<ST>& T, const u32* crc_tables) {
   const crr_workflow* wfp = in.wf + w;
@@ -2806,11 +2903,11 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   const i64 st = wf_stride(in, w);
   Geo G;
   load_geo(G, wfp, out, st);
-  if constexpr (!ST::kLds) T.S.G = G;
+  if constexpr (std::is_same<ST, HbmRows>::value) T.S.G = G;
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
 }
 __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  LdsArena<HugeTier>* arena, const u32* crc_tables) {
@@ -2935,6 +3032,40 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
     replay_wave_item(in, out, phase, w, H, crc_tables);
   }
 }
+// Long-history tail of a CRR_IN_TIERED batch ([wave_begin, big_begin), longest first): one wavefront
+// per workflow with its rows in registers, no LDS arena, so occupancy is register-limited and the
+// tail's wavefronts all run at once; a workflow that outgrows 64 slots (or resumes a loaded state)
+// is replayed again over its HBM rows.
+#ifndef CRR_TAIL_WAVES_PER_EU
+#define CRR_TAIL_WAVES_PER_EU 2
+#endif
+#ifndef CRR_TAIL_LDS
+#define CRR_TAIL_LDS 1
+#endif
+template <bool EMIT>
+__global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(crr_inputs in, crr_outputs out, int phase,
+                                                                             u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+#if CRR_TAIL_LDS
+  __shared__ WaveTier<LargeTier>::Arena arena;
+#endif
+  const u32 w = lo + blockIdx.x;
+  if (w >= hi) return;
+  build_crc_tables(crc_tables);
+#if CRR_TAIL_LDS
+  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, -1>> T;
+  T.S.M = &arena;
+#else
+  WaveTables<RegRows> T;
+#endif
+  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables);
+  if (T.retried) {
+    WaveTables<HbmRows> H;
+    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables);
+  }
+}
+template __global__ void replay_tail_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_tail_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
 union RetryArena {
   LdsArena<HugeTier> lane;
   BigArena wave;
@@ -2984,6 +3115,15 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
     }
   }
 }
+
+#if CRR_EXP & 128
+extern "C" int crr_debug_cycles(unsigned long long* dst, int n) {  // read and clear crr_dbg
+  if (n > 5 * 64) n = 5 * 64;
+  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(crr_dbg), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+  static const unsigned long long zero[5 * 64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(crr_dbg), zero, sizeof(zero)) == hipSuccess ? n : -1;
+}
+#endif
 
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).
 __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {

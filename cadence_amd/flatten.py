@@ -403,7 +403,7 @@ LONG_HISTORY = 256   # lane per workflow up to ~256 events, a wa
 
 
 def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[int] = LONG_HISTORY,
-               tiered: bool = True) -> HistoryBatch:
+               tiered: bool = True, big_caps: Optional[Dict[str, int]] = None) -> HistoryBatch:
     """Permute a canonical batch into the device layout.
 
     Workflows are sorted by event count (descending; ties by index) and packed 64 per group.
@@ -411,7 +411,8 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     workflow see CRR_EV_PAD slots.  With ``long_threshold`` (length bucketing), workflows longer
     than it form a tail after the groups: contiguous events and rows (stride 1), one wavefront
     each on the device (``long_threshold=None``: every workflow lane per workflow).  CAN ``aux``
-    references are remapped to device positions.  ``tiered``: lane workflows are first ordered by
+    references are remapped to device positions.  ``big_caps``: per-map live-set bounds above which a
+    long workflow goes to replay_big_kernel instead of the tail kernel (default WAVE_BIG_CAPS).  ``tiered``: lane workflows are first ordered by
     the LDS tier their live sets are expected to fit (``live_set_bounds``: 1 entry per map, 2, more;
     CRR_IN_TIERED), so each segment runs with the tier that holds it instead of being retried.
     """
@@ -434,7 +435,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     if tiered:
         lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
         big = np.zeros(longs.size, bool)                          # the tail: arena-sized first, then big
-        for k, cap in WAVE_LARGE_TIER.items():
+        for k, cap in (WAVE_BIG_CAPS if big_caps is None else big_caps).items():
             big |= bounds[k][longs] > cap
         longs = np.concatenate([longs[~big], longs[big]])
         n_big = int(big.sum())
@@ -661,7 +662,11 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
 
 # per-wave LDS arenas of the wave-per-workflow tail (replay_kernel.hip WaveTier<SmallTier>)
 WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp": 24}
-WAVE_LARGE_TIER = {"act": 64, "timer": 48, "child": 24, "rc": 16, "sig": 16, "rp": 32}   # WaveTier<LargeTier>
+# replay_tail_kernel's per-wave LDS arena is WaveTier<LargeTier> (64/48/24/16/16/32 rows); a workflow that
+# outgrows it is replayed again over its HBM rows in the same wavefront.  Only beyond 64 entries in some map
+# does a workflow go to replay_big_kernel (whose one-wave blocks hold a 57 KB arena): measured on the config-4
+# long tail, sending everything past the arena there costs more (poor occupancy) than the in-place retries.
+WAVE_BIG_CAPS = {"act": 64, "timer": 64, "child": 64, "rc": 64, "sig": 64, "rp": 64}
 
 
 def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:

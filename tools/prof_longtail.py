@@ -24,6 +24,8 @@ def main():
     p.add_argument("--unbounded", action="store_true", help="unbounded pending sets (random walk)")
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
     p.add_argument("--native", action="store_true", help="native generator (synth_native.long_tail)")
+    p.add_argument("--big-caps", type=int, default=None, help="one live-set bound for every map above which a long "
+                   "workflow goes to replay_big_kernel (default: the tail arena's own; huge: none)")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -49,10 +51,12 @@ def main():
     ref = None
     for th in a.thresholds.split(","):
         thv = None if th == "none" else int(th)
-        ib = interleave(b, long_threshold=thv)
+        caps = None if a.big_caps is None else {k: a.big_caps for k in ("act", "timer", "child", "rc", "sig", "rp")}
+        ib = interleave(b, long_threshold=thv, big_caps=caps)
         db = eng.upload(ib)
         eng.launch(db)
         torch.cuda.synchronize()
+        dbg = debug_cycles(eng)      # clears the instrumented build's counters (None otherwise)
         ms = []
         for _ in range(a.reps):
             eng.launch(db)
@@ -68,11 +72,46 @@ def main():
             same = not diff_results(ref[0], ref[1], ib, res)
         med = float(np.median(ms))
         print(json.dumps({"lib": a.lib, "threshold": th, "unbounded": a.unbounded, "workflows": b.n_wf, "events": int(cnt.sum()), "max_len": int(cnt.max()),
-                          "wave_tail": int(b.n_wf - (ib.wave_begin if ib.wave_begin is not None else b.n_wf)),
+                          "wave_tail": int(b.n_wf - (ib.wave_begin if ib.wave_begin is not None else b.n_wf)), "big_caps": a.big_caps,
+                          "tiers": list(ib.tiers) if ib.tiers else None,
                           "kernel_ms": ms, "median_ms": med, "events_per_s": float(cnt.sum()) / (med * 1e-3),
                           "ok": int((res.exec["status"] == 0).sum()), "same_as_first": same,
                           "retries_lane_wave": retries, "phase_ms": k,
                           "gen_s": gen_s}), flush=True)
+        dbg = debug_cycles(eng)
+        if dbg is not None:
+            print_cycles(dbg, a.reps)
+
+
+def debug_cycles(eng):
+    """CRR_EXP=128 builds: per-event-type shader cycles of the one-wavefront-per-workflow path."""
+    import ctypes
+    import numpy as np
+    f = getattr(eng.lib, "crr_debug_cycles", None)
+    if f is None:
+        return None
+    buf = (ctypes.c_ulonglong * 320)()
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if f(ctypes.addressof(buf), 320) != 320:
+        raise RuntimeError("crr_debug_cycles failed")
+    return np.frombuffer(buf, np.uint64).astype(np.float64).reshape(5, 64)
+
+
+def print_cycles(d, reps):
+    import numpy as np
+    from cadence_amd.abi import EventType
+    names = {int(e): e.name for e in EventType}
+    n = d[3]
+    tot = d[0] + d[1] + d[2]
+    print(f"wave path: {d[4][1] / reps:.0f} workflows/launch, {n.sum() / reps:.0f} events/launch, "
+          f"{d[4][0] / max(n.sum(), 1):.0f} cycles/event overall, {d[4][2] / max(d[4][1], 1):.0f} cycles/workflow tail")
+    print(f"{'type':42s} {'events':>10s} {'share':>6s} {'prolog':>7s} {'disp':>7s} {'epil':>7s} {'cyc%':>6s}")
+    for t in np.argsort(-tot):
+        if n[t] == 0:
+            continue
+        print(f"{names.get(int(t), str(t)):42s} {n[t] / reps:10.0f} {n[t] / n.sum():6.3f} {d[0][t] / n[t]:7.0f} "
+              f"{d[1][t] / n[t]:7.0f} {d[2][t] / n[t]:7.0f} {tot[t] / tot.sum() * 100:6.1f}")
+    print(flush=True)
 
 
 if __name__ == "__main__":

@@ -23,6 +23,35 @@ DIGEST_LEN = 6
 GOLDEN = 0x9E3779B1
 
 
+NUM_SHARDS = 16384   # numHistoryShards of the synthetic workloads
+
+
+def mix64(x: np.ndarray) -> np.ndarray:
+    """SplitMix64 finalizer over uint64 arrays (wrapping arithmetic)."""
+    x = np.asarray(x, np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def synthetic_shard_ids(w: np.ndarray, num_shards: int = NUM_SHARDS) -> np.ndarray:
+    """History shard of synthetic workflow index w -- the stand-in for WorkflowIDToHistoryShard
+    (common/util.go:313-316, farm.Fingerprint32(workflowID) % numberOfShards); the same function as
+    the native generator's crr_synth_shard_of."""
+    with np.errstate(over="ignore"):
+        h = mix64(np.asarray(w, np.uint64) + np.uint64(0x9E3779B97F4A7C15))
+    return (h % np.uint64(num_shards)).astype(np.int64)
+
+
+def rank_workflows(n_global: int, rank: int, world: int, num_shards: int = NUM_SHARDS) -> np.ndarray:
+    """Global indices of the workflows of a n_global-workflow workload that ``rank`` replays."""
+    w = np.arange(n_global, dtype=np.int64)
+    if world <= 1:
+        return w
+    return w[workflow_mask(synthetic_shard_ids(w, num_shards), rank, world)]
+
+
 def shards_for_rank(num_shards: int, rank: int, world: int) -> np.ndarray:
     """History shards owned by ``rank``: {s : s mod world == rank}."""
     return np.arange(rank, num_shards, world, dtype=np.int64)

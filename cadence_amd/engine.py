@@ -49,6 +49,10 @@ def lib():
         L.crr_timing_begin.restype = ctypes.c_int
         L.crr_timing_read.argtypes = [vp, ctypes.c_int]
         L.crr_timing_read.restype = ctypes.c_int
+        L.crr_compact_rows.argtypes = [vp, vp, vp, vp]
+        L.crr_compact_rows.restype = ctypes.c_int
+        L.crr_compact_scratch_bytes.argtypes = [ctypes.c_uint32]
+        L.crr_compact_scratch_bytes.restype = ctypes.c_size_t
         if L.crr_abi_version() != abi.ABI_VERSION:
             raise EngineUnavailable("ABI version mismatch")
         abi.check_layout(L)
@@ -71,6 +75,7 @@ class DeviceBatch:
     c_in: abi.CInputs
     c_out: abi.COutputs
     device: int
+    c_compact: Optional[object] = None
 
     @property
     def n_wf(self):
@@ -198,10 +203,81 @@ class ReplayEngine:
             tables[name] = T["out_" + name].cpu().numpy().view(dt)   # .cpu() is already a fresh host copy
         return ReplayResult(ex, tables)
 
+    # -- compacted download --------------------------------------------------------------------------
+    def compact(self, db: DeviceBatch, stream=None):
+        """Enqueue crr_compact_rows after the replay (same stream): dense live rows on the device."""
+        torch = self.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.dev)
+        T = db.tensors
+        if "cmp_offsets" not in T:
+            for name, dt, *_ in abi.TABLES:
+                rows = max(db.batch.table_rows.get(name, 0), 1) if (name != "tasks" or db.batch.emit_tasks) else 1
+                T["cmp_" + name] = torch.empty(rows * dt.itemsize, dtype=torch.uint8, device=self.dev)
+            T["cmp_offsets"] = torch.empty(len(COMPACT_TABLES) * (db.n_wf + 1), dtype=torch.int64, device=self.dev)
+            T["cmp_scratch"] = torch.empty(int(self.lib.crr_compact_scratch_bytes(db.n_wf)), dtype=torch.uint8,
+                                           device=self.dev)
+            co = CCompactOut()
+            for i, name in enumerate(COMPACT_TABLES):
+                co.rows[i] = T["cmp_" + name].data_ptr()
+            co.offsets = T["cmp_offsets"].data_ptr()
+            co.scratch = T["cmp_scratch"].data_ptr()
+            db.c_compact = co
+        rc = self.lib.crr_compact_rows(ctypes.byref(db.c_in), ctypes.byref(db.c_out), ctypes.byref(db.c_compact),
+                                       ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_compact_rows failed: {rc}")
+
+    def download_compact(self, db: DeviceBatch) -> CompactResult:
+        """Synchronise and copy the exec rows and the compacted live rows (exact sizes) to the host."""
+        self.torch.cuda.synchronize(self.dev)
+        T = db.tensors
+        n = db.n_wf
+        off = T["cmp_offsets"].cpu().numpy().reshape(len(COMPACT_TABLES), n + 1)
+        ex = T["exec"][:n * abi.EXEC_ROW.itemsize].cpu().numpy().view(abi.EXEC_ROW).copy()
+        rows = {}
+        for t, (name, dt, *_) in enumerate(abi.TABLES):
+            tot = int(off[t, n])
+            rows[name] = T["cmp_" + name][:tot * dt.itemsize].cpu().numpy().view(dt)
+        return CompactResult(ex, off, rows)
+
     def replay(self, batch: HistoryBatch) -> ReplayResult:
         db = self.upload(batch)
         self.launch(db)
         return self.download(db)
+
+
+COMPACT_TABLES = [t[0] for t in abi.TABLES]   # crr_compact_out.rows order
+
+
+class CCompactOut(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_void_p * len(COMPACT_TABLES)), ("offsets", ctypes.c_void_p), ("scratch", ctypes.c_void_p)]
+
+
+@dataclasses.dataclass
+class CompactResult:
+    """A replay's persisted output as downloaded by ``crr_compact_rows``: the exec rows and every
+    workflow's live rows, dense per table (batch order), with per-table exclusive prefixes."""
+    exec: np.ndarray                 # abi.EXEC_ROW [n_wf]
+    offsets: np.ndarray              # int64 [len(COMPACT_TABLES), n_wf + 1]
+    rows: Dict[str, np.ndarray]
+
+    def to_replay_result(self, batch: HistoryBatch) -> ReplayResult:
+        """Scatter the live rows back into the batch's slot-table layout (host side, for comparisons
+        with ``diff_results``; slots past a workflow's count stay zero)."""
+        from .result import allocate_host
+        res = allocate_host(batch)
+        res.exec[:] = self.exec
+        st = batch.wf_strides()
+        for t, (name, _dt, base_f, _c, _n) in enumerate(abi.TABLES):
+            off = self.offsets[t]
+            c = np.diff(off)
+            tot = int(off[-1])
+            if tot == 0 or name not in self.rows:
+                continue
+            wf_idx = np.repeat(np.arange(batch.n_wf), c)
+            slot = np.arange(tot) - np.repeat(off[:-1], c)
+            res.tables[name][batch.wf[base_f].astype(np.int64)[wf_idx] + slot * st[wf_idx]] = self.rows[name][:tot]
+        return res
 
 
 def crc32(data: bytes) -> int:

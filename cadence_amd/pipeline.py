@@ -1,0 +1,142 @@
+"""End-to-end replay from host buffers: pinned staging, chunked and overlapped.
+
+What a caller that holds histories in host memory pays (SURVEY.md §8d's PCIe-inclusive figure): the
+columns go up from pinned staging buffers (where the native decoder / flattener writes them), the
+replay and the live-row compaction (``crr_compact_rows``) run on the device, and only the exec rows
+and the dense live rows come back, into pinned buffers.  Three HIP streams: uploads of chunk i+1.. run
+while chunk i replays and while chunk i-1 downloads (PCIe is full duplex), so the wall time tends to
+the larger of the two transfer totals rather than their sum.
+
+Setup (untimed, once per batch shape): pinned host copies of the inputs, device buffers, pinned
+output buffers.  Timed: per chunk, the uploads, zero-filling the outputs, the replay, the compaction,
+the download of the exact live-row counts.  Replays from scratch only (a batch with loaded states,
+CRR_WF_FLAG_RESUME, keeps its rows in the output buffers this zero-fills).
+"""
+from __future__ import annotations
+
+import dataclasses
+import time
+from typing import Dict, List
+
+import numpy as np
+
+from . import abi
+from .engine import COMPACT_TABLES, CompactResult, DeviceBatch, ReplayEngine
+from .flatten import HistoryBatch
+
+
+@dataclasses.dataclass
+class _Chunk:
+    batch: HistoryBatch
+    db: DeviceBatch
+    host_in: Dict[str, object]        # name -> pinned uint8 tensor
+    dev_in: Dict[str, object]         # name -> device uint8 tensor (same bytes)
+    host_exec: object
+    host_off: object
+    host_rows: Dict[str, object]
+    host_tot: object
+    totals: np.ndarray = None
+
+
+def _input_arrays(batch: HistoryBatch) -> Dict[str, np.ndarray]:
+    arrs = {"ev_" + name: np.asarray(batch.cols[name], dtype=t) for name, t in abi.EVENT_COLUMNS}
+    arrs.update(act_side=batch.act_side, start_side=batch.start_side, reset_keys=batch.reset_keys,
+                arena=np.concatenate([batch.arena, np.zeros(16, np.uint8)]), wf=batch.wf)
+    return {k: np.ascontiguousarray(v).view(np.uint8).reshape(-1) for k, v in arrs.items()}
+
+
+class StreamingReplay:
+    """Chunked host -> device -> host replay of a list of (interleaved) batches."""
+
+    def __init__(self, eng: ReplayEngine, chunks: List[HistoryBatch]):
+        torch = eng.torch
+        self.eng, self.torch = eng, torch
+        self.chunks: List[_Chunk] = []
+        for b in chunks:
+            db = eng.upload(b)                      # device buffers (inputs + outputs) and the C structs
+            arrs = _input_arrays(b)
+            host_in, dev_in = {}, {}
+            for k, a in arrs.items():
+                host_in[k] = torch.from_numpy(a.copy()).pin_memory()
+                dev_in[k] = db.tensors[k][:a.size]
+            eng.compact(db)                         # allocates the dense buffers (first call)
+            n = b.n_wf
+            host_rows = {name: torch.empty(db.tensors["cmp_" + name].numel(), dtype=torch.uint8).pin_memory()
+                         for name in COMPACT_TABLES}
+            self.chunks.append(_Chunk(
+                b, db, host_in, dev_in,
+                torch.empty(n * abi.EXEC_ROW.itemsize, dtype=torch.uint8).pin_memory(),
+                torch.empty(len(COMPACT_TABLES) * (n + 1), dtype=torch.int64).pin_memory(),
+                host_rows, torch.empty(len(COMPACT_TABLES), dtype=torch.int64).pin_memory()))
+        torch.cuda.synchronize(eng.dev)
+        self.up = torch.cuda.Stream(eng.dev)
+        self.comp = torch.cuda.Stream(eng.dev)
+        self.down = torch.cuda.Stream(eng.dev)
+
+    @property
+    def n_events(self) -> int:
+        return sum(c.batch.n_events for c in self.chunks)
+
+    @property
+    def h2d_bytes(self) -> int:
+        return int(sum(t.numel() for c in self.chunks for t in c.host_in.values()))
+
+    def run(self) -> Dict[str, float]:
+        """One timed pass over every chunk; returns wall time and transfer volumes."""
+        torch, eng = self.torch, self.eng
+        torch.cuda.synchronize(eng.dev)
+        t0 = time.perf_counter()
+        ev_up, ev_tot = [], []
+        for c in self.chunks:                                      # 1. every upload, in order
+            with torch.cuda.stream(self.up):
+                for k, h in c.host_in.items():
+                    c.dev_in[k].copy_(h, non_blocking=True)
+                e = torch.cuda.Event()
+                e.record(self.up)
+                ev_up.append(e)
+        for c, e in zip(self.chunks, ev_up):                        # 2. replay + compaction per chunk
+            self.comp.wait_event(e)
+            with torch.cuda.stream(self.comp):
+                T = c.db.tensors
+                for k in ("exec", "scratch"):
+                    T[k].zero_()
+                for name, *_ in abi.TABLES:
+                    T["out_" + name].zero_()
+                eng.launch(c.db, self.comp)
+                eng.compact(c.db, self.comp)
+                n = c.batch.n_wf
+                c.host_tot.copy_(T["cmp_offsets"].view(len(COMPACT_TABLES), n + 1)[:, n], non_blocking=True)
+                et = torch.cuda.Event()
+                et.record(self.comp)
+                ev_tot.append(et)
+        d2h = 0
+        for c, et in zip(self.chunks, ev_tot):                      # 3. exact-size downloads
+            et.synchronize()
+            c.totals = c.host_tot.numpy().copy()
+            self.down.wait_event(et)
+            with torch.cuda.stream(self.down):
+                T = c.db.tensors
+                n = c.batch.n_wf
+                c.host_exec.copy_(T["exec"][:n * abi.EXEC_ROW.itemsize], non_blocking=True)
+                c.host_off.copy_(T["cmp_offsets"], non_blocking=True)
+                d2h += n * abi.EXEC_ROW.itemsize + c.host_off.numel() * 8
+                for t, (name, dt, *_) in enumerate(abi.TABLES):
+                    nb = int(c.totals[t]) * dt.itemsize
+                    if nb:
+                        c.host_rows[name][:nb].copy_(T["cmp_" + name][:nb], non_blocking=True)
+                        d2h += nb
+        self.down.synchronize()
+        wall = time.perf_counter() - t0
+        return {"wall_s": wall, "events": self.n_events, "events_per_s": self.n_events / wall,
+                "h2d_bytes": self.h2d_bytes, "d2h_bytes": int(d2h), "chunks": len(self.chunks)}
+
+    def results(self) -> List[CompactResult]:
+        out = []
+        for c in self.chunks:
+            n = c.batch.n_wf
+            off = c.host_off.numpy().reshape(len(COMPACT_TABLES), n + 1).copy()
+            rows = {}
+            for t, (name, dt, *_) in enumerate(abi.TABLES):
+                rows[name] = c.host_rows[name][:int(off[t, n]) * dt.itemsize].numpy().view(dt).copy()
+            out.append(CompactResult(c.host_exec.numpy().view(abi.EXEC_ROW).copy(), off, rows))
+        return out

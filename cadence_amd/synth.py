@@ -71,10 +71,50 @@ def activity_chain_template(k: int):
     return np.array(types, np.uint8), np.array(flags, np.uint8)
 
 
+class _CounterDraws:
+    """Per-workflow random draws: value j of stream s for workflow w is a hash of (seed, w, s, j), so a
+    workflow is the same whichever subset of a workload is generated (shard partitions)."""
+
+    def __init__(self, seed: int, wf_ids: np.ndarray):
+        from .dist import mix64
+        self.mix = mix64
+        self.seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+        self.ids = np.asarray(wf_ids, np.uint64)
+        self.stream = 0
+
+    def _u64(self, m: int) -> np.ndarray:
+        self.stream += 1
+        with np.errstate(over="ignore"):
+            x = (self.ids[:, None] * np.uint64(0x9E3779B97F4A7C15) + self.seed
+                 + np.uint64(self.stream) * np.uint64(0xD1B54A32D192ED03)
+                 + np.arange(m, dtype=np.uint64)[None, :] * np.uint64(0xA0761D6478BD642F))
+        return self.mix(self.mix(x))
+
+    def integers(self, lo: int, hi: int, size, dtype=np.int64):
+        """size = (n_wf, m) or n_wf * m (workflow-major)."""
+        n = self.ids.size
+        m = (size[1] if isinstance(size, tuple) else int(size) // max(n, 1))
+        v = (self._u64(m) % np.uint64(hi - lo)).astype(np.int64) + lo
+        return (v if isinstance(size, tuple) else v.reshape(-1)).astype(dtype)
+
+    def random(self, size) -> np.ndarray:
+        n = self.ids.size
+        m = int(size) // max(n, 1)
+        return ((self._u64(m) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))).reshape(-1)
+
+
 def activity_chain(n_wf: int, k: int, seed: int, version: int = 1, with_keys: bool = True,
-                   now_ns: int = BASE_TS + 10 ** 15) -> HistoryBatch:
-    """Config 1/2 workload: n_wf activity-chain workflows with k activities each (canonical layout)."""
-    rng = np.random.default_rng(seed)
+                   now_ns: int = BASE_TS + 10 ** 15, wf_ids=None) -> HistoryBatch:
+    """Config 1/2 workload: n_wf activity-chain workflows with k activities each (canonical layout).
+    ``wf_ids``: the workflows' indices in a larger workload (shard partitions, dist.rank_workflows); their
+    draws then depend only on (seed, index), so every rank generates exactly its part of one workload."""
+    if wf_ids is not None:
+        wf_ids = np.asarray(wf_ids, np.int64)
+        assert wf_ids.size == n_wf
+        rng = _CounterDraws(seed, wf_ids)
+    else:
+        wf_ids = np.arange(n_wf, dtype=np.int64)
+        rng = np.random.default_rng(seed)
     types, flags = activity_chain_template(k)
     L = types.size
     N = n_wf * L
@@ -87,9 +127,9 @@ def activity_chain(n_wf: int, k: int, seed: int, version: int = 1, with_keys: bo
     # timestamps: start = BASE + wf * 1s, deltas U[1 ms, 10 s]
     deltas = rng.integers(1_000_000, 10_000_000_000, size=(n_wf, L), dtype=np.int64)
     deltas[:, 0] = 0
-    ts = np.cumsum(deltas, axis=1) + (BASE_TS + np.arange(n_wf, dtype=np.int64) * 1_000_000_000)[:, None]
+    ts = np.cumsum(deltas, axis=1) + (BASE_TS + wf_ids * 1_000_000_000)[:, None]
     cols["timestamp"] = ts.reshape(-1)
-    cols["task_id"] = (np.arange(N, dtype=np.int64) + 1_000_000)
+    cols["task_id"] = ((wf_ids[:, None] * L + np.arange(L, dtype=np.int64)[None, :]).reshape(-1) + 1_000_000)
     ref = np.zeros((n_wf, L), np.int64)
     aux = np.zeros((n_wf, L), np.int32)
     key = np.zeros((n_wf, L), np.uint32)

@@ -24,7 +24,9 @@ class CSynthParams(ctypes.Structure):
                 ("invalid_rate", ctypes.c_double), ("can_rate", ctypes.c_double),
                 ("unknown_domain_rate", ctypes.c_double),
                 ("min_len", ctypes.c_int32), ("max_len", ctypes.c_int32), ("run_cap", ctypes.c_int32),
-                ("caps", ctypes.c_int32 * 5), ("alpha", ctypes.c_double)]
+                ("caps", ctypes.c_int32 * 5), ("alpha", ctypes.c_double),
+                ("num_shards", ctypes.c_uint32), ("world", ctypes.c_uint32), ("rank", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 def _run(p: CSynthParams, n_threads: int) -> HistoryBatch:
@@ -37,19 +39,38 @@ def _run(p: CSynthParams, n_threads: int) -> HistoryBatch:
 
 
 def mixed(n: int, seed: int = SEED_C3, mean_len: int = 40, multi_version: bool = False, invalid_rate: float = 0.0,
-          can_rate: float = 0.0, unknown_domain_rate: float = 0.0, n_threads: int = 0) -> HistoryBatch:
-    """n mixed random-walk workflows (configs 3 / 5); defaults: every history valid."""
+          can_rate: float = 0.0, unknown_domain_rate: float = 0.0, n_threads: int = 0, shard=None) -> HistoryBatch:
+    """n mixed random-walk workflows (configs 3 / 5); defaults: every history valid.  ``shard`` =
+    (num_shards, world, rank): only this rank's shards of the n-workflow workload."""
     p = CSynthParams(kind=0, n=n, seed=seed, mean_len=mean_len, multi_version=int(multi_version),
                      invalid_rate=invalid_rate, can_rate=can_rate, unknown_domain_rate=unknown_domain_rate)
+    _set_shard(p, shard)
     return _run(p, n_threads)
+
+
+def _set_shard(p: CSynthParams, shard):
+    if shard is not None:
+        p.num_shards, p.world, p.rank = (int(x) for x in shard)
+
+
+def shard_of(w, num_shards: int):
+    """crr_synth_shard_of over an array of workflow indices (the generator's own function)."""
+    import numpy as np
+    L = decode.lib()
+    f = L.crr_synth_shard_of
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint64, ctypes.c_uint32]
+    return np.array([f(int(x), int(num_shards)) for x in np.asarray(w).ravel()], np.int64)
 
 
 def long_tail(n: int, seed: int = SEED_C4, max_len: int = 50_000, run_cap: int = 10_000, min_len: int = 10,
               alpha: float = 1.2, multi_version: bool = False, invalid_rate: float = 0.0, caps=LONG_TAIL_CAPS,
-              n_threads: int = 0) -> HistoryBatch:
-    """n logical long-tail workflows (config 4): Zipf lengths up to max_len, continue-as-new every run_cap."""
+              n_threads: int = 0, shard=None) -> HistoryBatch:
+    """n logical long-tail workflows (config 4): Zipf lengths up to max_len, continue-as-new every run_cap.
+    ``shard``: as in ``mixed`` (by logical workflow: its continue-as-new runs share its workflow ID)."""
     p = CSynthParams(kind=1, n=n, seed=seed, multi_version=int(multi_version), invalid_rate=invalid_rate,
                      min_len=min_len, max_len=max_len, run_cap=run_cap, alpha=alpha)
+    _set_shard(p, shard)
     for i, c in enumerate(caps or (0, 0, 0, 0, 0)):
         p.caps[i] = c
     return _run(p, n_threads)

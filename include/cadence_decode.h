@@ -101,7 +101,15 @@ typedef struct crr_synth_params {
     int32_t  min_len, max_len, run_cap;   /* long tail */
     int32_t  caps[5];              /* concurrently pending activity / timer / child / rc / signal caps (<= 0: none) */
     double   alpha;                /* long tail: Zipf exponent */
+    /* shard partition of one global workload: with num_shards > 0 and world > 1 only the (logical)
+     * workflows w with crr_synth_shard_of(w, num_shards) % world == rank are generated, each exactly as
+     * in the whole workload (per-workflow seeded); continue-as-new runs stay with their workflow */
+    uint32_t num_shards, world, rank, reserved;
 } crr_synth_params;
+
+/* History shard of synthetic workflow w (stand-in for common/util.go:313-316 WorkflowIDToHistoryShard:
+ * farm.Fingerprint32(workflowID) % numberOfShards; here a SplitMix64 finalizer of the workflow index). */
+uint32_t crr_synth_shard_of(uint64_t w, uint32_t num_shards);
 
 crr_decoded* crr_synth_histories(const crr_synth_params* params, int n_threads, int* err);
 

@@ -543,6 +543,24 @@ float crr_last_kernel_ms(int which);
 int crr_timing_begin(void);
 int crr_timing_read(float* ms, int cap);
 
+/* ---- live-row compaction for the download --------------------------------------------------------
+ * After crr_replay (same inputs / outputs, same stream): every workflow's live rows -- slots 0..n-1 of
+ * its slot-table regions, n = its exec-row count clamped to [0, capacity] -- gathered into dense
+ * per-table buffers in workflow (batch) order, with each table's exclusive prefix over workflows, so a
+ * caller copies to the host only the rows it persists.  Replaces the persisted-snapshot walk over the
+ * pending maps (mutableStateBuilder.CloseTransactionAsSnapshot, mutable_state_builder.go:4033-4100).
+ * Tables: 0 activity, 1 timer, 2 child, 3 request-cancel, 4 signal, 5 version-history items,
+ * 6 reset points, 7 tasks (CRR_IN_EMIT_TASKS only).  rows[t] NULL: table t only counted.
+ * Returns 0 on successful launch, -1 on an invalid argument, else the hipError_t. */
+#define CRR_COMPACT_TABLES 8
+typedef struct crr_compact_out {
+    void*    rows[CRR_COMPACT_TABLES];  /* device, 8-byte aligned, >= the table's total live rows each */
+    int64_t* offsets;                   /* device [CRR_COMPACT_TABLES][n_wf + 1]; [t][n_wf] = the total */
+    void*    scratch;                   /* device, crr_compact_scratch_bytes(n_wf) bytes */
+} crr_compact_out;
+size_t crr_compact_scratch_bytes(uint32_t n_wf);
+int crr_compact_rows(const crr_inputs* in, const crr_outputs* out, const crr_compact_out* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

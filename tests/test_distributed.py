@@ -28,8 +28,10 @@ def _worker(rank, world, port, q):
     shard_of = np.repeat(np.arange(n_shards), per)
     mine = cdist.workflow_mask(shard_of, rank, world)
     res = oracle.replay(batch, 1)
-    local = cdist.digest_numpy(res.exec[mine])
-    t = torch.from_numpy(local.copy())
+    # the digest code the GPU ranks run (dist.digest_torch over the raw exec-row bytes), here on CPU tensors
+    raw = torch.from_numpy(np.ascontiguousarray(res.exec[mine]).view(np.uint8).reshape(-1).copy())
+    t = cdist.digest_torch(torch, raw, int(mine.sum()))
+    assert (t.numpy() == cdist.digest_numpy(res.exec[mine])).all()
     cdist.all_reduce_digest(torch, dist, t)
     q.put((rank, t.numpy().tolist(), cdist.digest_numpy(res.exec).tolist()))
     dist.destroy_process_group()
@@ -51,6 +53,29 @@ def test_two_rank_shard_partition_and_digest_reduce():
     assert reduced[0] == reduced[1]
     assert reduced[0] == out[0][2]       # sum over disjoint shards == digest of the whole batch
     assert reduced[0][1] == 64 * 8        # every workflow replayed exactly once
+
+
+def test_rank_workflows_partition_one_workload():
+    """bench.py's N-rank split of one global workload: disjoint, complete, shard-consistent, and each
+    rank's generated part equals the same workflows of the whole (per-workflow seeded draws)."""
+    from cadence_amd import synth_native
+    n, world = 4000, 4
+    parts = [cdist.rank_workflows(n, r, world) for r in range(world)]
+    allw = np.sort(np.concatenate(parts))
+    assert (allw == np.arange(n)).all()
+    sh = cdist.synthetic_shard_ids(np.arange(n))
+    for r, p in enumerate(parts):
+        assert (sh[p] % world == r).all()
+    assert (synth_native.shard_of(np.arange(500), cdist.NUM_SHARDS) == sh[:500]).all()
+    whole = synth.activity_chain(n, 2, synth.SEED_C2, wf_ids=np.arange(n), with_keys=False)
+    part = synth.activity_chain(parts[1].size, 2, synth.SEED_C2, wf_ids=parts[1], with_keys=False)
+    L = 17
+    for c in ("event_id", "timestamp", "task_id", "ref", "key", "etype", "version"):
+        assert (whole.cols[c].reshape(n, L)[parts[1]] == part.cols[c].reshape(-1, L)).all(), c
+    # native generator: the rank's shards of the mixed workload, event for event
+    tot = synth_native.mixed(2000)
+    ps = [synth_native.mixed(2000, shard=(cdist.NUM_SHARDS, 2, r)) for r in range(2)]
+    assert sum(p.n_wf for p in ps) == tot.n_wf and sum(p.n_events for p in ps) == tot.n_events
 
 
 def test_shards_for_rank_partition():

@@ -1,12 +1,22 @@
 """Benchmark: history events replayed/s (+ workflows rebuilt/s, % of HBM peak) on MI355X.
 
-One step = one crr_replay launch over this rank's whole shard of workflows (config 2 shape:
-activity-chain histories of 29 events, 1M workflows per GPU), inputs resident in HBM, followed
-(N > 1) by the job's one exchange: an RCCL all-reduce of counters and the checksum digest.
-Weak scaling: every rank replays its own shard (shards = disjoint workflow sets, as Cadence
-partitions workflows by shardID); value = events of all ranks / max-over-ranks wall time.
+Headline (``value``): BASELINE config 2 -- activity-chain histories of 29 events, 1M workflows per
+GPU, inputs resident in HBM; one step = one crr_replay over this rank's shard (every workflow
+rebuilt from scratch, checksum included), followed (N > 1) by the job's one exchange, an RCCL
+all-reduce of the counters + checksum digest.  N ranks split ONE global workload (N x 1M workflows)
+by history shard (dist.rank_workflows: shard = hash(workflow) mod 16384, shard -> rank = shard mod N),
+so per-GPU work is fixed (weak scaling); value = events of all ranks / max-over-ranks wall time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Beside it, on every rank with the same shard split and timing rules (``configs``):
+  config 3 -- 1.25M mixed histories per GPU (the per-GPU shard of the 10M x 8-GPU job),
+  config 4 -- long-tail histories (Zipf lengths up to 50k events, continue-as-new every 10k),
+  passive replication -- the last batch of every config-3 history applied onto its loaded state,
+each with its roofline and a bit-exact parity check against the oracle on a sample; and on rank 0 at
+N=1: the end-to-end figure from host buffers (pinned, chunked, overlapped, compacted download), the
+host-ingest rates (native decoder, flatten) and the CPU baseline (oracle on the host cores, config 2
+sample and BASELINE config 1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--headline-only]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -24,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
+MAX_TIMED_STEPS = 512   # crr_timing ring size (capi.hip kRing)
 
 
 def parse():
@@ -31,183 +42,398 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workflows", type=int, default=1_000_000, help="workflows per GPU (config 2: 1M)")
+    p.add_argument("--workflows", type=int, default=1_000_000, help="config 2 workflows per GPU (1M)")
     p.add_argument("--activities", type=int, default=4, help="activities per workflow (k=4 -> 29 events)")
+    p.add_argument("--headline-only", action="store_true", help="config 2 only (no configs 3/4, e2e, CPU)")
+    p.add_argument("--config-steps", type=int, default=5, help="timed steps of the config 3 / 4 / replication lines")
+    p.add_argument("--c3-workflows", type=int, default=1_250_000, help="config 3 mixed workflows per GPU")
+    p.add_argument("--c4-workflows", type=int, default=2000, help="config 4 logical workflows per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=0, help="threads for the CPU baseline (0: os cpu share)")
-    p.add_argument("--cpu-sample", type=int, default=1_000_000, help="workflows in the CPU baseline sample")
-    p.add_argument("--cpu-seconds", type=float, default=2.0,
-                   help="minimum wall seconds of CPU-baseline replay (x threads = CPU seconds; 2 s x 16 = 32)")
-    return p.parse_args()
+    p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the CPUs this process may use)")
+    p.add_argument("--cpu-sample", type=int, default=1_000_000, help="config 2 workflows in the CPU baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall seconds per CPU-baseline figure")
+    a = p.parse_args()
+    if a.steps > MAX_TIMED_STEPS or a.config_steps > MAX_TIMED_STEPS:
+        p.error(f"--steps / --config-steps: at most {MAX_TIMED_STEPS} launches are timed per region")
+    if a.steps < 1:
+        p.error("--steps must be >= 1")
+    return a
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    import torch.distributed as dist
+def host_cpus() -> int:
+    """CPUs this process may run on: the cgroup CPU quota when one is set (the GPU box's per-GPU share),
+    else the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
 
+
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.args = args
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local_rank)
+        if self.world > 1:
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", self.local_rank))
+        from cadence_amd.engine import ReplayEngine
+        self.eng = ReplayEngine(self.local_rank)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def reduce(self, values, op="max"):
+        """All-reduce a list of floats over the ranks (identity at N=1)."""
+        t = self.torch.tensor(values, dtype=self.torch.float64, device="cuda")
+        if self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return [float(x) for x in t.cpu()]
+
+
+def timed_steps(ctx, db, steps, warmup, per_step=None, before_step=None):
+    """warmup, barrier + sync, K launches (HIP-event ring around each launch's fast group), sync +
+    barrier; returns (max-over-ranks wall seconds, per-launch fast-group ms)."""
+    torch, eng = ctx.torch, ctx.eng
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        if before_step:
+            before_step()
+        eng.launch(db, stream)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    eng.timing_begin()
+    wall = 0.0
+    if before_step is None:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.launch(db, stream)
+            if per_step:
+                per_step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        wall = time.perf_counter() - t0
+    else:
+        # each step restores its input state first (device copy, synchronised, outside the clock)
+        for _ in range(steps):
+            before_step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.launch(db, stream)
+            torch.cuda.synchronize()
+            wall += time.perf_counter() - t0
+        ctx.barrier()
+    ms = eng.timing_read()
+    if len(ms) != steps:
+        raise RuntimeError(f"timed {len(ms)} kernel launches, expected {steps}")
+    return ctx.reduce([wall])[0], ms
+
+
+def roofline(alg_bytes, kernel_ms, kernel, traffic=None):
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": kernel, "kernel_ms": kernel_ms, "algorithmic_bytes_per_launch": int(alg_bytes)}
+    if traffic:
+        r["traffic_GBs"] = traffic / (kernel_ms * 1e-3) / 1e9
+        r["traffic_frac"] = r["traffic_GBs"] / HBM_PEAK_GBS
+    return r
+
+
+# ---- config 2 (headline) -------------------------------------------------------------------------------
+def config2(ctx):
+    from cadence_amd import abi, synth
     from cadence_amd import dist as cdist
-    from cadence_amd import synth
-    from cadence_amd.engine import ReplayEngine
     from cadence_amd.flatten import interleave
-
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local_rank))
-    eng = ReplayEngine(local_rank)
-
+    args, torch, eng = ctx.args, ctx.torch, ctx.eng
     k = args.activities
-    n_wf = args.workflows
     t0 = time.time()
-    canon = synth.activity_chain(n_wf, k, synth.SEED_C2 + rank, with_keys=False)
+    ids = cdist.rank_workflows(args.workflows * ctx.world, ctx.rank, ctx.world)
+    canon = synth.activity_chain(ids.size, k, synth.SEED_C2, with_keys=False, wf_ids=ids)
     batch = interleave(canon)
     db = eng.upload(batch)
-    gen_s = time.time() - t0
-    n_events = batch.n_events
-    stream = torch.cuda.current_stream()
+    setup_s = time.time() - t0
+    n_wf, n_events = batch.n_wf, batch.n_events
 
-    for _ in range(args.warmup):
-        eng.launch(db, stream)
-    torch.cuda.synchronize()
+    def exchange():
+        d = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
+        cdist.all_reduce_digest(torch, ctx.dist, d)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    eng.timing_begin()          # per-launch HIP events around the dominant kernel, on the launch stream
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        eng.launch(db, stream)
-        if world > 1:
-            d = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
-            cdist.all_reduce_digest(torch, dist, d)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    ms = eng.timing_read()
-    if len(ms) != args.steps:
-        raise RuntimeError(f"timed {len(ms)} kernel launches, expected {args.steps}")
+    wall, ms = timed_steps(ctx, db, args.steps, args.warmup, per_step=exchange if ctx.world > 1 else None)
     kernel_avg_ms = float(np.mean(ms))
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
-
+    digest = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
+    if ctx.world > 1:
+        cdist.all_reduce_digest(torch, ctx.dist, digest)
+    digest = digest.cpu().numpy()
+    tot_events, tot_wf = ctx.reduce([float(n_events), float(n_wf)], op="sum")
     res = eng.download(db)
-    from cadence_amd import abi
     tier = "replay_lds_small_kernel" if db.c_in.flags & abi.IN_LDS_SMALL else "replay_lds_kernel"
     tail = bool(db.c_in.flags & abi.IN_WAVE_TAIL) and db.c_in.wave_begin < db.n_wf
     emit = bool(db.c_in.flags & abi.IN_EMIT_TASKS)
     kernel_name = f"{tier}<{str(tail).lower()}, {str(emit).lower()}>"  # <WAVE_TAIL, EMIT>, as rocprofv3 names it
-    ok = bool((res.exec["status"] == 0).all())
     alg_bytes = synth.algorithmic_bytes(batch, res)
-    achieved_gbs = alg_bytes / (kernel_avg_ms * 1e-3) / 1e9
-
-    total_events = n_events * world * args.steps
-    value = total_events / elapsed_max
-    line = {
-        "metric": "history events replayed/sec (node) + workflows rebuilt/sec; % HBM peak",
-        "value": value,
-        "unit": "events/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed_max / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "int64",
-        "data": "synthetic",
-        "config": {"workload": "config 2: activity-chain histories (schedule/start/complete + decisions), "
-                               f"{k} activities = {n_events // n_wf} events/workflow, {n_wf} workflows per GPU, "
-                               "wave-interleaved SoA resident in HBM",
-                   "workflows_per_gpu": n_wf, "events_per_workflow": n_events // n_wf,
-                   "parallelism": f"shard-partitioned x{world} (RCCL all-reduce of counters + checksum digest)"},
-        "workflows_per_s": n_wf * world * args.steps / elapsed_max,
-        "all_ok": ok,
-        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": kernel_name, "kernel_ms": kernel_avg_ms,
-                     "algorithmic_bytes_per_launch": alg_bytes},
-        "setup_s": gen_s,
-    }
+    traffic = None
     if os.path.exists(PROFILE_TRAFFIC):
         try:
             tr = json.load(open(PROFILE_TRAFFIC))
             if (tr.get("workflows") == n_wf and tr.get("events_per_workflow") == n_events // n_wf
                     and tr.get("kernel") == kernel_name):
-                line["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
-        except Exception:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             pass
-
-    if rank == 0 and world == 1:
-        line["pcie_inclusive"] = pcie_inclusive(eng, batch, torch)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args, res, batch, k)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def pcie_inclusive(eng, batch, torch, reps=3):
-    """SURVEY.md §8d's second figure: one replay with host buffers -- device allocation + H2D of the
-    columns, side records and descriptors, the replay, D2H of the execution rows and the slot
-    tables -- never the headline `value` (which has the inputs resident in HBM)."""
-    times, parts = [], []
-    for _ in range(reps):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        db = eng.upload(batch)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        eng.launch(db)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        r = eng.download(db)
-        torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        times.append(t3 - t0)
-        parts.append((t1 - t0, t2 - t1, t3 - t2))
-        del db, r
-    t = float(np.median(times))
-    up, run, down = (float(np.median([p[i] for p in parts])) * 1e3 for i in range(3))
-    h2d = sum(v.nbytes for v in batch.cols.values()) + batch.act_side.nbytes + batch.start_side.nbytes \
-        + batch.arena.nbytes + batch.wf.nbytes
-    return {"events_per_s": batch.n_events / t, "ms": t * 1e3, "h2d_bytes": int(h2d),
-            "upload_ms": up, "replay_ms": run, "download_ms": down,
-            "note": "pageable host buffers, allocation + upload + replay + download of exec rows and slot tables"}
+    line = {
+        "metric": "history events replayed/sec (node) + workflows rebuilt/sec; % HBM peak",
+        "value": tot_events * args.steps / wall,
+        "unit": "events/s",
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded activity-chain histories, per-workflow draws)",
+        "config": {"workload": "config 2: activity-chain histories (schedule/start/complete + decisions), "
+                               f"{k} activities = {n_events // n_wf} events/workflow, {args.workflows} workflows per GPU "
+                               f"(one {args.workflows * ctx.world}-workflow workload split by history shard), "
+                               "wave-interleaved SoA resident in HBM",
+                   "workflows_per_gpu": n_wf, "events_per_workflow": n_events // n_wf,
+                   "parallelism": f"shard-partitioned x{ctx.world} (RCCL all-reduce of counters + checksum digest)"},
+        "workflows_per_s": tot_wf * args.steps / wall,
+        "all_ok": bool(digest[2] == 0 and digest[1] == tot_wf),
+        "digest": [int(x) for x in digest],
+        "roofline": roofline(alg_bytes, kernel_avg_ms, kernel_name, traffic),
+        "setup_s": setup_s,
+    }
+    return line, batch, res, db
 
 
-def cpu_baseline(args, gpu_res, gpu_batch, k):
-    """The oracle (C++ restatement of the Go stateBuilder, per-workflow hash maps) on host cores,
-    over a bounded sample of the same workload; also checks the GPU rows against it."""
+# ---- configs 3 / 4 and passive replication ----------------------------------------------------------
+FAST_GROUP = "crr_replay phase-1 launch group (tier kernels on side streams, fork to join)"
+
+
+def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
+    """One non-headline line: generate this rank's shard, time `config_steps` replays, roofline over the
+    launch group, parity of a sample against the oracle (rank 0)."""
+    from cadence_amd import synth
+    from cadence_amd import dist as cdist
+    from cadence_amd.flatten import interleave
+    args, torch, eng = ctx.args, ctx.torch, ctx.eng
+    t0 = time.time()
+    canon = make_canon()
+    t1 = time.time()
+    batch = interleave(canon, long_threshold=long_threshold)
+    t2 = time.time()
+    db = eng.upload(batch)
+    wall, ms = timed_steps(ctx, db, args.config_steps, 1)
+    res = eng.download(db)
+    digest = cdist.digest_numpy(res.exec)
+    tot_events, tot_wf, tot_ok = ctx.reduce([float(batch.n_events), float(batch.n_wf), float(digest[1])], op="sum")
+    grp_ms = float(np.mean(ms))
+    out = {"workload": workload, "value": tot_events * args.config_steps / wall, "unit": "events/s",
+           "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
+           "workflows_per_gpu": batch.n_wf, "events_per_gpu": batch.n_events, "workflows_ok": int(tot_ok),
+           "workflows_per_s": tot_wf * args.config_steps / wall,
+           "tiers": list(batch.tiers) if batch.tiers else None, "wave_tail": batch.n_wf - (batch.wave_begin or batch.n_wf),
+           "roofline": roofline(synth.algorithmic_bytes(batch, res), grp_ms, FAST_GROUP),
+           "setup_s": {"generate": t1 - t0, "interleave": t2 - t1}}
+    if ctx.rank == 0:
+        out["parity_sample"] = parity_sample(ctx, sample_fn, long_threshold)
+    return out, batch, res, db
+
+
+def parity_sample(ctx, sample_fn, long_threshold):
+    from oracle import oracle
+    from cadence_amd.flatten import interleave
+    from cadence_amd.result import diff_results
+    canon = sample_fn()
+    b = interleave(canon, long_threshold=long_threshold)
+    gpu = ctx.eng.replay(b)
+    t0 = time.perf_counter()
+    ref = oracle.replay(canon, host_cpus())
+    dt = time.perf_counter() - t0
+    d = diff_results(b, gpu, canon, ref)
+    return {"workflows": canon.n_wf, "events": canon.n_events, "bit_exact": not d, "first_diffs": d[:3],
+            "oracle_s": dt, "ok": int((gpu.exec["status"] == 0).sum())}
+
+
+def passive_replication(ctx, batch, one_shot):
+    from cadence_amd.replication import PassiveReplication
+    args, eng = ctx.args, ctx.eng
+    pr = PassiveReplication(eng, batch)
+    pr.setup()
+    wall, ms = timed_steps(ctx, pr.db_new, args.config_steps, 1, before_step=pr.restore)
+    v = pr.verify(one_shot)
+    tot_ev, tot_tasks = ctx.reduce([float(pr.n_events), float(v["split_workflows"])], op="sum")
+    out = {"workload": "config 3 shard: the last event batch of every history applied onto its loaded mutable state "
+                       "(ndc/history_replicator.go:385-460 -> StateBuilder.ApplyEvents on a Load-ed state), rows in HBM",
+           "value": tot_ev * args.config_steps / wall, "unit": "events/s",
+           "replication_tasks_per_s": tot_tasks * args.config_steps / wall,
+           "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
+           "events_per_gpu": pr.n_events, "tasks_per_gpu": v["split_workflows"],
+           "vs_one_shot": v,
+           "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP)}
+    del pr
+    return out
+
+
+def _resume_bytes(pr):
+    """Algorithmic bytes of one replication step: the new events' columns, the descriptor, the loaded
+    exec row read and written, the loaded + final live rows (read, then written back), the token."""
+    from cadence_amd import abi
+    b = pr.batch
+    ex = pr.prefix.exec
+    rows = (112 * ex["n_activity"].astype(np.int64).sum() + 40 * ex["n_timer"].astype(np.int64).sum()
+            + 48 * ex["n_child"].astype(np.int64).sum() + 32 * (ex["n_rc"].astype(np.int64).sum() + ex["n_signal"].astype(np.int64).sum())
+            + 16 * ex["n_vh_items"].astype(np.int64).sum() + 16 * ex["n_reset_points"].astype(np.int64).sum())
+    return int(pr.n_events * abi.BYTES_PER_EVENT + b.n_wf * (abi.WORKFLOW.itemsize + 2 * abi.EXEC_ROW.itemsize + 96) + 2 * rows)
+
+
+# ---- rank 0, N = 1: end to end, host ingest, CPU baseline ---------------------------------------------------
+def end_to_end(ctx, n_wf, k, chunks=8):
+    """Config 2 from host buffers: pinned staging, `chunks` chunks overlapped on three streams, live rows
+    compacted on the device; checked against the HBM-resident digest of the same workflows."""
+    from cadence_amd import dist as cdist
+    from cadence_amd import synth
+    from cadence_amd.flatten import interleave
+    from cadence_amd.pipeline import StreamingReplay
+    bounds = np.linspace(0, n_wf, chunks + 1).astype(np.int64)
+    t0 = time.time()
+    parts = [interleave(synth.activity_chain(int(b - a), k, synth.SEED_C2, with_keys=False, wf_ids=np.arange(a, b)))
+             for a, b in zip(bounds[:-1], bounds[1:])]
+    sr = StreamingReplay(ctx.eng, parts)
+    setup = time.time() - t0
+    sr.run()                                     # warm
+    runs = [sr.run() for _ in range(3)]
+    best = min(runs, key=lambda r: r["wall_s"])
+    med = float(np.median([r["wall_s"] for r in runs]))
+    digest = np.zeros(6, np.int64)
+    for cr in sr.results():
+        digest += cdist.digest_numpy(cr.exec)
+    out = {"events_per_s": best["events"] / med, "ms": med * 1e3, "events": best["events"], "chunks": chunks,
+           "h2d_bytes": best["h2d_bytes"], "d2h_bytes": best["d2h_bytes"],
+           "h2d_GBs": best["h2d_bytes"] / med / 1e9, "setup_s": setup, "digest": [int(x) for x in digest],
+           "note": "host columns in pinned staging buffers (where the decoder writes them); per chunk: H2D, output "
+                   "zero-fill, replay, crr_compact_rows, D2H of the exec rows + the live rows only; three streams "
+                   "overlap chunks; median of 3 passes"}
+    del sr
+    return out
+
+
+def host_ingest(ctx, flatten_s, flatten_events):
+    """Host-side rates that feed the engine: the native thriftrw decoder (crr_decode_histories, all host
+    CPUs) over encoded mixed histories, and the numpy interleave of the config-2 batch."""
+    from cadence_amd import synth_mixed
+    from cadence_amd.decode import WorkflowSource, time_native_decode
+    from cadence_amd.thrift_codec import serialize_history
+    hs = synth_mixed.mixed_histories(3000, 0xCAD00005, mean_len=40)
+    src = [WorkflowSource(blobs=serialize_history(h), run_id=h.run_id, branch_id=h.branch_id, now_ns=h.now_ns,
+                          domain_failover_version=h.domain_failover_version) for h in hs]
+    dec = time_native_decode(src, {"domain-a", "domain-b", "parent-domain"}, n_threads=host_cpus(), min_seconds=1.0)
+    dec["threads"] = host_cpus()
+    return {"decode": dec, "interleave_config2": {"events_per_s": flatten_events / flatten_s, "seconds": flatten_s}}
+
+
+def cpu_baseline(ctx, gpu_res, gpu_batch, k):
+    """The oracle (C++ restatement of the Go stateBuilder, per-workflow hash maps, std::thread workers)
+    on this process's host CPUs: a bounded sample of config 2 (bit-compared with the GPU rows) and
+    BASELINE config 1 (10k activity chains of 23 events)."""
+    from oracle import oracle
     from cadence_amd import synth
     from cadence_amd.result import diff_results
-    from oracle import oracle
+    args = ctx.args
+    threads = args.cpu_threads or host_cpus()
+
+    def timed(batch):
+        passes, dt, res = 0, 0.0, None
+        while passes == 0 or dt < args.cpu_seconds:
+            t0 = time.perf_counter()
+            r = oracle.replay(batch, threads)
+            dt += time.perf_counter() - t0
+            res = res if res is not None else r
+            passes += 1
+        return passes, dt, res
+
     n = min(args.cpu_sample, args.workflows)
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    sample = synth.activity_chain(n, k, synth.SEED_C2, with_keys=True)
-    # repeat whole passes over the sample until >= cpu_seconds of wall time (bounded CPU work)
-    passes, dt, res = 0, 0.0, None
-    while passes == 0 or dt < args.cpu_seconds:
-        t0 = time.perf_counter()
-        r = oracle.replay(sample, threads)
-        dt += time.perf_counter() - t0
-        res = res if res is not None else r
-        passes += 1
+    sample = synth.activity_chain(n, k, synth.SEED_C2, with_keys=True, wf_ids=np.arange(n))
+    passes, dt, res = timed(sample)
     out = {"value": sample.n_events * passes / dt, "unit": "events/s", "cores": threads, "kind": "port",
-           "sample": f"{passes} pass(es) over {n} config-2 workflows ({sample.n_events} events), seed SEED_C2, "
-                     f"{threads} std::thread workers, CPU restatement of Go stateBuilder (reference not runnable)",
+           "host_cpus_visible": os.cpu_count(),
+           "sample": f"{passes} pass(es) over {n} config-2 workflows ({sample.n_events} events), {threads} std::thread "
+                     "workers (this process's CPU share), CPU restatement of the Go stateBuilder (reference not runnable)",
            "wall_s": dt, "cpu_seconds_approx": dt * threads}
-    if n == args.workflows:
-        d = diff_results(gpu_batch, gpu_res, sample, res)
-        out["gpu_parity_bit_exact"] = not d
+    if n == gpu_batch.n_wf:
+        out["gpu_parity_bit_exact"] = not diff_results(gpu_batch, gpu_res, sample, res)
+    c1 = synth.activity_chain(10_000, 3, synth.SEED_C1, with_keys=True)
+    p1, d1, _ = timed(c1)
+    out["config1"] = {"events_per_s": c1.n_events * p1 / d1, "workflows_per_s": c1.n_wf * p1 / d1,
+                      "workload": "BASELINE config 1: 10k activity-chain histories x 23 events", "passes": p1,
+                      "cores": threads}
     return out
+
+
+def main():
+    args = parse()
+    ctx = Ctx(args)
+    torch = ctx.torch
+    from cadence_amd import synth_native
+    from cadence_amd import dist as cdist
+    line, batch2, res2, db2 = config2(ctx)
+    if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
+        from cadence_amd.flatten import interleave
+        from cadence_amd import synth
+        canon = synth.activity_chain(200_000, args.activities, synth.SEED_C2, with_keys=False)
+        flat_t0 = time.perf_counter()
+        interleave(canon)
+        flat_s, flat_ev = time.perf_counter() - flat_t0, canon.n_events
+        del canon
+    del db2
+    torch.cuda.empty_cache()
+    if not args.headline_only:
+        shard = (cdist.NUM_SHARDS, ctx.world, ctx.rank)
+        n3 = args.c3_workflows * ctx.world
+        c3, b3, r3, db3 = run_config(
+            ctx, "config3", lambda: synth_native.mixed(n3, shard=shard),
+            f"config 3: {args.c3_workflows} mixed histories per GPU (timers, signals, child workflows, cancel requests; "
+            f"10..70 events), the rank's history shards of one {n3}-workflow workload",
+            lambda: synth_native.mixed(50_000, shard=shard))
+        del db3
+        torch.cuda.empty_cache()
+        pr = passive_replication(ctx, b3, r3)
+        del b3, r3
+        torch.cuda.empty_cache()
+        n4 = args.c4_workflows * ctx.world
+        c4, b4, r4, db4 = run_config(
+            ctx, "config4", lambda: synth_native.long_tail(n4, shard=shard),
+            f"config 4: {args.c4_workflows} long-tail workflows per GPU (Zipf lengths up to 50k events, continued as new "
+            "every 10k: each run a workflow, a CAN's new-run history its next run's first batch), lane per workflow up "
+            "to 256 events, a wavefront per longer run",
+            lambda: synth_native.long_tail(60, shard=shard))
+        del db4, b4, r4
+        torch.cuda.empty_cache()
+        line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr}
+    if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
+        line["pcie_inclusive"] = end_to_end(ctx, args.workflows, args.activities)
+        line["pcie_inclusive"]["matches_resident_digest"] = line["pcie_inclusive"]["digest"] == line["digest"]
+        line["host_ingest"] = host_ingest(ctx, flat_s, flat_ev)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(ctx, res2, batch2, args.activities)
+        if "pcie_inclusive" in line:
+            line["pcie_inclusive"]["vs_cpu_baseline"] = line["pcie_inclusive"]["events_per_s"] / line["cpu_baseline"]["value"]
+    if ctx.rank == 0:
+        print(json.dumps(line), flush=True)
+    if ctx.world > 1:
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -103,6 +103,45 @@ def _copy(ptr, n, dtype):
 def decode_histories(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable[str]] = None,
                      n_threads: int = 0) -> HistoryBatch:
     """Decode every workflow's blobs into one canonical HistoryBatch (raises DeserializationError)."""
+    L = lib()
+    args = _prepare(sources, known_domains)
+    return batch_from_handle(L, _decode_call(L, args, n_threads))
+
+
+def time_native_decode(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable[str]] = None,
+                       n_threads: int = 0, min_seconds: float = 1.0) -> dict:
+    """Wall time of crr_decode_histories alone (blobs already in native buffers, the Python argument
+    marshalling excluded), repeated for at least ``min_seconds``: the host-ingest decode rate."""
+    import time
+    L = lib()
+    args = _prepare(sources, known_domains)
+    n_ev, reps, dt = 0, 0, 0.0
+    while reps == 0 or dt < min_seconds:
+        t0 = time.perf_counter()
+        h = _decode_call(L, args, n_threads)
+        dt += time.perf_counter() - t0
+        if reps == 0:
+            v = CDecodedView()
+            L.crr_decoded_get_view(h, ctypes.byref(v))
+            n_ev = int(v.n_events)
+        L.crr_decoded_free(h)
+        reps += 1
+    blob_bytes = int(sum(args[1][i] for i in range(args[2])))
+    return {"events": n_ev, "workflows": len(sources), "blob_bytes": blob_bytes, "reps": reps,
+            "seconds_per_pass": dt / reps, "events_per_s": n_ev * reps / dt, "MB_per_s": blob_bytes * reps / dt / 1e6}
+
+
+def _decode_call(L, args, n_threads: int):
+    bptr, blen, nb, cw, n_src, kd, nk, _keep = args
+    err = ctypes.c_int(0)
+    err_blob = ctypes.c_int64(-1)
+    h = L.crr_decode_histories(bptr, blen, nb, cw, n_src, kd, nk, int(n_threads), ctypes.byref(err), ctypes.byref(err_blob))
+    if not h:
+        raise DeserializationError(err.value, err_blob.value)
+    return h
+
+
+def _prepare(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable[str]]):
     blobs: List[bytes] = []
     cw = (CWfSource * max(len(sources), 1))()
     keep = []
@@ -141,14 +180,7 @@ def decode_histories(sources: Sequence[WorkflowSource], known_domains: Optional[
         names = [n.encode() for n in known_domains]
         kd = (ctypes.c_char_p * max(len(names), 1))(*names)
         nk = len(names)
-    err = ctypes.c_int(0)
-    err_blob = ctypes.c_int64(-1)
-    L = lib()
-    h = L.crr_decode_histories(bptr, blen, nb, cw, len(sources), kd, nk, int(n_threads),
-                               ctypes.byref(err), ctypes.byref(err_blob))
-    if not h:
-        raise DeserializationError(err.value, err_blob.value)
-    return batch_from_handle(L, h)
+    return bptr, blen, nb, cw, len(sources), kd, nk, (keep, bufs)
 
 
 def batch_from_handle(L, h) -> HistoryBatch:

@@ -1,0 +1,203 @@
+"""Passive replication at scale: one new batch applied onto every workflow's loaded mutable state.
+
+The production hot path of ``ndc/history_replicator.go:385-460`` (call at :396): the state persisted
+after batches 1..k-1 is loaded (``mutableStateBuilder.Load``, mutable_state_builder.go:306-349) and
+``StateBuilder.ApplyEvents`` applies batch k onto it (state_builder.go:73-88, :90-648).  On the device
+the loaded state is the previous replay's output rows, left in place in HBM (slots 0..n-1 of each
+workflow's regions, exactly where ``write_init`` puts a state loaded from the host), so a replication
+step is one ``crr_replay`` over the new batch with CRR_WF_FLAG_RESUME.
+
+``PassiveReplication`` cuts every workflow of an interleaved batch before its last event batch: the
+prefix replays once from scratch (setup), the device output buffers are snapshotted, and each
+measured step restores the snapshot (device copy, outside the timed launch) and applies the last
+batches.  ``verify`` checks the result against the one-shot replay of the whole histories.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict
+
+import numpy as np
+
+from . import abi
+from .engine import DeviceBatch, ReplayEngine
+from .flatten import HistoryBatch
+from .result import ReplayResult, gather_live
+
+
+def last_batch_cut(batch: HistoryBatch) -> np.ndarray:
+    """Per workflow: the step at which its last event batch starts (0 for single-batch histories)."""
+    cnt = batch.wf["ev_count"].astype(np.int64)
+    st = batch.wf_strides()
+    tot = int(cnt.sum())
+    wf_idx = np.repeat(np.arange(batch.n_wf), cnt)
+    step = np.arange(tot) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    idx = batch.wf["ev_begin"].astype(np.int64)[wf_idx] + step * st[wf_idx]
+    first = (batch.cols["etype"][idx] & abi.BATCH_FIRST) != 0
+    cut = np.zeros(batch.n_wf, np.int64)
+    np.maximum.at(cut, wf_idx[first], step[first])
+    return cut
+
+
+def suffix_batch(batch: HistoryBatch, cut: np.ndarray, split: np.ndarray, suf_wf: np.ndarray) -> HistoryBatch:
+    """The new events alone, laid out as the host would upload them: every workflow's events from its
+    cut on, re-interleaved (lane workflows: group-uniform bases, 64-wide; the wave tail contiguous),
+    with the descriptors of ``suf_wf`` (table bases unchanged: the loaded rows stay where they are)."""
+    n = batch.n_wf
+    wave = batch.stride
+    n_lane = batch.wave_begin if batch.wave_begin is not None else n
+    st = batch.wf_strides()
+    cnt = np.where(split, batch.wf["ev_count"].astype(np.int64) - cut, 0)
+    n_groups = (n_lane + wave - 1) // wave
+    pos = np.arange(n_lane)
+    gcnt = np.zeros(n_groups * wave, np.int64)
+    gcnt[:n_lane] = cnt[:n_lane]
+    glen = gcnt.reshape(n_groups, wave).max(axis=1) if n_groups else np.zeros(0, np.int64)
+    gbase = np.concatenate([[0], np.cumsum(glen * wave)[:-1]]).astype(np.int64) if n_groups else glen
+    lane_slots = int((glen * wave).sum())
+    begin = np.empty(n, np.int64)
+    begin[:n_lane] = gbase[pos // wave] + pos % wave
+    tail = cnt[n_lane:]
+    begin[n_lane:] = lane_slots + np.concatenate([[0], np.cumsum(tail)[:-1]]).astype(np.int64)
+    nst = np.where(np.arange(n) < n_lane, wave, 1)
+    wf_idx = np.repeat(np.arange(n), cnt)
+    k = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    src = batch.wf["ev_begin"].astype(np.int64)[wf_idx] + (cut[wf_idx] + k) * st[wf_idx]
+    dst = begin[wf_idx] + k * nst[wf_idx]
+    total = lane_slots + int(tail.sum())
+    cols = {}
+    for name, t in abi.EVENT_COLUMNS:
+        c = np.zeros(max(total, 1), dtype=t)
+        if name == "etype":
+            c[:] = abi.EV_PAD | abi.BATCH_FIRST | abi.BATCH_LAST
+        c[dst] = batch.cols[name][src]
+        cols[name] = c
+    wf = suf_wf.copy()
+    wf["ev_begin"] = begin
+    wf["ev_count"] = cnt
+    out = dataclasses.replace(batch, cols=cols, wf=wf, init=None, table_rows=dict(batch.table_rows))
+    if batch.key_off is not None:
+        out.key_off = np.zeros(max(total, 1), np.uint32)
+        out.key_len = np.zeros(max(total, 1), np.uint32)
+        out.key_off[dst] = batch.key_off[src]
+        out.key_len[dst] = batch.key_len[src]
+    return out
+
+
+def split_descriptors(batch: HistoryBatch, cut: np.ndarray):
+    """(prefix wf, suffix wf, split mask) descriptor arrays over the same device layout (the suffix's
+    ev_begin still indexes the whole batch's columns: ``suffix_batch`` relays them out)."""
+    split = (cut > 0) & ((batch.wf["flags"] & abi.WF_FLAG_NEW_RUN) == 0)
+    pre = batch.wf.copy()
+    suf = batch.wf.copy()
+    st = batch.wf_strides()
+    c = np.where(split, cut, 0)
+    cnt = batch.wf["ev_count"].astype(np.int64)
+    ea = batch.wf["empty_batch_at"].astype(np.int64)
+    pre["ev_count"] = np.where(split, c, cnt)
+    pre["empty_batch_at"] = np.where(split & (ea >= c), -1, ea)
+    # the prefix is an intermediate state: no rebuild finalisation / task refresh yet
+    pre["final_token_len"] = np.where(split, abi.NO_TOKEN, pre["final_token_len"])
+    pre["flags"] = np.where(split, pre["flags"] & ~np.uint32(abi.WF_FLAG_REFRESH_TASKS), pre["flags"])
+    suf["ev_begin"] = batch.wf["ev_begin"] + np.where(split, c * st, 0)
+    suf["ev_count"] = np.where(split, cnt - c, 0)
+    suf["empty_batch_at"] = np.where(split, np.where(ea >= c, ea - c, -1), -1)
+    # every workflow resumes: a split one applies its last batch, the others apply nothing (their rows
+    # are re-finalised unchanged)
+    suf["flags"] = suf["flags"] | np.uint32(abi.WF_FLAG_RESUME)
+    return pre, suf, split
+
+
+@dataclasses.dataclass
+class PassiveReplication:
+    eng: ReplayEngine
+    batch: HistoryBatch                   # interleaved, from scratch
+    db: DeviceBatch = None                # the whole histories' layout: its output buffers hold the state
+    db_new: DeviceBatch = None            # the new batches (suffix events), writing into db's outputs
+    split: np.ndarray = None
+    prefix: ReplayResult = None
+    snapshot: Dict[str, object] = None
+    n_events: int = 0                     # events applied per step
+
+    def setup(self):
+        eng, torch, b = self.eng, self.eng.torch, self.batch
+        cut = last_batch_cut(b)
+        pre, suf, self.split = split_descriptors(b, cut)
+        db = eng.upload(b)
+        self.db = db
+        wf_dev = db.tensors["wf"]
+        nb = pre.nbytes
+        wf_dev[:nb].copy_(torch.from_numpy(pre.view(np.uint8)))
+        eng.launch(db)
+        torch.cuda.synchronize(eng.dev)
+        self.prefix = eng.download(db)
+        sb = suffix_batch(b, cut, self.split, suf)
+        self.n_events = sb.n_events
+        dn = eng.upload(sb)
+        dn.c_out = db.c_out                        # apply onto the loaded rows in place
+        # resumed workflows continue over HBM rows: every lane workflow in the wide (GlobalTables)
+        # segment, the long tail in the tail / big kernels (their HBM-row pass resumes)
+        if sb.tiers is not None:
+            dn.c_in.large_begin = dn.c_in.compact_begin = dn.c_in.compact2_begin = dn.c_in.wide_begin = 0
+            dn.c_in.flags &= ~abi.IN_LDS_SMALL
+        for name, *_ in abi.TABLES:                # only db's outputs are used
+            dn.tensors.pop("out_" + name, None)
+        dn.tensors.pop("exec", None)
+        self.db_new = dn
+        self.snapshot = {k: db.tensors[k].clone() for k in self._state_keys()}
+        torch.cuda.synchronize(eng.dev)
+
+    def _state_keys(self):
+        return ["exec"] + ["out_" + name for name, *_ in abi.TABLES]
+
+    def restore(self, stream=None):
+        torch = self.eng.torch
+        s = stream if stream is not None else torch.cuda.current_stream(self.eng.dev)
+        with torch.cuda.stream(s):
+            for k in self._state_keys():
+                self.db.tensors[k].copy_(self.snapshot[k], non_blocking=True)
+
+    def step(self, stream=None):
+        self.eng.launch(self.db_new, stream)
+
+    def verify(self, one_shot: ReplayResult) -> Dict[str, int]:
+        """Compare the last step's rows with the one-shot replay of the whole histories (same layout):
+        every field of the exec row but the per-call counters, and every live row, for the split
+        workflows whose prefix and whole replays are OK and whose loaded state is Load-stable (each
+        live activity keeps its ActivityID mapping, mutable_state_builder.go:311-314)."""
+        b = self.batch
+        res = self.eng.download(self.db)
+        ok = (self.prefix.exec["status"] == 0) & (one_shot.exec["status"] == 0) & self.split
+        live_pre = gather_live(b, self.prefix)
+        c = np.clip(self.prefix.exec["n_activity"].astype(np.int64), 0, b.wf["act_cap"].astype(np.int64))
+        wf = np.repeat(np.arange(b.n_wf), c)
+        unstable = np.zeros(b.n_wf, bool)
+        np.logical_or.at(unstable, wf[(live_pre["act"]["flags"] & abi.ROW_MAPPED) == 0], True)
+        sel = ok & ~unstable
+        bad = 0
+        for f in abi.EXEC_ROW.names:
+            if f in ("reserved", "inconsistencies", "n_tasks"):
+                continue
+            bad += int(((res.exec[f] != one_shot.exec[f]) & sel).sum())
+        la, lb = gather_live(b, res), gather_live(b, one_shot)
+        for t, (name, _dt, _b, cap_f, n_f) in enumerate(abi.TABLES):
+            if name == "tasks":
+                continue
+            cap = b.wf[cap_f].astype(np.int64)     # gather_live's clamp
+            ca = np.clip(res.exec[n_f].astype(np.int64), 0, cap)
+            cb = np.clip(one_shot.exec[n_f].astype(np.int64), 0, cap)
+            keep_a = np.repeat(sel, ca)
+            keep_b = np.repeat(sel, cb)
+            ra, rb = la[name][keep_a], lb[name][keep_b]
+            if ra.shape != rb.shape:
+                bad += 1
+                continue
+            for fld in ra.dtype.names:
+                if fld == "reserved":
+                    continue
+                x, y = ra[fld], rb[fld]
+                if fld == "flags":   # Load recomputes the ActivityID mapping bit; the persisted flags must agree
+                    x, y = x & ~np.uint32(abi.ROW_MAPPED), y & ~np.uint32(abi.ROW_MAPPED)
+                bad += int((x != y).sum())
+        return {"compared_workflows": int(sel.sum()), "split_workflows": int(self.split.sum()),
+                "resumed_ok": int((res.exec["status"] == 0).sum()), "mismatches": bad}

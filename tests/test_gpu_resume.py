@@ -67,3 +67,33 @@ def test_resume_passive_replication_last_batch(engine):
     hs = synth_mixed.mixed_histories(4000, 63, multi_version=True)
     loaded, n = _device_split(engine, hs, 7, interleave, last_only=True)
     assert n > 2500
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("native", [False, True])
+def test_passive_replication_in_place_matches_one_shot(native):
+    """The bench's passive-replication step at test size: every workflow cut before its last batch, the
+    prefix replayed, the last batches applied onto the rows left in HBM (CRR_WF_FLAG_RESUME) -- equal
+    to the one-shot replay for every Load-stable workflow, checksum included, over two restored steps."""
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.flatten import interleave
+    from cadence_amd.replication import PassiveReplication
+    eng = ReplayEngine(0)
+    if native:
+        from cadence_amd import synth_native
+        canon = synth_native.mixed(20000, can_rate=0.3)
+    else:
+        from cadence_amd import synth_mixed
+        from cadence_amd.flatten import flatten
+        canon = flatten(synth_mixed.mixed_histories(3000, 44, mean_len=120, multi_version=True, can_rate=0.3),
+                        known_domains={"domain-a", "domain-b", "parent-domain"})
+    b = interleave(canon, long_threshold=150)
+    one = eng.replay(b)
+    pr = PassiveReplication(eng, b)
+    pr.setup()
+    for _ in range(2):
+        pr.restore()
+        pr.step()
+    v = pr.verify(one)
+    assert v["mismatches"] == 0, v
+    assert v["compared_workflows"] > 0.5 * v["split_workflows"] > 0, v   # the rest: failed or not Load-stable

@@ -301,32 +301,46 @@ def _resume_bytes(pr):
 
 # ---- rank 0, N = 1: end to end, host ingest, CPU baseline ---------------------------------------------------
 def end_to_end(ctx, n_wf, k, chunks=8):
-    """Config 2 from host buffers: pinned staging, `chunks` chunks overlapped on three streams, live rows
-    compacted on the device; checked against the HBM-resident digest of the same workflows."""
+    """Config 2 from host buffers: pinned staging, `chunks` chunks overlapped on three streams, the event
+    columns in the narrow upload format widened on the device (wire.py; the 49-B/event columns
+    alongside as ``columns_wide``), live rows compacted on the device; checked against the
+    HBM-resident digest of the same workflows."""
     from cadence_amd import dist as cdist
     from cadence_amd import synth
     from cadence_amd.flatten import interleave
     from cadence_amd.pipeline import StreamingReplay
     bounds = np.linspace(0, n_wf, chunks + 1).astype(np.int64)
-    t0 = time.time()
     parts = [interleave(synth.activity_chain(int(b - a), k, synth.SEED_C2, with_keys=False, wf_ids=np.arange(a, b)))
              for a, b in zip(bounds[:-1], bounds[1:])]
-    sr = StreamingReplay(ctx.eng, parts)
-    setup = time.time() - t0
-    sr.run()                                     # warm
-    runs = [sr.run() for _ in range(3)]
-    best = min(runs, key=lambda r: r["wall_s"])
-    med = float(np.median([r["wall_s"] for r in runs]))
-    digest = np.zeros(6, np.int64)
-    for cr in sr.results():
-        digest += cdist.digest_numpy(cr.exec)
-    out = {"events_per_s": best["events"] / med, "ms": med * 1e3, "events": best["events"], "chunks": chunks,
-           "h2d_bytes": best["h2d_bytes"], "d2h_bytes": best["d2h_bytes"],
-           "h2d_GBs": best["h2d_bytes"] / med / 1e9, "setup_s": setup, "digest": [int(x) for x in digest],
-           "note": "host columns in pinned staging buffers (where the decoder writes them); per chunk: H2D, output "
-                   "zero-fill, replay, crr_compact_rows, D2H of the exec rows + the live rows only; three streams "
-                   "overlap chunks; median of 3 passes"}
-    del sr
+    out = None
+    for wire in (True, False):
+        t0 = time.time()
+        sr = StreamingReplay(ctx.eng, parts, wire=wire)
+        setup = time.time() - t0
+        sr.run()                                     # warm
+        runs = [sr.run() for _ in range(3)]
+        med = float(np.median([r["wall_s"] for r in runs]))
+        r0 = runs[0]
+        digest = np.zeros(6, np.int64)
+        for cr in sr.results():
+            digest += cdist.digest_numpy(cr.exec)
+        fig = {"events_per_s": r0["events"] / med, "ms": med * 1e3, "events": r0["events"], "chunks": chunks,
+               "h2d_bytes": r0["h2d_bytes"], "d2h_bytes": r0["d2h_bytes"], "h2d_bytes_per_event": r0["h2d_bytes"] / r0["events"],
+               "h2d_GBs": r0["h2d_bytes"] / med / 1e9, "setup_s": setup, "digest": [int(x) for x in digest]}
+        if wire:
+            fig["pack_s"] = sr.pack_s
+            from cadence_amd.wire import COLUMNS
+            fig["widths"] = {c: int(getattr(sr.chunks[0].db.c_packed, c).width) for c in COLUMNS}
+            out = fig
+            out["note"] = ("host columns in pinned staging buffers (where the decoder writes them), event columns in the "
+                           "narrow upload format (per-workflow deltas at the batch's narrowest byte width; host packing "
+                           "time pack_s is not in the figure); per chunk: H2D, output zero-fill, crr_widen_events, replay, "
+                           "crr_compact_rows, D2H of the exec rows + the live rows only; three streams overlap chunks; "
+                           "median of 3 passes")
+        else:
+            out["columns_wide"] = fig
+        del sr
+        ctx.torch.cuda.empty_cache()
     return out
 
 
@@ -424,7 +438,8 @@ def main():
         line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr}
     if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
         line["pcie_inclusive"] = end_to_end(ctx, args.workflows, args.activities)
-        line["pcie_inclusive"]["matches_resident_digest"] = line["pcie_inclusive"]["digest"] == line["digest"]
+        e2e = line["pcie_inclusive"]
+        e2e["matches_resident_digest"] = e2e["digest"] == line["digest"] and e2e["columns_wide"]["digest"] == line["digest"]
         line["host_ingest"] = host_ingest(ctx, flat_s, flat_ev)
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ctx, res2, batch2, args.activities)

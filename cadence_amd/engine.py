@@ -53,6 +53,8 @@ def lib():
         L.crr_compact_rows.restype = ctypes.c_int
         L.crr_compact_scratch_bytes.argtypes = [ctypes.c_uint32]
         L.crr_compact_scratch_bytes.restype = ctypes.c_size_t
+        L.crr_widen_events.argtypes = [vp, vp, vp]
+        L.crr_widen_events.restype = ctypes.c_int
         if L.crr_abi_version() != abi.ABI_VERSION:
             raise EngineUnavailable("ABI version mismatch")
         abi.check_layout(L)
@@ -76,6 +78,7 @@ class DeviceBatch:
     c_out: abi.COutputs
     device: int
     c_compact: Optional[object] = None
+    c_packed: Optional[object] = None
 
     @property
     def n_wf(self):
@@ -239,6 +242,33 @@ class ReplayEngine:
             tot = int(off[t, n])
             rows[name] = T["cmp_" + name][:tot * dt.itemsize].cpu().numpy().view(dt)
         return CompactResult(ex, off, rows)
+
+    # -- narrow upload format (wire.py) --------------------------------------------------------------
+    def attach_packed(self, db: DeviceBatch, pk) -> object:
+        """Device buffers for a batch's packed columns and the crr_packed_events struct over them
+        (filled by the caller's copies); returns the struct."""
+        from .wire import COLUMNS, CPackedEvents
+        torch = self.torch
+        T = db.tensors
+        cp = CPackedEvents()
+        for c in COLUMNS:
+            a = pk.data[c]
+            T["pk_" + c] = torch.empty(max(a.size, 1) + 16, dtype=torch.uint8, device=self.dev)
+            col = getattr(cp, c)
+            col.data = T["pk_" + c].data_ptr()
+            col.width = pk.width[c]
+            col.kind = pk.kind[c]
+        T["pk_ts_base"] = torch.empty(max(pk.ts_base.size, 1), dtype=torch.int64, device=self.dev)
+        cp.ts_base = T["pk_ts_base"].data_ptr()
+        db.c_packed = cp
+        return cp
+
+    def widen(self, db: DeviceBatch, stream=None):
+        """Enqueue crr_widen_events: the packed columns -> the batch's event columns in HBM."""
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.dev)
+        rc = self.lib.crr_widen_events(ctypes.byref(db.c_packed), ctypes.byref(db.c_in), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_widen_events failed: {rc}")
 
     def replay(self, batch: HistoryBatch) -> ReplayResult:
         db = self.upload(batch)

@@ -48,17 +48,29 @@ def _input_arrays(batch: HistoryBatch) -> Dict[str, np.ndarray]:
 class StreamingReplay:
     """Chunked host -> device -> host replay of a list of (interleaved) batches."""
 
-    def __init__(self, eng: ReplayEngine, chunks: List[HistoryBatch]):
+    def __init__(self, eng: ReplayEngine, chunks: List[HistoryBatch], wire: bool = False):
+        """``wire``: ship the event columns in the narrow format (wire.py) and widen them on the device."""
         torch = eng.torch
-        self.eng, self.torch = eng, torch
+        self.eng, self.torch, self.wire = eng, torch, wire
         self.chunks: List[_Chunk] = []
+        self.pack_s = 0.0
         for b in chunks:
             db = eng.upload(b)                      # device buffers (inputs + outputs) and the C structs
             arrs = _input_arrays(b)
+            if wire:
+                from .wire import COLUMNS, pack_events
+                t0 = time.perf_counter()
+                pk = pack_events(b)
+                self.pack_s += time.perf_counter() - t0
+                eng.attach_packed(db, pk)
+                for c in COLUMNS:
+                    del arrs["ev_" + c]
+                    arrs["pk_" + c] = pk.data[c]
+                arrs["pk_ts_base"] = pk.ts_base.view(np.uint8)
             host_in, dev_in = {}, {}
             for k, a in arrs.items():
                 host_in[k] = torch.from_numpy(a.copy()).pin_memory()
-                dev_in[k] = db.tensors[k][:a.size]
+                dev_in[k] = db.tensors[k].view(torch.uint8)[:a.size]
             eng.compact(db)                         # allocates the dense buffers (first call)
             n = b.n_wf
             host_rows = {name: torch.empty(db.tensors["cmp_" + name].numel(), dtype=torch.uint8).pin_memory()
@@ -102,6 +114,8 @@ class StreamingReplay:
                     T[k].zero_()
                 for name, *_ in abi.TABLES:
                     T["out_" + name].zero_()
+                if self.wire:
+                    eng.widen(c.db, self.comp)
                 eng.launch(c.db, self.comp)
                 eng.compact(c.db, self.comp)
                 n = c.batch.n_wf

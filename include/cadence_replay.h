@@ -561,6 +561,33 @@ typedef struct crr_compact_out {
 size_t crr_compact_scratch_bytes(uint32_t n_wf);
 int crr_compact_rows(const crr_inputs* in, const crr_outputs* out, const crr_compact_out* dst, void* stream);
 
+/* ---- narrow upload format ------------------------------------------------------------------------
+ * The host may ship the event columns narrow (cadence_amd/wire.py): per column one byte width (1..8)
+ * for the whole batch and an encoding; crr_widen_events rebuilds the exact crr_events columns of
+ * `in` (device buffers, written) slot for slot in the same layout (in->wf, stride, wave tail), pads
+ * zeroed, before crr_replay on the same stream.  The etype column is shipped as is.
+ *   CRR_PACK_PLAIN     value, sign-extended
+ *   CRR_PACK_UNSIGNED  value, zero-extended
+ *   CRR_PACK_DELTA     value - the previous event's value of the same workflow (step 0: - 0, the
+ *                      timestamp column: - ts_base[w]); uint64 wrap-around, so exact for any input
+ *   CRR_PACK_ID_MINUS  (ref only) event_id - ref
+ * Returns 0 on successful launch, -1 on an invalid argument, else the hipError_t.  Not part of the
+ * reference interface: a transfer encoding between the host flattener and crr_replay. */
+#define CRR_PACK_PLAIN    0u
+#define CRR_PACK_UNSIGNED 1u
+#define CRR_PACK_DELTA    2u
+#define CRR_PACK_ID_MINUS 3u
+typedef struct crr_packed_column {
+    const uint8_t* data;     /* device: n_slots * width bytes, little-endian */
+    uint32_t       width;    /* 1..8 */
+    uint32_t       kind;     /* CRR_PACK_* */
+} crr_packed_column;
+typedef struct crr_packed_events {
+    crr_packed_column event_id, version, timestamp, task_id, ref, key, aux;
+    const int64_t*    ts_base;   /* device [n_wf]: the timestamp delta base (NULL: 0) */
+} crr_packed_events;
+int crr_widen_events(const crr_packed_events* packed, const crr_inputs* in, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,13 +47,50 @@ def test_compaction_matches_slot_tables(eng, emit):
 
 
 @pytest.mark.gpu
-def test_streaming_pipeline_matches_oracle(eng):
+@pytest.mark.parametrize("layout", ["interleaved", "canonical"])
+def test_widen_rebuilds_columns(eng, layout):
+    import torch
+    from cadence_amd.wire import event_slots, pack_events
+    canon = _mixed(2500, 17, mean_len=70, multi_version=True, invalid_rate=0.1, can_rate=0.3)
+    b = interleave(canon, long_threshold=100) if layout == "interleaved" else canon
+    db = eng.upload(b)
+    for name, _t in abi.EVENT_COLUMNS:
+        if name != "etype":
+            db.tensors["ev_" + name].fill_(0xA5)       # garbage the widening must overwrite
+    pk = pack_events(b)
+    eng.attach_packed(db, pk)
+    for c, a in pk.data.items():
+        db.tensors["pk_" + c][:a.size].copy_(torch.from_numpy(a))
+    db.tensors["pk_ts_base"].copy_(torch.from_numpy(pk.ts_base))
+    eng.widen(db)
+    torch.cuda.synchronize()
+    _w, _s, slot, _p = event_slots(b)
+    n_lane = b.wave_begin if b.wave_begin is not None else (b.n_wf if b.stride == 64 else 0)
+    pad = np.zeros(b.n_slots, bool)
+    if b.stride == 64 and n_lane:      # padding of live lanes (lanes past the last workflow are never read)
+        lane_slots = int(b.wf["ev_begin"][n_lane]) if n_lane < b.n_wf else b.n_slots
+        p = np.arange(lane_slots)
+        gb = b.wf["ev_begin"][:n_lane:64].astype(np.int64)            # group bases (lane 0 of each group)
+        w = (np.searchsorted(gb, p, side="right") - 1) * 64 + p % 64
+        pad[:lane_slots] = ((b.cols["etype"][:lane_slots] & abi.ETYPE_MASK) == abi.EV_PAD) & (w < n_lane)
+    for name, t in abi.EVENT_COLUMNS:
+        if name == "etype":
+            continue
+        got = db.tensors["ev_" + name][:b.n_slots * np.dtype(t).itemsize].cpu().numpy().view(t)
+        assert (got[slot] == b.cols[name][slot]).all(), name
+        assert (got[pad] == 0).all(), name
+    assert (eng.replay(b).exec["checksum"] != 0).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wire", [False, True])
+def test_streaming_pipeline_matches_oracle(eng, wire):
     from oracle import oracle
     from cadence_amd.pipeline import StreamingReplay
     chunks = [interleave(_mixed(1500, 90 + i, mean_len=60, multi_version=True, invalid_rate=0.05, can_rate=0.2))
               for i in range(3)]
     chunks.append(interleave(synth.activity_chain(4000, 3, synth.SEED_C2, wf_ids=np.arange(4000, 8000))))
-    sr = StreamingReplay(eng, chunks)
+    sr = StreamingReplay(eng, chunks, wire=wire)
     for _ in range(2):                       # a second pass reuses every buffer (outputs re-zeroed)
         st = sr.run()
     assert st["events"] == sum(c.n_events for c in chunks) and st["d2h_bytes"] > 0

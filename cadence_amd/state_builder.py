@@ -29,7 +29,7 @@ import numpy as np
 
 from . import abi
 from .abi import EventType as ET, Status
-from .flatten import HistoryBatch, flatten, interleave
+from .flatten import HistoryBatch, LoadedStates, flatten, interleave
 from .history import HistoryEvent, WorkflowHistory, det_uuid, thrift_history_branch_token
 
 EMPTY_UUID = "emptyUuid"  # common.EmptyUUID (common/constants.go:44)
@@ -280,6 +280,9 @@ class MutableState:
         self.inconsistencies: int = 0
         self.transfer_tasks: List[Task] = []
         self.timer_tasks: List[Task] = []
+        # what mutableStateBuilder.Load would read back (mutable_state_builder.go:306-349): the engine's row
+        # images of this state, so a StateBuilder constructed on it continues it on the device
+        self._loaded: Optional["_LoadedImage"] = None
 
     # mutable_state.go:59-239 (the subset replay callers read)
     def get_execution_info(self) -> WorkflowExecutionInfo:
@@ -361,6 +364,17 @@ class MutableState:
 
 # ---- the batched engine ---------------------------------------------------------------------------------
 @dataclasses.dataclass
+class _LoadedImage:
+    """A replayed state as the engine reloads it: its exec row and live rows (abi row images), the
+    workflow's key interner, and the events every provenance step of those rows refers to."""
+    history: WorkflowHistory          # identity (IDs, branch) of the workflow
+    events: List[HistoryEvent]        # every event applied so far (provenance steps index this list)
+    exec_row: np.ndarray              # abi.EXEC_ROW [1]
+    rows: Dict[str, np.ndarray]       # table -> live rows
+    interner: Dict[str, int]
+
+
+@dataclasses.dataclass
 class ReplayOutcome:
     """What ApplyEvents returns for one workflow: its state, its error, and for a continue-as-new
     the new run's state (state_builder.go:587-627)."""
@@ -389,10 +403,13 @@ class BatchStateBuilder:
         self.layout = layout
         self.emit_tasks = emit_tasks       # generate the transfer / timer tasks (CRR_IN_EMIT_TASKS)
         self.histories: List[WorkflowHistory] = []
+        self.loaded: List[Optional[_LoadedImage]] = []
         self._outcomes: Optional[List[ReplayOutcome]] = None
 
-    def add(self, history: WorkflowHistory) -> int:
+    def add(self, history: WorkflowHistory, loaded: Optional[_LoadedImage] = None) -> int:
+        """Stage a workflow; ``loaded``: its batches apply onto this loaded state (CRR_WF_FLAG_RESUME)."""
         self.histories.append(history)
+        self.loaded.append(loaded)
         self._outcomes = None
         return len(self.histories) - 1
 
@@ -412,14 +429,21 @@ class BatchStateBuilder:
     def replay(self) -> List[ReplayOutcome]:
         """One device replay of every staged workflow (canonical order of ``add``)."""
         known = None if self.domain_ids is None else set(self.domain_ids)
-        canon = flatten(self.histories, known_domains=known)
+        loaded = _loaded_states(self.loaded)
+        canon = flatten(self.histories, known_domains=known, loaded=loaded)
         canon.emit_tasks = self.emit_tasks
         batch = interleave(canon) if self.layout == "interleaved" else canon
         if self.engine is None:
             from .engine import ReplayEngine   # raises EngineUnavailable without the HIP library / a GPU
             self.engine = ReplayEngine(0)
         res = self.engine.replay(batch)
-        states = materialise(self.histories, batch, res, self.domain_ids, self.uuid_fn)
+        # a loaded workflow's provenance steps count from its first event ever (crr_exec_row.src_next)
+        all_events = [(li.events if li is not None else []) + h.events for h, li in zip(self.histories, self.loaded)]
+        states = materialise(self.histories, batch, res, self.domain_ids, self.uuid_fn, all_events)
+        images = res.to_loaded(batch)
+        for w, h in enumerate(self.histories):
+            if images.mask[w]:
+                states[w][0]._loaded = _image(images, w, self.loaded[w].history if self.loaded[w] else h, all_events[w])
         out = []
         for w, h in enumerate(self.histories):
             ms, st, step = states[w]
@@ -432,13 +456,50 @@ class BatchStateBuilder:
         return out
 
 
+def _loaded_states(images: Sequence[Optional[_LoadedImage]]) -> Optional[LoadedStates]:
+    """The batch's loaded states (flatten's ``loaded``), or None when every workflow starts fresh."""
+    if all(li is None for li in images):
+        return None
+    n = len(images)
+    ex = np.zeros(n, abi.EXEC_ROW)
+    mask = np.zeros(n, bool)
+    rows = {name: [] for name, *_ in abi.TABLES if name != "tasks"}
+    its = []
+    for w, li in enumerate(images):
+        its.append(dict(li.interner) if li is not None else None)
+        if li is None:
+            continue
+        ex[w] = li.exec_row
+        mask[w] = True
+        for name in rows:
+            rows[name].append(li.rows[name])
+    cat = {}
+    for name, dt, *_r in abi.TABLES:
+        if name != "tasks":
+            cat[name] = np.concatenate(rows[name]) if rows[name] else np.zeros(0, dt)
+    return LoadedStates(ex, cat, mask, its)
+
+
+def _image(images: LoadedStates, w: int, history: WorkflowHistory, events: List[HistoryEvent]) -> _LoadedImage:
+    rows = {}
+    for name, *_r in abi.TABLES:
+        if name == "tasks":
+            continue
+        c = images.counts(name)
+        off = int(c[:w].sum())
+        rows[name] = images.rows[name][off:off + int(c[w])].copy()
+    return _LoadedImage(history, list(events), images.exec[w:w + 1].copy(), rows,
+                        dict(images.interners[w]) if images.interners is not None else {"": 0})
+
+
 def _attr(e: HistoryEvent, name, default=None):
     return e.get(name, default)
 
 
 def materialise(histories: Sequence[WorkflowHistory], batch: HistoryBatch, res, domain_ids=None,
-                uuid_fn: Callable[[str, str, int], str] = _default_uuid):
-    """Device rows -> one MutableState per workflow (canonical order): [(state, status, fail_step)]."""
+                uuid_fn: Callable[[str, str, int], str] = _default_uuid, events=None):
+    """Device rows -> one MutableState per workflow (canonical order): [(state, status, fail_step)].
+    ``events[w]``: the events workflow w's provenance steps index (default: its history's events)."""
     n = len(histories)
     dev_of = np.arange(n) if batch.perm is None else np.argsort(batch.perm, kind="stable")
     strides = batch.wf_strides()
@@ -447,13 +508,13 @@ def materialise(histories: Sequence[WorkflowHistory], batch: HistoryBatch, res, 
         d = int(dev_of[w])
         ex = res.exec[d]
         wfr = batch.wf[d]
-        events = h.events
+        evs = h.events if events is None else events[w]
         rows = {}
         for name, _dt, base_f, cap_f, n_f in abi.TABLES:
             k = min(int(ex[n_f]), int(wfr[cap_f]))
             idx = int(wfr[base_f]) + np.arange(max(k, 0), dtype=np.int64) * int(strides[d])
             rows[name] = res.tables[name][idx]
-        out.append((_materialise_one(h, events, ex, rows, domain_ids, uuid_fn), int(ex["status"]), int(ex["fail_step"])))
+        out.append((_materialise_one(h, evs, ex, rows, domain_ids, uuid_fn), int(ex["status"]), int(ex["fail_step"])))
     return out
 
 
@@ -583,19 +644,37 @@ def _materialise_one(h: WorkflowHistory, events: List[HistoryEvent], ex, rows, d
 class StateBuilder:
     """``execution.StateBuilder`` for one workflow over a :class:`BatchStateBuilder`.
 
+    ``NewStateBuilder(shard, logger, mutableState)`` (state_builder.go:73-88): ``mutable_state`` is the
+    state the events apply onto -- None for a fresh ``NewMutableStateBuilderWithVersionHistories``
+    (rebuild, start-event replication), or a state a previous replay returned, i.e. what
+    ``mutableStateBuilder.Load`` reads back (the passive-replication path, ndc/history_replicator.go:
+    385-460): its rows are reloaded into the engine (CRR_WF_FLAG_RESUME) and only the new batches replay.
+
     ``apply_events`` stages a batch (the ``history`` argument of one Go ``ApplyEvents`` call); the
     device replay runs when the state is read (``get_mutable_state``) or the batch builder
-    flushes, so many workflows share one launch.  Errors are the Go errors, raised from
-    ``get_mutable_state`` (an empty ``history`` raises at once, as Go returns before touching state).
+    flushes, so many workflows share one launch.  Deviation from Go, by design: Go's
+    ``ApplyEvents`` returns ``(MutableState, error)`` per call (state_builder.go:90-97); here the
+    call returns None and the error of the first failing event of any staged call is raised by
+    ``get_mutable_state`` -- the outcome is the same because replay stops at the first error in both
+    (the caller aborts on it, state_rebuilder.go:221), but it surfaces at the read, not at the call.
+    An empty ``history`` raises at once, as Go returns before touching state.
     """
 
     def __init__(self, domain_failover_version: int = 0, domain_id: str = "domain-id", workflow_id: str = "workflow-id",
                  run_id: str = "run-id", branch_id: str = "branch-id", now_ns: int = 0,
-                 batch_builder: Optional[BatchStateBuilder] = None):
+                 batch_builder: Optional[BatchStateBuilder] = None, mutable_state: Optional[MutableState] = None):
         self._bb = batch_builder if batch_builder is not None else BatchStateBuilder()
+        loaded = None
+        if mutable_state is not None:
+            loaded = mutable_state._loaded
+            if loaded is None:
+                raise InternalServiceError("mutable state was not produced by a replay: no row image to load")
+            o = loaded.history
+            domain_id, workflow_id, run_id, branch_id = o.domain_id, o.workflow_id, o.run_id, o.branch_id
+            domain_failover_version = o.domain_failover_version
         self._h = WorkflowHistory(batches=[], domain_id=domain_id, domain_failover_version=domain_failover_version,
                                   workflow_id=workflow_id, run_id=run_id, branch_id=branch_id, now_ns=now_ns)
-        self._w = self._bb.add(self._h)      # staged now: every StateBuilder of a batch shares one replay
+        self._w = self._bb.add(self._h, loaded)   # staged now: every StateBuilder of a batch shares one replay
         self._new_run_w: Optional[int] = None
 
     def apply_events(self, domain_id: str, request_id: str, workflow_execution: Dict[str, str],

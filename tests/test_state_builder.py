@@ -224,3 +224,73 @@ def test_generated_tasks_materialised(engine):  # MutableState.GetTransferTasks 
     assert [t.kind for t in timers] == [abi.TaskKind.WorkflowTimeout, abi.TaskKind.DecisionTimeout,
                                         abi.TaskKind.ActivityTimeout]
     assert timers[-1].visibility_timestamp == NOW + 5 * SEC + 10 * SEC
+
+
+def test_state_builder_continues_a_loaded_mutable_state(engine):
+    """NewStateBuilder(shard, logger, mutableState) (state_builder.go:73-88) over the state a previous
+    replay returned -- what mutableStateBuilder.Load reads back (mutable_state_builder.go:306-349) on the
+    passive-replication path (ndc/history_replicator.go:385-460): the remaining batches applied onto it
+    give the one-shot replay's state (every workflow whose activity-ID map survives a reload)."""
+    import random
+    from cadence_amd import synth_mixed
+    hs = [h for h in synth_mixed.mixed_histories(80, 21, mean_len=40, multi_version=True) if len(h.batches) >= 2]
+    rng = random.Random(5)
+    one_bb, pre_bb, res_bb = (BatchStateBuilder(engine=engine) for _ in range(3))
+
+    def builder(h, bb, **kw):
+        return StateBuilder(h.domain_failover_version, h.domain_id, h.workflow_id, h.run_id, h.branch_id,
+                            now_ns=h.now_ns, batch_builder=bb, **kw)
+
+    ex = {"workflow_id": "", "run_id": ""}
+    one, pre, cut = [], [], []
+    for h in hs:
+        ex = {"workflow_id": h.workflow_id, "run_id": h.run_id}
+        k = rng.randint(1, len(h.batches) - 1)
+        a, b = builder(h, one_bb), builder(h, pre_bb)
+        for bt in h.batches:
+            a.apply_events(h.domain_id, h.request_id, ex, bt)
+        for bt in h.batches[:k]:
+            b.apply_events(h.domain_id, h.request_id, ex, bt)
+        one.append(a)
+        pre.append(b)
+        cut.append(k)
+    resumed = []
+    for h, b, k in zip(hs, pre, cut):
+        try:
+            ms = b.get_mutable_state()
+        except Exception:
+            resumed.append(None)
+            continue
+        stable = len(ms.pending_activity_id_to_event_id) == len(ms.pending_activity_info_ids)
+        r = builder(h, res_bb, mutable_state=ms)
+        for bt in h.batches[k:]:
+            r.apply_events(h.domain_id, h.request_id, {"workflow_id": h.workflow_id, "run_id": h.run_id}, bt)
+        resumed.append(r if stable else None)
+    compared = 0
+    for a, r in zip(one, resumed):
+        if r is None:
+            continue
+        try:
+            ma = a.get_mutable_state()
+        except Exception as e:
+            with pytest.raises(type(e)):
+                r.get_mutable_state()
+            continue
+        mr = r.get_mutable_state()
+        assert mr.get_checksum() == ma.get_checksum()
+        assert mr.execution_info == ma.execution_info
+        assert mr.get_current_version() == ma.get_current_version()
+        assert mr.pending_activity_info_ids == ma.pending_activity_info_ids
+        assert mr.pending_timer_info_ids == ma.pending_timer_info_ids
+        assert mr.pending_child_execution_info_ids == ma.pending_child_execution_info_ids
+        assert mr.pending_request_cancel_info_ids == ma.pending_request_cancel_info_ids
+        assert mr.pending_signal_info_ids == ma.pending_signal_info_ids
+        assert mr.version_histories == ma.version_histories
+        compared += 1
+    assert compared > len(hs) // 2
+
+
+def test_state_builder_rejects_a_state_without_row_image():
+    from cadence_amd.state_builder import MutableState
+    with pytest.raises(InternalServiceError):
+        StateBuilder(mutable_state=MutableState())

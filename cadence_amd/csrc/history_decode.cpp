@@ -11,6 +11,7 @@
 // length + bytes, list = element type + be32 count, struct = fields until a 0 byte.
 #include "cadence_decode.h"
 #include "host_flatten.h"
+#include "json_decode.h"
 
 #include <algorithm>
 #include <cstring>
@@ -308,6 +309,7 @@ void read_event(Reader& r, Event& e) {
 struct Ctx {
   const uint8_t* const* blobs;
   const uint64_t* lens;
+  const uint32_t* encodings;  // null: every blob thriftrw
   uint32_t n_blobs;
   const crr_wf_source* wfs;
   const std::unordered_set<std::string>* known;  // null: every name resolves
@@ -322,8 +324,21 @@ void decode_workflow(const Ctx& c, uint32_t w, Chunk& k) {
     if (bi >= c.n_blobs) throw DecodeError{CRR_DECODE_BAD_ARGUMENT};
     k.err_blob = bi;
     const uint64_t len = c.lens[bi];
+    const uint32_t enc = c.encodings ? c.encodings[bi] : CRR_ENCODING_THRIFTRW;
     f.batch_begin();
-    if (len > 0) {
+    if (enc > CRR_ENCODING_EMPTY) throw DecodeError{CRR_DECODE_UNKNOWN_ENCODING};
+    if (len > 0 && enc != CRR_ENCODING_THRIFTRW) {   // json.Unmarshal(data, &[]*types.HistoryEvent)
+      std::vector<Event> evs;
+      try {
+        json_decode_batch(reinterpret_cast<const char*>(c.blobs[bi]), reinterpret_cast<const char*>(c.blobs[bi]) + len, evs);
+      } catch (const JsonError& je) {
+        throw DecodeError{je.code};
+      }
+      for (Event& ev : evs) {
+        ev.a.new_run = src.new_run_wf;
+        f.add(ev);
+      }
+    } else if (len > 0) {
       Reader r{c.blobs[bi], c.blobs[bi] + len};
       if (r.u8() != 0x59) throw DecodeError{CRR_DECODE_BAD_PREAMBLE};  // version0Thriftrw.go:53-58
       // History{10 Events list<HistoryEvent>}
@@ -378,6 +393,14 @@ extern "C" {
 crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* blob_lens, uint32_t n_blobs,
                                   const crr_wf_source* wfs, uint32_t n_wf, const char* const* known_domains,
                                   uint32_t n_known, int n_threads, int* err, int64_t* err_blob) {
+  return crr_decode_histories_enc(blobs, blob_lens, nullptr, n_blobs, wfs, n_wf, known_domains, n_known, n_threads, err,
+                                  err_blob);
+}
+
+crr_decoded* crr_decode_histories_enc(const uint8_t* const* blobs, const uint64_t* blob_lens,
+                                      const uint32_t* blob_encodings, uint32_t n_blobs, const crr_wf_source* wfs,
+                                      uint32_t n_wf, const char* const* known_domains, uint32_t n_known, int n_threads,
+                                      int* err, int64_t* err_blob) {
   if (err) *err = CRR_DECODE_OK;
   if (err_blob) *err_blob = -1;
   if ((n_blobs && (!blobs || !blob_lens)) || (n_wf && !wfs)) {
@@ -388,7 +411,7 @@ crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* b
   const bool all_known = n_known == 0xFFFFFFFFu;
   if (!all_known)
     for (uint32_t i = 0; i < n_known; ++i) known.emplace(known_domains[i] ? known_domains[i] : "");
-  Ctx c{blobs, blob_lens, n_blobs, wfs, all_known ? nullptr : &known};
+  Ctx c{blobs, blob_lens, blob_encodings, n_blobs, wfs, all_known ? nullptr : &known};
 
   if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
   const uint32_t T = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)n_threads, (n_wf + 255) / 256));

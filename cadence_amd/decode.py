@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("CRR_HOST_LIB_PATH") or os.path.join(_HERE, "libcadenc
 _lib = None
 
 ERRORS = {-1: "bad argument", -2: "bad preamble (not a version-0 thriftrw blob)", -3: "truncated blob",
-          -4: "unexpected thrift type"}
+          -4: "unexpected thrift type", -5: "json.Unmarshal error", -6: "unknown encoding type"}
 
 
 class DeserializationError(RuntimeError):
@@ -66,6 +66,9 @@ def lib():
         L.crr_decode_histories.argtypes = [vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32, vp, ctypes.c_uint32,
                                            ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]
         L.crr_decode_histories.restype = vp
+        L.crr_decode_histories_enc.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32, vp, ctypes.c_uint32,
+                                               ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]
+        L.crr_decode_histories_enc.restype = vp
         L.crr_decoded_get_view.argtypes = [vp, ctypes.POINTER(CDecodedView)]
         L.crr_decoded_get_view.restype = ctypes.c_int
         L.crr_decoded_free.argtypes = [vp]
@@ -91,6 +94,7 @@ class WorkflowSource:
     is_new_run: bool = False
     refresh_tasks: bool = False          # Rebuild's RefreshTasks after the replay
     retention_days: int = 1
+    encodings: Optional[List[str]] = None   # per blob: "thriftrw" (default), "json", "" (empty), "unknown"
 
 
 def _copy(ptr, n, dtype):
@@ -126,23 +130,28 @@ def time_native_decode(sources: Sequence[WorkflowSource], known_domains: Optiona
             n_ev = int(v.n_events)
         L.crr_decoded_free(h)
         reps += 1
-    blob_bytes = int(sum(args[1][i] for i in range(args[2])))
+    blob_bytes = int(sum(args[1][i] for i in range(args[3])))
     return {"events": n_ev, "workflows": len(sources), "blob_bytes": blob_bytes, "reps": reps,
             "seconds_per_pass": dt / reps, "events_per_s": n_ev * reps / dt, "MB_per_s": blob_bytes * reps / dt / 1e6}
 
 
 def _decode_call(L, args, n_threads: int):
-    bptr, blen, nb, cw, n_src, kd, nk, _keep = args
+    bptr, blen, benc, nb, cw, n_src, kd, nk, _keep = args
     err = ctypes.c_int(0)
     err_blob = ctypes.c_int64(-1)
-    h = L.crr_decode_histories(bptr, blen, nb, cw, n_src, kd, nk, int(n_threads), ctypes.byref(err), ctypes.byref(err_blob))
+    h = L.crr_decode_histories_enc(bptr, blen, benc, nb, cw, n_src, kd, nk, int(n_threads), ctypes.byref(err),
+                                   ctypes.byref(err_blob))
     if not h:
         raise DeserializationError(err.value, err_blob.value)
     return h
 
 
+ENCODINGS = {"thriftrw": 0, "json": 1, "unknow": 2, "unknown": 2, "": 3}   # common.EncodingType -> CRR_ENCODING_*
+
+
 def _prepare(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable[str]]):
     blobs: List[bytes] = []
+    encs: List[int] = []
     cw = (CWfSource * max(len(sources), 1))()
     keep = []
     for w, s in enumerate(sources):
@@ -150,6 +159,9 @@ def _prepare(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable
         c.blob_begin = len(blobs)
         c.blob_count = len(s.blobs)
         blobs.extend(s.blobs)
+        for i in range(len(s.blobs)):
+            e = "thriftrw" if s.encodings is None else s.encodings[i]
+            encs.append(ENCODINGS.get(e, 0xFF))
         c.init_version = s.domain_failover_version
         c.now_ns = s.now_ns
         c.run_id = s.run_id.encode()
@@ -180,7 +192,8 @@ def _prepare(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable
         names = [n.encode() for n in known_domains]
         kd = (ctypes.c_char_p * max(len(names), 1))(*names)
         nk = len(names)
-    return bptr, blen, nb, cw, len(sources), kd, nk, (keep, bufs)
+    benc = (ctypes.c_uint32 * max(nb, 1))(*encs) if encs else (ctypes.c_uint32 * 1)()
+    return bptr, blen, benc, nb, cw, len(sources), kd, nk, (keep, bufs)
 
 
 def batch_from_handle(L, h) -> HistoryBatch:

@@ -87,6 +87,7 @@ _JSON_ATTR = {
         "initiator": "initiator", "parentWorkflowDomain": "parent_workflow_domain",
         "parentWorkflowDomainId": "parent_workflow_domain_id", "attempt": "attempt",
         "cronSchedule": "cron_schedule", "continuedExecutionRunId": "continued_execution_run_id",
+        "expirationTimestamp": "expiration_timestamp", "prevAutoResetPoints": "prev_auto_reset_points",
     },
     "decisionTaskScheduledEventAttributes": {"startToCloseTimeoutSeconds": "start_to_close_timeout_seconds",
                                              "attempt": "attempt"},
@@ -137,6 +138,11 @@ def events_from_json(raw) -> List[HistoryEvent]:
                     continue
                 if name == "timeout_type" and isinstance(jv, str):
                     jv = _TIMEOUT_NAMES[jv]
+                if name == "retry_policy" and isinstance(jv, dict):     # RetryPolicy{expirationIntervalInSeconds}
+                    jv = {"expiration_interval_in_seconds": jv.get("expirationIntervalInSeconds", 0)}
+                if name == "prev_auto_reset_points" and jv is not None:  # ResetPoints{points: [{binaryChecksum}]}
+                    pts = jv.get("points")
+                    jv = "nil_points" if pts is None else [(p or {}).get("binaryChecksum", "") for p in pts]
                 attrs[name] = jv
             if k == "workflowExecutionStartedEventAttributes":
                 attrs.setdefault("prev_auto_reset_points", None)

@@ -69,6 +69,16 @@ typedef struct crr_decoded crr_decoded;
 #define CRR_DECODE_BAD_PREAMBLE   -2   /* not a version-0 thriftrw blob (version0Thriftrw.go:53-58) */
 #define CRR_DECODE_TRUNCATED      -3   /* thrift value runs past the end of the blob */
 #define CRR_DECODE_BAD_TYPE       -4   /* field / element of an unexpected or unknown thrift type */
+#define CRR_DECODE_BAD_JSON       -5   /* a json-encoded blob json.Unmarshal rejects (syntax or type error) */
+#define CRR_DECODE_UNKNOWN_ENCODING -6 /* NewUnknownEncodingTypeError (serializer.go:326-327) */
+
+/* DataBlob.Encoding of each blob (common.EncodingType): serializerImpl.deserialize
+ * (common/persistence/serializer.go:321-328) decodes thriftrw with the thriftrw codec and json, the
+ * unknown and the empty encodings with json.Unmarshal (backward compatibility); anything else fails. */
+#define CRR_ENCODING_THRIFTRW 0u
+#define CRR_ENCODING_JSON     1u
+#define CRR_ENCODING_UNKNOWN  2u
+#define CRR_ENCODING_EMPTY    3u
 
 /* Decode every workflow's blobs.  known_domains: names the domain cache resolves (NULL with
  * n_known == UINT32_MAX: every name resolves).  n_threads <= 0: hardware concurrency.
@@ -78,6 +88,12 @@ crr_decoded* crr_decode_histories(const uint8_t* const* blobs, const uint64_t* b
                                   const crr_wf_source* wfs, uint32_t n_wf,
                                   const char* const* known_domains, uint32_t n_known,
                                   int n_threads, int* err, int64_t* err_blob);
+/* Same, with each blob's encoding (CRR_ENCODING_*; NULL: every blob thriftrw). */
+crr_decoded* crr_decode_histories_enc(const uint8_t* const* blobs, const uint64_t* blob_lens,
+                                      const uint32_t* blob_encodings, uint32_t n_blobs,
+                                      const crr_wf_source* wfs, uint32_t n_wf,
+                                      const char* const* known_domains, uint32_t n_known,
+                                      int n_threads, int* err, int64_t* err_blob);
 int  crr_decoded_get_view(const crr_decoded* d, crr_decoded_view* view);
 void crr_decoded_free(crr_decoded* d);
 

@@ -26,8 +26,11 @@ static std::vector<std::vector<uint8_t>> load(const char* path) {
   return out;
 }
 
+static uint32_t g_encoding = CRR_ENCODING_THRIFTRW;  // argv[3] == "json": every blob json-encoded
+
 static int decode(const std::vector<std::vector<uint8_t>>& blobs, int threads) {
   std::vector<const uint8_t*> p;
+  std::vector<uint32_t> enc(blobs.size(), g_encoding);
   std::vector<uint64_t> len;
   std::vector<crr_wf_source> wf;
   for (size_t i = 0; i < blobs.size(); ++i) {
@@ -45,8 +48,8 @@ static int decode(const std::vector<std::vector<uint8_t>>& blobs, int threads) {
   int err = 0;
   int64_t bad = -1;
   const char* known[] = {"domain-a", "domain-b"};
-  crr_decoded* d = crr_decode_histories(p.data(), len.data(), (uint32_t)p.size(), wf.data(), (uint32_t)wf.size(),
-                                        known, 2, threads, &err, &bad);
+  crr_decoded* d = crr_decode_histories_enc(p.data(), len.data(), enc.data(), (uint32_t)p.size(), wf.data(),
+                                            (uint32_t)wf.size(), known, 2, threads, &err, &bad);
   if (!d) return err;
   crr_decoded_view v;
   crr_decoded_get_view(d, &v);
@@ -59,6 +62,7 @@ static int decode(const std::vector<std::vector<uint8_t>>& blobs, int threads) {
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 2000;
+  if (argc > 3 && std::strcmp(argv[3], "json") == 0) g_encoding = CRR_ENCODING_JSON;
   auto corpus = load(argv[1]);
   if (corpus.empty()) { std::fprintf(stderr, "empty corpus\n"); return 2; }
   if (decode(corpus, 4) != 0) { std::fprintf(stderr, "intact corpus failed to decode\n"); return 1; }

@@ -17,6 +17,7 @@ __global__ void replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase
 template <bool EMIT>
 __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+__global__ void checksum_fill_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
 __global__ void replay_tail_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
@@ -224,13 +225,17 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, wb, n_lane);
+        // the compact tiers leave the checksum to a fill pass over their segment (their blocks then hold
+        // no CRC tables: more of them per CU)
         if (run_c2) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact2_kernel<true>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
           else hipLaunchKernelGGL((crr::replay_compact2_kernel<false>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
+          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((wb - c2 + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c2, *in, *out, phase, c2, wb);
         }
         if (run_c1) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
           else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
+          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((c2 - cb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c1, *in, *out, phase, cb, c2);
         }
         launch_fast(s_large, false, false, lb, cb);
         launch_fast(s, true, false, 0, lb);

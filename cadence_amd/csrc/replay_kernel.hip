@@ -1092,8 +1092,6 @@ struct CompactArena {
   u32 a_fl[A_SLOTS][LANES];
   u32 a_src[A_SLOTS][LANES];     // sched | started << 10 | cancel-requested << 20 (kStepMask: none)
   i64 a_cand[A_SLOTS][LANES];    // timestamp of the activity's earliest timer candidate
-  i64 a_s2c[A_SLOTS][LANES];     // ScheduledTime + ScheduleToCloseTimeout
-  int2 a_to[A_SLOTS][LANES];     // StartToCloseTimeout, HeartbeatTimeout
   u32 t_sid[T_SLOTS][LANES];
   u32 t_key[T_SLOTS][LANES];
   u32 t_fl[T_SLOTS][LANES];      // LIVE | TF_CREATED | src << 8
@@ -1191,8 +1189,6 @@ struct CompactTables {
     M->a_fl[j][t] = row.flags | ((u32)cy << CF_CAND_SHIFT);
     M->a_src[j][t] = (u32)row.sched_src | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
     M->a_cand[j][t] = ct;
-    M->a_s2c[j][t] = add_seconds(row.scheduled_time, row.schedule_to_close);
-    M->a_to[j][t] = make_int2(row.start_to_close, row.heartbeat);
     ++L.n_act;
     return CRR_OK;
   }
@@ -1201,12 +1197,16 @@ struct CompactTables {
     if (j < 0) return id_fits(sched) ? CRR_ERR_MISSING_ACTIVITY_INFO : CRR_INTERNAL_RETRY;
     const u32 f = M->a_fl[j][t];
     if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
-    // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime
-    const int2 to = M->a_to[j][t];
-    i64 ct = M->a_s2c[j][t];
+    // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime; the
+    // scheduled time and timeouts are re-read from the ActivityTaskScheduled event (not kept in LDS:
+    // 16 B less per slot is more wavefronts per CU)
+    const i32 ss = (i32)step_field(M->a_src[j][t], 0);
+    const i64 six = ix(ss);
+    const crr_activity_side as = in->act_side[in->ev.aux[six]];
+    i64 ct = add_seconds(in->ev.timestamp[six], as.schedule_to_close);
     i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-    cand_min(ct, cy, add_seconds(ts, to.x), CRR_TIMEOUT_START_TO_CLOSE);
-    if (to.y > 0) cand_min(ct, cy, add_seconds(ts, to.y), CRR_TIMEOUT_HEARTBEAT);
+    cand_min(ct, cy, add_seconds(ts, as.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+    if (as.heartbeat > 0) cand_min(ct, cy, add_seconds(ts, as.heartbeat), CRR_TIMEOUT_HEARTBEAT);
     M->a_cand[j][t] = ct;
     M->a_fl[j][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
     const u32 w = M->a_src[j][t];
@@ -1401,7 +1401,7 @@ struct CompactTables {
   __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
     sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
       swp(M->a_key[i][t], M->a_key[b][t]); swp(M->a_src[i][t], M->a_src[b][t]);
-      swp(M->a_cand[i][t], M->a_cand[b][t]); swp(M->a_s2c[i][t], M->a_s2c[b][t]); swp(M->a_to[i][t], M->a_to[b][t]);
+      swp(M->a_cand[i][t], M->a_cand[b][t]);
     });
     sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
       swp(M->t_exp[i][t], M->t_exp[b][t]); swp(M->t_key[i][t], M->t_key[b][t]);
@@ -2500,7 +2500,9 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
 
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
 // the replay loop of a launch that does not ask for tasks carries none of its registers.
-template <bool EMIT, class P, class SRC>
+// CRC (compile time): the checksum computed here; without it the caller's launch is followed by
+// checksum_fill_kernel over the same workflows (no CRC tables in the kernel's LDS).
+template <bool EMIT, class P, class SRC, bool CRC = true>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
                                             const Geo& G, P& T, SRC& src, const u32* crc_tables) {
   const i32 n_ev = wfp->ev_count;
@@ -2701,7 +2703,7 @@ done_events:
     return;
   }
   // the checksum's branch-token words go out before the row write-back, whose work hides their latency
-  const bool want_crc = L.status == CRR_OK && !(CRR_EXP & 1);
+  const bool want_crc = CRC && L.status == CRR_OK && !(CRR_EXP & 1);
   TokenWords TW;
   TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
   if (L.vh_n > 0) {
@@ -2750,7 +2752,9 @@ done_events:
   R.expiration_ns = L.expiration_ns;
   R.src_next = L.src_base + n_ev;
   R.reserved = 0;
-  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
+  if constexpr (CRC) {
+    if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
+  }
   out.exec[w] = R;
 #if CRR_EXP & 128
   if constexpr (kDbg) {
@@ -2980,9 +2984,7 @@ using CompactTier1 = CTier<4, 3, 2, 1, 1, 4, 64>;
 using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
 template <class TIER, bool EMIT>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
-  __shared__ u32 crc_tables[8 * 256];
   __shared__ CompactArena<TIER> arena;
-  build_crc_tables<64>(crc_tables);
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
   if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
@@ -3001,14 +3003,22 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   CompactTables<TIER> T;
   T.init(&arena, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT, CompactTables<TIER>, LaneSource, false>(in, out, w, wfp, G, T, S, nullptr);
 }
+// register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
+// limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
+#ifndef CRR_COMPACT1_WAVES_PER_EU
+#define CRR_COMPACT1_WAVES_PER_EU 3
+#endif
+#ifndef CRR_COMPACT2_WAVES_PER_EU
+#define CRR_COMPACT2_WAVES_PER_EU 2
+#endif
 template <bool EMIT>
-__global__ void __launch_bounds__(64) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+__global__ void __launch_bounds__(64, CRR_COMPACT1_WAVES_PER_EU) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   replay_compact<CompactTier1, EMIT>(in, out, phase, lo, hi);
 }
 template <bool EMIT>
-__global__ void __launch_bounds__(64) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+__global__ void __launch_bounds__(64, CRR_COMPACT2_WAVES_PER_EU) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   replay_compact<CompactTier2, EMIT>(in, out, phase, lo, hi);
 }
 template __global__ void replay_compact1_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
@@ -3124,6 +3134,28 @@ extern "C" int crr_debug_cycles(unsigned long long* dst, int n) {  // read and c
   return hipMemcpyToSymbol(HIP_SYMBOL(crr_dbg), zero, sizeof(zero)) == hipSuccess ? n : -1;
 }
 #endif
+
+// The checksum of the workflows [lo, hi) a CRC-less launch (replay_body<..., false>) just replayed
+// in this phase: the same payload_crc over the rows it wrote, stored into their exec rows.
+__global__ void __launch_bounds__(kBlock) checksum_fill_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  build_crc_tables(crc_tables);
+  const u32 w = lo + blockIdx.x * kBlock + threadIdx.x;
+  if (w >= hi) return;
+  const crr_workflow* wfp = in.wf + w;
+  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
+  crr_exec_row* R = out.exec + w;
+  if (R->status != CRR_OK) return;  // failed (no checksum) or handed to the retry pass (it computes its own)
+  Geo G;
+  load_geo(G, wfp, out, wf_stride(in, w));
+  GlobalTables ids;
+  TokenWords TW;
+  TW.issue(token_desc(wfp), R->token_src, in.arena);
+  u32 len = 0;
+  const u32 crc = payload_crc(*R, ids, G, TW, in.arena, crc_tables, &len);
+  R->checksum = crc;
+  R->payload_len = len;
+}
 
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).
 __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {

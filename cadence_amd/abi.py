@@ -291,7 +291,7 @@ class CInputs(ctypes.Structure):
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("compact_begin", ctypes.c_uint32),
                 ("compact2_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
-                ("big_begin", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32)]
 
 
 class COutputs(ctypes.Structure):

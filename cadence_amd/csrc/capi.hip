@@ -16,6 +16,8 @@ template <bool EMIT>
 __global__ void replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
 __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
+template <bool EMIT>
+__global__ void replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void checksum_fill_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
@@ -110,7 +112,7 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
     // (64-workflow) boundary, or its wavefronts would straddle two groups
     const uint32_t n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
     if (in->stride != 64) return false;
-    for (uint32_t b : {in->large_begin, in->compact_begin, in->compact2_begin, in->wide_begin})
+    for (uint32_t b : {in->large_begin, in->compact_begin, in->compact2_begin, in->wide_begin, in->hbm_begin})
       if (b < n_lane && (b & 63u)) return false;
   }
   return true;
@@ -201,13 +203,14 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
         const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
         const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
+        const uint32_t hb = clampb(in->hbm_begin, wb);
         const bool run_small = lb > 0, run_large = cb > lb, run_tail = tail && tail_end > n_lane;
-        const bool run_c1 = c2 > cb, run_c2 = wb > c2, run_wide = wb < n_lane;
+        const bool run_c1 = c2 > cb, run_c2 = wb > c2, run_c3 = hb > wb, run_wide = hb < n_lane;
         const bool run_big = tail_end < in->n_wf;
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
-        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_wide + (int)run_big +
-                              (int)run_tail > 1 &&
+        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_c3 + (int)run_wide +
+                              (int)run_big + (int)run_tail > 1 &&
                           ensure_side_streams();
         hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
         hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s, s_tail = fork ? g_side.st[5] : s;
@@ -222,9 +225,14 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
         }
+        if (run_c3) {
+          if (emit) hipLaunchKernelGGL((crr::replay_compact3_kernel<true>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
+          else hipLaunchKernelGGL((crr::replay_compact3_kernel<false>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
+          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((hb - wb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_wide, *in, *out, phase, wb, hb);
+        }
         if (run_wide)
-          hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - wb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
-                             s_wide, *in, *out, phase, wb, n_lane);
+          hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - hb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
+                             s_wide, *in, *out, phase, hb, n_lane);
         // the compact tiers leave the checksum to a fill pass over their segment (their blocks then hold
         // no CRC tables: more of them per CU)
         if (run_c2) {

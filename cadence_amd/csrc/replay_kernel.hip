@@ -27,7 +27,8 @@
 
 // Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
 // checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
-// record loads, bit 16 the start side record loads.  Bit 128 keeps outputs valid and counts shader
+// record loads, bit 16 the start side record loads, bit 256 the pending-map operations of the dispatch
+// (MOP_*).  Bit 128 keeps outputs valid and counts shader
 // cycles per event type in the one-wavefront-per-workflow path (crr_debug_cycles).
 #ifndef CRR_EXP
 #define CRR_EXP 0
@@ -362,6 +363,74 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
 // ===================================================================================================
 // GlobalTables: pending maps as slot tables in the HBM output rows (any layout, unbounded).
 // ===================================================================================================
+struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
+
+// The rows each insert writes (mutable_state_builder.go:2142-2197, :3057-3081, :3417-3453, :2760-2779, :2883-2905)
+__device__ __forceinline__ crr_activity_row activity_row(const Ev& ev, i32 s, i64 batch_first_id,
+                                                         const crr_activity_side& as) {
+  crr_activity_row row;
+  row.schedule_id = ev.id;
+  row.version = ev.ver;
+  row.scheduled_batch_id = batch_first_id;
+  row.scheduled_time = ev.ts;
+  row.started_id = CRR_EMPTY_EVENT_ID;
+  row.started_time = CRR_ZERO_TIME;
+  row.cancel_request_id = CRR_EMPTY_EVENT_ID;
+  row.last_hb_timeout_vis_s = 0;
+  row.sched_src = s;
+  row.started_src = -1;
+  row.schedule_to_start = as.schedule_to_start;
+  row.schedule_to_close = as.schedule_to_close;
+  row.start_to_close = as.start_to_close;
+  row.heartbeat = as.heartbeat;
+  row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+  row.key = ev.key;
+  row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
+  row.attempt = 0;
+  row.last_heartbeat_time = CRR_ZERO_TIME;
+  return row;
+}
+__device__ __forceinline__ crr_timer_row timer_row(const Ev& ev, i32 s) {
+  crr_timer_row row;
+  row.started_id = ev.id;
+  row.version = ev.ver;
+  row.expiry_time = add_seconds(ev.ts, ev.ref);
+  row.task_status = CRR_TIMER_TASK_STATUS_NONE;
+  row.key = ev.key;
+  row.src = s;
+  row.flags = CRR_ROW_LIVE;
+  return row;
+}
+__device__ __forceinline__ crr_child_row child_row(const Ev& ev, i32 s, i64 batch_first_id) {
+  crr_child_row row;
+  row.initiated_id = ev.id;
+  row.version = ev.ver;
+  row.initiated_batch_id = batch_first_id;
+  row.started_id = CRR_EMPTY_EVENT_ID;
+  row.src = s;
+  row.started_src = -1;
+  row.flags = CRR_ROW_LIVE;
+  row.reserved = 0;
+  return row;
+}
+__device__ __forceinline__ crr_initiated_row initiated_row(const Ev& ev, i32 s, i64 batch_first_id) {
+  crr_initiated_row row;
+  row.initiated_id = ev.id;
+  row.version = ev.ver;
+  row.initiated_batch_id = batch_first_id;
+  row.src = s;
+  row.flags = CRR_ROW_LIVE;
+  return row;
+}
+
+enum : u32 {
+  MOP_NONE = 0,
+  MOP_ACT_INSERT, MOP_ACT_START, MOP_ACT_DELETE, MOP_ACT_CANCEL,  // ReplicateActivityTask* / DeleteActivity
+  MOP_TIMER_START, MOP_TIMER_DELETE,                             // ReplicateTimerStarted / DeleteUserTimer
+  MOP_CHILD_INSERT, MOP_CHILD_START, MOP_CHILD_DELETE,
+  MOP_RC_INSERT, MOP_RC_DELETE, MOP_SIG_INSERT, MOP_SIG_DELETE
+};
+
 struct GlobalTables {
   static constexpr bool kResumable = true;  // rows live in HBM: a loaded state is continued in place
   __device__ __forceinline__ static bool fits(i64) { return true; }
@@ -1087,20 +1156,15 @@ constexpr i32 kMaxCompactSteps = (1 << kStepBits) - 1;  // step kStepMask encode
 template <class TIER>
 struct CompactArena {
   CRR_TIER_SLOTS
-  u32 a_sid[A_SLOTS][LANES];
   u32 a_key[A_SLOTS][LANES];
   u32 a_fl[A_SLOTS][LANES];
   u32 a_src[A_SLOTS][LANES];     // sched | started << 10 | cancel-requested << 20 (kStepMask: none)
   i64 a_cand[A_SLOTS][LANES];    // timestamp of the activity's earliest timer candidate
-  u32 t_sid[T_SLOTS][LANES];
   u32 t_key[T_SLOTS][LANES];
   u32 t_fl[T_SLOTS][LANES];      // LIVE | TF_CREATED | src << 8
   i64 t_exp[T_SLOTS][LANES];
-  u32 c_id[C_SLOTS][LANES];
   u32 c_fl[C_SLOTS][LANES];      // LIVE | initiated src << 8 | started src << 18 (kStepMask: none)
-  u32 r_id[R_SLOTS][LANES];
   u32 r_fl[R_SLOTS][LANES];      // LIVE | src << 8
-  u32 s_id[S_SLOTS][LANES];
   u32 s_fl[S_SLOTS][LANES];
   u32 p_key[P_SLOTS][LANES];
   u32 p_fl[P_SLOTS][LANES];      // row flags (LIVE | RESETTABLE) | src << 8 | (prev_index + 1) << 18
@@ -1110,11 +1174,18 @@ template <class TIER>
 struct CompactTables {
   CRR_TIER_SLOTS
   static constexpr bool kResumable = false;  // rows are rebuilt from this call's events
+  static constexpr bool kFusedMapOps = true;
   using Arena = CompactArena<TIER>;
   Arena* M;
   int t;  // threadIdx.x
   const crr_inputs* in;
   i64 ev_begin;
+  // No entry stores its event ID: every insert checks that its event's ID is id0 + its step (Cadence
+  // assigns IDs consecutively from the first event), so an entry's ID is id0 + the step it keeps anyway,
+  // and a lookup by ID compares steps.  An insert that breaks the rule hands the workflow to the general
+  // path (speed only, never results).
+  i64 id0 = 0;
+  bool have_id0 = false;
   bool retried = false;
   __device__ __forceinline__ void load(Lane&, const Geo&) {}
 
@@ -1134,9 +1205,8 @@ struct CompactTables {
 #pragma unroll
     for (int j = 0; j < S_SLOTS; ++j) M->s_fl[j][t] = 0;
   }
-  // fits the compact encodings (u32 IDs, 10-bit steps); else the general path replays it
+  // fits the compact encodings (10-bit steps); else the general path replays it
   __device__ __forceinline__ static bool fits(i64 n_ev) { return n_ev <= kMaxCompactSteps; }
-  __device__ __forceinline__ static bool id_fits(i64 id) { return id >= 0 && id <= (i64)0xFFFFFFFFu; }
   __device__ __forceinline__ i64 ix(i32 step) const { return ev_begin + (i64)step * 64; }
   __device__ __forceinline__ i64 ev_id(i32 step) const { return in->ev.event_id[ix(step)]; }
   __device__ __forceinline__ i64 ev_ver(i32 step) const { return in->ev.version[ix(step)]; }
@@ -1146,16 +1216,19 @@ struct CompactTables {
     return ev_id(step);
   }
   __device__ __forceinline__ static u32 step_field(u32 w, int k) { return (w >> (kStepBits * k)) & kStepMask; }
-
-  __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
-    if (!id_fits(sched)) return -1;
-    const u32 s32 = (u32)sched;
-    i32 hit = -1;
-#pragma unroll
-    for (int j = A_SLOTS - 1; j >= 0; --j)
-      if ((M->a_fl[j][t] & CRR_ROW_LIVE) && M->a_sid[j][t] == s32) hit = j;
-    return hit;
+  __device__ __forceinline__ i64 id_at(u32 step) const { return (i64)((u64)id0 + step); }
+  // the step an entry inserted by event ID `id` holds, or kStepMask (matches no entry)
+  __device__ __forceinline__ u32 step_of(i64 id) const {
+    const u64 d = (u64)id - (u64)id0;
+    return (have_id0 && d < (u64)kStepMask) ? (u32)d : kStepMask;
   }
+  // an insert by the event at step s: its ID must be id0 + s
+  __device__ __forceinline__ bool insert_ok(i64 id, i32 s) {
+    const i64 b = (i64)((u64)id - (u64)s);
+    if (!have_id0) { id0 = b; have_id0 = true; return true; }
+    return b == id0;
+  }
+
   __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
     i32 hit = -1;
 #pragma unroll
@@ -1170,157 +1243,171 @@ struct CompactTables {
   __device__ __forceinline__ static void cand_min(i64& ct, i32& cy, i64 t2, i32 y2) {
     if (t2 < ct || (t2 == ct && y2 < cy)) { ct = t2; cy = y2; }
   }
-  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
-    if (!id_fits(row.schedule_id)) return CRR_INTERNAL_RETRY;
-    i32 m = find_act_mapped(row.key);
-    i32 j = -1;
+
+  // Map operations (apply_event runs them after its switch, every lane at once): one pass over a map's
+  // slots finds the entry an operation addresses and the first free slot, then the operation's writes.
+  __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 /*bfid*/,
+                                        const crr_activity_side& as) {
+    if (op <= MOP_ACT_CANCEL) return act_op(L, G, op, ev, s, as);
+    if (op <= MOP_TIMER_DELETE) return timer_op(L, G, op, ev, s);
+    if (op <= MOP_CHILD_DELETE) return child_op(L, G, op, ev, s);
+    return init_op(L, G, op, ev, s);
+  }
+  // ActivityTaskScheduled / Started / closes / CancelRequested: the live entry with ScheduleID == ref
+  // (start, delete) or the mapped live entry with ActivityID == key (insert, cancel), and the first free
+  // slot (insert)
+  __device__ __forceinline__ int act_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, const crr_activity_side& as) {
+    const bool by_id = op == MOP_ACT_START || op == MOP_ACT_DELETE;
+    const u32 want = by_id ? step_of(ev.ref) : ev.key;
+    const u32 need = by_id ? CRR_ROW_LIVE : (CRR_ROW_LIVE | CRR_ROW_MAPPED);
+    i32 hit = -1, fr = -1;
 #pragma unroll
-    for (int k = A_SLOTS - 1; k >= 0; --k)
-      if (!(M->a_fl[k][t] & CRR_ROW_LIVE)) j = k;
-    if (j < 0) return CRR_INTERNAL_RETRY;
-    if (j >= G.act_cap) return CRR_ERR_CAPACITY;
-    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
-    // not started: ScheduleToClose and ScheduleToStart
-    i64 ct = add_seconds(row.scheduled_time, row.schedule_to_close);
-    i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-    cand_min(ct, cy, add_seconds(row.scheduled_time, row.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
-    M->a_sid[j][t] = (u32)row.schedule_id;
-    M->a_key[j][t] = row.key;
-    M->a_fl[j][t] = row.flags | ((u32)cy << CF_CAND_SHIFT);
-    M->a_src[j][t] = (u32)row.sched_src | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
-    M->a_cand[j][t] = ct;
-    ++L.n_act;
-    return CRR_OK;
-  }
-  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
-    const i32 j = find_act_by_id(sched);
-    if (j < 0) return id_fits(sched) ? CRR_ERR_MISSING_ACTIVITY_INFO : CRR_INTERNAL_RETRY;
-    const u32 f = M->a_fl[j][t];
-    if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
-    // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime; the
-    // scheduled time and timeouts are re-read from the ActivityTaskScheduled event (not kept in LDS:
-    // 16 B less per slot is more wavefronts per CU)
-    const i32 ss = (i32)step_field(M->a_src[j][t], 0);
-    const i64 six = ix(ss);
-    const crr_activity_side as = in->act_side[in->ev.aux[six]];
-    i64 ct = add_seconds(in->ev.timestamp[six], as.schedule_to_close);
-    i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-    cand_min(ct, cy, add_seconds(ts, as.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
-    if (as.heartbeat > 0) cand_min(ct, cy, add_seconds(ts, as.heartbeat), CRR_TIMEOUT_HEARTBEAT);
-    M->a_cand[j][t] = ct;
-    M->a_fl[j][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
-    const u32 w = M->a_src[j][t];
-    M->a_src[j][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
-    return CRR_OK;
-  }
-  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
-    const i32 j = find_act_by_id(sched);
-    if (j < 0) { ++L.inconsistencies; return; }
-    const u32 f = M->a_fl[j][t];
-    const u32 key = M->a_key[j][t];
-    M->a_fl[j][t] = 0;
+    for (int j = A_SLOTS - 1; j >= 0; --j) {
+      const u32 f = M->a_fl[j][t];
+      const u32 v = by_id ? (M->a_src[j][t] & kStepMask) : M->a_key[j][t];
+      if ((f & need) == need && v == want) hit = j;
+      if (!(f & CRR_ROW_LIVE)) fr = j;
+    }
+    if (op == MOP_ACT_INSERT) {
+      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
+      if (fr >= G.act_cap) return CRR_ERR_CAPACITY;
+      if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
+      // not started: ScheduleToClose and ScheduleToStart
+      i64 ct = add_seconds(ev.ts, as.schedule_to_close);
+      i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+      cand_min(ct, cy, add_seconds(ev.ts, as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+      const u32 fl = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
+      M->a_key[fr][t] = ev.key;
+      M->a_fl[fr][t] = fl | ((u32)cy << CF_CAND_SHIFT);
+      M->a_src[fr][t] = (u32)s | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
+      M->a_cand[fr][t] = ct;
+      ++L.n_act;
+      return CRR_OK;
+    }
+    if (op == MOP_ACT_START) {  // :2254-2276
+      if (hit < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
+      const u32 f = M->a_fl[hit][t];
+      if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
+      // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime; the
+      // scheduled time and timeouts are re-read from the ActivityTaskScheduled event (not kept in LDS)
+      const u32 w = M->a_src[hit][t];
+      const i64 six = ix((i32)step_field(w, 0));
+      const crr_activity_side sa = in->act_side[in->ev.aux[six]];
+      i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
+      i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+      cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+      if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
+      M->a_cand[hit][t] = ct;
+      M->a_fl[hit][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
+      M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
+      return CRR_OK;
+    }
+    if (op == MOP_ACT_CANCEL) {  // :2444-2467
+      if (hit < 0) return CRR_OK;
+      M->a_fl[hit][t] |= CRR_ROW_CANCEL_REQUESTED;
+      const u32 w = M->a_src[hit][t];
+      M->a_src[hit][t] = (w & ~(kStepMask << (2 * kStepBits))) | ((u32)s << (2 * kStepBits));
+      return CRR_OK;
+    }
+    // MOP_ACT_DELETE (DeleteActivity, mutable_state_builder.go:1310-1339)
+    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
+    const u32 f = M->a_fl[hit][t];
+    const u32 key = M->a_key[hit][t];
+    M->a_fl[hit][t] = 0;
     --L.n_act;
-    if (f & CRR_ROW_MAPPED) return;
+    if (f & CRR_ROW_MAPPED) return CRR_OK;
     const i32 m = find_act_mapped(key);
     if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
     else ++L.inconsistencies;
+    return CRR_OK;
   }
-  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 /*id*/, i64 /*ver*/, i32 s) {
-    const i32 j = find_act_mapped(key);
-    if (j < 0) return;
-    M->a_fl[j][t] |= CRR_ROW_CANCEL_REQUESTED;
-    const u32 w = M->a_src[j][t];
-    M->a_src[j][t] = (w & ~(kStepMask << (2 * kStepBits))) | ((u32)s << (2 * kStepBits));
-  }
-
-  __device__ __forceinline__ i32 find_timer(u32 key) const {
-    i32 hit = -1;
+  // TimerStarted (an existing TimerID is overwritten) / Fired / Canceled (:3057-3081, :1390-1419)
+  __device__ __forceinline__ int timer_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
+    i32 hit = -1, fr = -1;
 #pragma unroll
-    for (int j = T_SLOTS - 1; j >= 0; --j)
-      if ((M->t_fl[j][t] & CRR_ROW_LIVE) && M->t_key[j][t] == key) hit = j;
-    return hit;
-  }
-  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
-    if (!id_fits(row.started_id)) return CRR_INTERNAL_RETRY;
-    i32 j = find_timer(row.key);
+    for (int j = T_SLOTS - 1; j >= 0; --j) {
+      const u32 f = M->t_fl[j][t];
+      if ((f & CRR_ROW_LIVE) && M->t_key[j][t] == ev.key) hit = j;
+      if (!(f & CRR_ROW_LIVE)) fr = j;
+    }
+    if (op == MOP_TIMER_DELETE) {
+      if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
+      M->t_fl[hit][t] = 0;
+      --L.n_timer;
+      return CRR_OK;
+    }
+    if (!insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
+    i32 j = hit;
     if (j < 0) {
-#pragma unroll
-      for (int k = T_SLOTS - 1; k >= 0; --k)
-        if (!(M->t_fl[k][t] & CRR_ROW_LIVE)) j = k;
-      if (j < 0) return CRR_INTERNAL_RETRY;
-      if (j >= G.timer_cap) return CRR_ERR_CAPACITY;
+      if (fr < 0) return CRR_INTERNAL_RETRY;
+      if (fr >= G.timer_cap) return CRR_ERR_CAPACITY;
+      j = fr;
       ++L.n_timer;
     }
-    M->t_sid[j][t] = (u32)row.started_id;
-    M->t_exp[j][t] = row.expiry_time;
-    M->t_key[j][t] = row.key;
-    M->t_fl[j][t] = CRR_ROW_LIVE | ((u32)row.src << 8);
+    M->t_exp[j][t] = add_seconds(ev.ts, ev.ref);
+    M->t_key[j][t] = ev.key;
+    M->t_fl[j][t] = CRR_ROW_LIVE | ((u32)s << 8);
     return CRR_OK;
   }
-  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
-    const i32 j = find_timer(key);
-    if (j < 0) { ++L.inconsistencies; return; }
-    M->t_fl[j][t] = 0;
-    --L.n_timer;
+  // StartChildWorkflowExecutionInitiated / ChildWorkflowExecutionStarted / its closes (:3417-3453,
+  // :3485-3507, DeletePendingChildExecution :1160-1178): entries by InitiatedID == ref
+  __device__ __forceinline__ int child_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
+    const u32 want = op == MOP_CHILD_INSERT ? kStepMask : step_of(ev.ref);
+    i32 hit = -1, fr = -1;
+#pragma unroll
+    for (int j = C_SLOTS - 1; j >= 0; --j) {
+      const u32 f = M->c_fl[j][t];
+      if ((f & (CRR_ROW_LIVE | (kStepMask << 8))) == (CRR_ROW_LIVE | (want << 8))) hit = j;
+      if (!(f & CRR_ROW_LIVE)) fr = j;
+    }
+    if (op == MOP_CHILD_INSERT) {
+      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
+      if (fr >= G.child_cap) return CRR_ERR_CAPACITY;
+      M->c_fl[fr][t] = CRR_ROW_LIVE | ((u32)s << 8) | (kStepMask << (8 + kStepBits));
+      ++L.n_child;
+      return CRR_OK;
+    }
+    if (op == MOP_CHILD_START) {
+      if (hit < 0) return CRR_ERR_MISSING_CHILD_INFO;
+      const u32 f = M->c_fl[hit][t];
+      M->c_fl[hit][t] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
+      return CRR_OK;
+    }
+    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
+    M->c_fl[hit][t] = 0;
+    --L.n_child;
+    return CRR_OK;
+  }
+  // RequestCancelExternal / SignalExternal initiated and their resolutions (:2760-2779, :2883-2905,
+  // DeletePendingRequestCancel :1181-1199, DeletePendingSignal :1202-1220)
+  template <int N>
+  __device__ __forceinline__ int initiated_op(u32 (*fl)[LANES], i32& n, i32 cap, bool insert, const Ev& ev, i32 s,
+                                              Lane& L) {
+    const u32 want = insert ? kStepMask : step_of(ev.ref);
+    i32 hit = -1, fr = -1;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {
+      const u32 f = fl[j][t];
+      if ((f & (CRR_ROW_LIVE | (kStepMask << 8))) == (CRR_ROW_LIVE | (want << 8))) hit = j;
+      if (!(f & CRR_ROW_LIVE)) fr = j;
+    }
+    if (insert) {
+      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
+      if (fr >= cap) return CRR_ERR_CAPACITY;
+      fl[fr][t] = CRR_ROW_LIVE | ((u32)s << 8);
+      ++n;
+      return CRR_OK;
+    }
+    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
+    fl[hit][t] = 0;
+    --n;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int init_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
+    if (op <= MOP_RC_DELETE) return initiated_op<R_SLOTS>(M->r_fl, L.n_rc, G.rc_cap, op == MOP_RC_INSERT, ev, s, L);
+    return initiated_op<S_SLOTS>(M->s_fl, L.n_sig, G.sig_cap, op == MOP_SIG_INSERT, ev, s, L);
   }
 
-  template <int N>
-  __device__ __forceinline__ i32 find_init(const u32 (*ids)[LANES], const u32 (*fl)[LANES], i64 id) const {
-    if (!id_fits(id)) return -1;
-    const u32 i32id = (u32)id;
-    i32 hit = -1;
-#pragma unroll
-    for (int j = N - 1; j >= 0; --j)
-      if ((fl[j][t] & CRR_ROW_LIVE) && ids[j][t] == i32id) hit = j;
-    return hit;
-  }
-  template <int N>
-  __device__ __forceinline__ i32 free_init(const u32 (*fl)[LANES]) const {
-    i32 hit = -1;
-#pragma unroll
-    for (int j = N - 1; j >= 0; --j)
-      if (!(fl[j][t] & CRR_ROW_LIVE)) hit = j;
-    return hit;
-  }
-  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
-    if (!id_fits(row.initiated_id)) return CRR_INTERNAL_RETRY;
-    const i32 j = free_init<C_SLOTS>(M->c_fl);
-    if (j < 0) return CRR_INTERNAL_RETRY;
-    if (j >= G.child_cap) return CRR_ERR_CAPACITY;
-    M->c_id[j][t] = (u32)row.initiated_id;
-    M->c_fl[j][t] = CRR_ROW_LIVE | ((u32)row.src << 8) | (kStepMask << (8 + kStepBits));
-    ++L.n_child;
-    return CRR_OK;
-  }
-  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
-    const i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
-    if (j < 0) return id_fits(init) ? CRR_ERR_MISSING_CHILD_INFO : CRR_INTERNAL_RETRY;
-    const u32 f = M->c_fl[j][t];
-    M->c_fl[j][t] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
-    return CRR_OK;
-  }
-  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
-    const i32 j = find_init<C_SLOTS>(M->c_id, M->c_fl, init);
-    if (j < 0) { ++L.inconsistencies; return; }
-    M->c_fl[j][t] = 0;
-    --L.n_child;
-  }
-  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
-    if (!id_fits(row.initiated_id)) return CRR_INTERNAL_RETRY;
-    const i32 j = is_rc ? free_init<R_SLOTS>(M->r_fl) : free_init<S_SLOTS>(M->s_fl);
-    if (j < 0) return CRR_INTERNAL_RETRY;
-    if (j >= (is_rc ? G.rc_cap : G.sig_cap)) return CRR_ERR_CAPACITY;
-    const u32 f = CRR_ROW_LIVE | ((u32)row.src << 8);
-    if (is_rc) { M->r_id[j][t] = (u32)row.initiated_id; M->r_fl[j][t] = f; ++L.n_rc; }
-    else { M->s_id[j][t] = (u32)row.initiated_id; M->s_fl[j][t] = f; ++L.n_sig; }
-    return CRR_OK;
-  }
-  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
-    const i32 j = is_rc ? find_init<R_SLOTS>(M->r_id, M->r_fl, init) : find_init<S_SLOTS>(M->s_id, M->s_fl, init);
-    if (j < 0) { ++L.inconsistencies; return; }
-    if (is_rc) { M->r_fl[j][t] = 0; --L.n_rc; }
-    else { M->s_fl[j][t] = 0; --L.n_sig; }
-  }
   __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
     if (L.n_rp >= P_SLOTS || row.prev_index >= (i32)kStepMask - 1) return CRR_INTERNAL_RETRY;
@@ -1346,7 +1433,7 @@ struct CompactTables {
         const u32 f = M->a_fl[j][t];
         if (!(f & CRR_ROW_LIVE)) continue;
         const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
-        B.offer(M->a_cand[j][t], (i64)M->a_sid[j][t], y, j, ((f >> LF_TTS_SHIFT) & timer_mask(y)) != 0);
+        B.offer(M->a_cand[j][t], id_at(M->a_src[j][t] & kStepMask), y, j, ((f >> LF_TTS_SHIFT) & timer_mask(y)) != 0);
       }
       if (B.have && !B.created) {
         M->a_fl[B.j][t] |= (timer_mask(B.y) << LF_TTS_SHIFT) | (B.y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
@@ -1359,7 +1446,7 @@ struct CompactTables {
       for (int j = 0; j < T_SLOTS; ++j) {
         const u32 f = M->t_fl[j][t];
         if (!(f & CRR_ROW_LIVE)) continue;
-        B.offer(M->t_exp[j][t], (i64)M->t_sid[j][t], 0, j, (f & TF_CREATED) != 0);
+        B.offer(M->t_exp[j][t], id_at((f >> 8) & kStepMask), 0, j, (f & TF_CREATED) != 0);
       }
       if (B.have && !B.created) {
         M->t_fl[B.j][t] |= TF_CREATED;
@@ -1379,36 +1466,35 @@ struct CompactTables {
 
   template <class V>
   __device__ __forceinline__ static void swp(V& a, V& b) { V x = a; a = b; b = x; }
-  // selection sort of the live slots by event ID (slots 0..n-1 afterwards)
-  template <int N, class SwapFn>
-  __device__ __forceinline__ void sort_slots(u32 (*ids)[LANES], u32 (*fl)[LANES], i32 n, SwapFn swap_fn) {
+  // selection sort of the live slots by event ID -- by step: IDs are id0 + step (slots 0..n-1 afterwards)
+  template <int N, class StepFn, class SwapFn>
+  __device__ __forceinline__ void sort_slots(u32 (*fl)[LANES], i32 n, StepFn step_fn, SwapFn swap_fn) {
     for (i32 i = 0; i < n; ++i) {
       i32 best = -1;
-      u32 bid = 0;
+      u32 bst = 0;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j < i || !(fl[j][t] & CRR_ROW_LIVE)) continue;
-        const u32 id = ids[j][t];
-        if (best < 0 || id < bid) { best = j; bid = id; }
+        const u32 st = step_fn(j);
+        if (best < 0 || st < bst) { best = j; bst = st; }
       }
       if (best != i) {
         swap_fn(i, best);
-        swp(ids[i][t], ids[best][t]);
         swp(fl[i][t], fl[best][t]);
       }
     }
   }
   __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
-    sort_slots<A_SLOTS>(M->a_sid, M->a_fl, L.n_act, [&](int i, int b) {
+    sort_slots<A_SLOTS>(M->a_fl, L.n_act, [&](int j) { return M->a_src[j][t] & kStepMask; }, [&](int i, int b) {
       swp(M->a_key[i][t], M->a_key[b][t]); swp(M->a_src[i][t], M->a_src[b][t]);
       swp(M->a_cand[i][t], M->a_cand[b][t]);
     });
-    sort_slots<T_SLOTS>(M->t_sid, M->t_fl, L.n_timer, [&](int i, int b) {
+    sort_slots<T_SLOTS>(M->t_fl, L.n_timer, [&](int j) { return (M->t_fl[j][t] >> 8) & kStepMask; }, [&](int i, int b) {
       swp(M->t_exp[i][t], M->t_exp[b][t]); swp(M->t_key[i][t], M->t_key[b][t]);
     });
-    sort_slots<C_SLOTS>(M->c_id, M->c_fl, L.n_child, [&](int, int) {});
-    sort_slots<R_SLOTS>(M->r_id, M->r_fl, L.n_rc, [&](int, int) {});
-    sort_slots<S_SLOTS>(M->s_id, M->s_fl, L.n_sig, [&](int, int) {});
+    sort_slots<C_SLOTS>(M->c_fl, L.n_child, [&](int j) { return (M->c_fl[j][t] >> 8) & kStepMask; }, [&](int, int) {});
+    sort_slots<R_SLOTS>(M->r_fl, L.n_rc, [&](int j) { return (M->r_fl[j][t] >> 8) & kStepMask; }, [&](int, int) {});
+    sort_slots<S_SLOTS>(M->s_fl, L.n_sig, [&](int j) { return (M->s_fl[j][t] >> 8) & kStepMask; }, [&](int, int) {});
 
     for (i32 i = 0; i < L.n_act; ++i) {  // ReplicateActivityTask{Scheduled,Started,CancelRequested} images
       const u32 f = M->a_fl[i][t];
@@ -1418,7 +1504,7 @@ struct CompactTables {
       // the ActivityTaskScheduled event's own fields: timestamp, side record (timeouts)
       const crr_activity_side as = in->act_side[in->ev.aux[ix(ss)]];
       crr_activity_row r;
-      r.schedule_id = (i64)M->a_sid[i][t];
+      r.schedule_id = id_at((u32)ss);
       r.version = ev_ver(max(ss, max(started ? st : -1, cancel ? sc : -1)));  // last of Scheduled / Started / CancelRequested
       r.scheduled_batch_id = batch_first_id(ss);
       r.scheduled_time = ev_ts(ss);
@@ -1441,7 +1527,7 @@ struct CompactTables {
       const u32 f = M->t_fl[i][t];
       const i32 src = (i32)((f >> 8) & kStepMask);
       crr_timer_row r;
-      r.started_id = (i64)M->t_sid[i][t];
+      r.started_id = id_at((u32)src);
       r.version = ev_ver(src);
       r.expiry_time = M->t_exp[i][t];
       r.task_status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
@@ -1455,7 +1541,7 @@ struct CompactTables {
       const i32 src = (i32)((f >> 8) & kStepMask), sst = (i32)((f >> (8 + kStepBits)) & kStepMask);
       const bool started = sst != (i32)kStepMask;
       crr_child_row r;
-      r.initiated_id = (i64)M->c_id[i][t];
+      r.initiated_id = id_at((u32)src);
       r.version = ev_ver(src);
       r.initiated_batch_id = batch_first_id(src);
       r.started_id = started ? ev_id(sst) : CRR_EMPTY_EVENT_ID;
@@ -1468,7 +1554,7 @@ struct CompactTables {
     for (i32 i = 0; i < L.n_rc; ++i) {
       const i32 src = (i32)((M->r_fl[i][t] >> 8) & kStepMask);
       crr_initiated_row r;
-      r.initiated_id = (i64)M->r_id[i][t];
+      r.initiated_id = id_at((u32)src);
       r.version = ev_ver(src);
       r.initiated_batch_id = batch_first_id(src);
       r.src = src;
@@ -1478,7 +1564,7 @@ struct CompactTables {
     for (i32 i = 0; i < L.n_sig; ++i) {
       const i32 src = (i32)((M->s_fl[i][t] >> 8) & kStepMask);
       crr_initiated_row r;
-      r.initiated_id = (i64)M->s_id[i][t];
+      r.initiated_id = id_at((u32)src);
       r.version = ev_ver(src);
       r.initiated_batch_id = batch_first_id(src);
       r.src = src;
@@ -1495,11 +1581,11 @@ struct CompactTables {
       *G.rp(i) = r;
     }
   }
-  __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return (i64)M->t_sid[i][t]; }
-  __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return (i64)M->a_sid[i][t]; }
-  __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return (i64)M->s_id[i][t]; }
-  __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return (i64)M->r_id[i][t]; }
-  __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return (i64)M->c_id[i][t]; }
+  __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return id_at((M->t_fl[i][t] >> 8) & kStepMask); }
+  __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return id_at(M->a_src[i][t] & kStepMask); }
+  __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return id_at((M->s_fl[i][t] >> 8) & kStepMask); }
+  __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return id_at((M->r_fl[i][t] >> 8) & kStepMask); }
+  __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return id_at((M->c_fl[i][t] >> 8) & kStepMask); }
   // the general path replays a workflow this tier cannot hold: list 0 of the retry pass
   __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) {
     const u64 m = __builtin_amdgcn_ballot_w64(true);
@@ -2028,7 +2114,6 @@ struct WaveTables {
 // step s is processed.  WaveSource: one workflow per wavefront, 64 consecutive events are loaded per
 // column in one coalesced instruction (one event per lane, the next chunk one chunk ahead) and step s
 // is read out of lane s % 64 into scalar registers.
-struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
 
 // Lane per workflow: step k of this lane's workflow is column element begin + k * st.
 // Loads are typed: the event type of step s+1 is fetched one step ahead of its columns, so only the
@@ -2248,6 +2333,39 @@ __device__ __forceinline__ void close_tasks(Lane& L, const Geo& G, const TaskSin
   K.add(L, G, CRR_TASK_DELETE_HISTORY, 0, ver, add_seconds(ts, (i64)retention_days * 86400), 0, 0, s);
 }
 
+// Pending-map operations of the dispatch.  The 42-way switch below only decides which one an event
+// performs (after the checks that precede it in Go); the operation itself runs after the switch, at
+// one program point for every lane of the wavefront -- in a divergent wavefront (lane per workflow,
+// mixed event types) each map's code then runs once per step instead of once per event type that
+// touches it -- followed by what the transition does after it (its task, a late domain check).
+
+// A map operation through the policy's per-operation methods (a policy may fuse them instead:
+// P::kFusedMapOps, P::map_op)
+template <class P>
+__device__ __forceinline__ int map_op_by_method(P& T, Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s,
+                                                i64 batch_first_id, const crr_activity_side& as) {
+  switch (op) {
+    case MOP_ACT_INSERT: return T.act_insert(L, G, activity_row(ev, s, batch_first_id, as));
+    case MOP_ACT_START: return T.act_start(L, G, ev.ref, ev.id, ev.ver, s, ev.ts);
+    case MOP_ACT_DELETE: T.act_delete(L, G, ev.ref); return CRR_OK;
+    case MOP_ACT_CANCEL: T.act_cancel(L, G, ev.key, ev.id, ev.ver, s); return CRR_OK;
+    case MOP_TIMER_START: return T.timer_start(L, G, timer_row(ev, s));
+    case MOP_TIMER_DELETE: T.timer_delete(L, G, ev.key); return CRR_OK;
+    case MOP_CHILD_INSERT: return T.child_insert(L, G, child_row(ev, s, batch_first_id));
+    case MOP_CHILD_START: return T.child_start(L, G, ev.ref, ev.id, s);
+    case MOP_CHILD_DELETE: T.child_delete(L, G, ev.ref); return CRR_OK;
+    case MOP_RC_INSERT: return T.init_insert(L, G, true, initiated_row(ev, s, batch_first_id));
+    case MOP_RC_DELETE: T.init_delete(L, G, true, ev.ref); return CRR_OK;
+    case MOP_SIG_INSERT: return T.init_insert(L, G, false, initiated_row(ev, s, batch_first_id));
+    case MOP_SIG_DELETE: T.init_delete(L, G, false, ev.ref); return CRR_OK;
+    default: return CRR_OK;
+  }
+}
+template <class P, class = void>
+struct FusedMapOps { static constexpr bool value = false; };
+template <class P>
+struct FusedMapOps<P, decltype((void)P::kFusedMapOps)> { static constexpr bool value = P::kFusedMapOps; };
+
 // One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
 // code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
 template <class P>
@@ -2256,6 +2374,8 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
                                            const i64 now_ns, const TaskSink& K, const i32 retention_days) {
   const i64 id = ev.id;
   const i64 ver = ev.ver;
+  u32 op = MOP_NONE;
+  crr_activity_side as{};
 #define FAIL(code, step) return (code)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
     switch (t) {
@@ -2344,80 +2464,39 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
 #if CRR_EXP & 8
-        crr_activity_side as{10, 20, 30, 0, 0, 0, 1, 0};
+        as = crr_activity_side{10, 20, 30, 0, 0, 0, 1, 0};
 #else
-        const crr_activity_side as = in.act_side[ev.aux];
+        as = in.act_side[ev.aux];
 #endif
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-        crr_activity_row row;
-        row.schedule_id = id;
-        row.version = ver;
-        row.scheduled_batch_id = batch_first_id;
-        row.scheduled_time = ev.ts;
-        row.started_id = CRR_EMPTY_EVENT_ID;
-        row.started_time = CRR_ZERO_TIME;
-        row.cancel_request_id = CRR_EMPTY_EVENT_ID;
-        row.last_hb_timeout_vis_s = 0;
-        row.sched_src = s;
-        row.started_src = -1;
-        row.schedule_to_start = as.schedule_to_start;
-        row.schedule_to_close = as.schedule_to_close;
-        row.start_to_close = as.start_to_close;
-        row.heartbeat = as.heartbeat;
-        row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
-        row.key = ev.key;
-        row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
-        row.attempt = 0;
-        row.last_heartbeat_time = CRR_ZERO_TIME;
-        CHECK(T.act_insert(L, G, row));
-        K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks
+        op = MOP_ACT_INSERT;  // then GenerateActivityTransferTasks (below)
         break;
       }
       case CRR_EV_ACTIVITY_TASK_STARTED:  // :297-302 -> :2254-2276
-        CHECK(T.act_start(L, G, ev.ref, id, ver, s, ev.ts));
+        op = MOP_ACT_START;
         break;
       case CRR_EV_ACTIVITY_TASK_COMPLETED:
       case CRR_EV_ACTIVITY_TASK_FAILED:
       case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
       case CRR_EV_ACTIVITY_TASK_CANCELED:  // :304-337 -> DeleteActivity (:1310-1339)
-        T.act_delete(L, G, ev.ref);
+        op = MOP_ACT_DELETE;
         break;
       case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED:  // :325-330 -> :2444-2467
-        T.act_cancel(L, G, ev.key, id, ver, s);
+        op = MOP_ACT_CANCEL;
         break;
-      case CRR_EV_TIMER_STARTED: {  // :342-347 -> :3057-3081
-        crr_timer_row row;
-        row.started_id = id;
-        row.version = ver;
-        row.expiry_time = add_seconds(ev.ts, ev.ref);
-        row.task_status = CRR_TIMER_TASK_STATUS_NONE;
-        row.key = ev.key;
-        row.src = s;
-        row.flags = CRR_ROW_LIVE;
-        CHECK(T.timer_start(L, G, row));
+      case CRR_EV_TIMER_STARTED:  // :342-347 -> :3057-3081
+        op = MOP_TIMER_START;
         break;
-      }
       case CRR_EV_TIMER_FIRED:
       case CRR_EV_TIMER_CANCELED:  // :349-361 -> DeleteUserTimer (:1390-1419)
-        T.timer_delete(L, G, ev.key);
+        op = MOP_TIMER_DELETE;
         break;
-      case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: {  // :366-381 -> :3417-3453
+      case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:  // :366-381 -> :3417-3453
         if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-        crr_child_row row;
-        row.initiated_id = id;
-        row.version = ver;
-        row.initiated_batch_id = batch_first_id;
-        row.started_id = CRR_EMPTY_EVENT_ID;
-        row.src = s;
-        row.started_src = -1;
-        row.flags = CRR_ROW_LIVE;
-        row.reserved = 0;
-        CHECK(T.child_insert(L, G, row));
-        K.add(L, G, CRR_TASK_START_CHILD, 0, ver, 0, id, 0, s);  // GenerateChildWorkflowTasks
+        op = MOP_CHILD_INSERT;  // then GenerateChildWorkflowTasks (below)
         break;
-      }
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:  // :390-395 -> :3485-3507
-        CHECK(T.child_start(L, G, ev.ref, id, s));
+        op = MOP_CHILD_START;
         break;
       case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
@@ -2425,30 +2504,21 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED:  // DeletePendingChildExecution (:1160-1178)
-        T.child_delete(L, G, ev.ref);
+        op = MOP_CHILD_DELETE;
         break;
-      case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
-      case CRR_EV_SIGNAL_EXTERNAL_INITIATED: {  // :432-447 / :463-478 -> :2760-2779 / :2883-2905
-        crr_initiated_row row;
-        row.initiated_id = id;
-        row.version = ver;
-        row.initiated_batch_id = batch_first_id;
-        row.src = s;
-        row.flags = CRR_ROW_LIVE;
-        CHECK(T.init_insert(L, G, t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED, row));
-        // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
-        if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-        K.add(L, G, t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0,
-              ver, 0, id, 0, s);
+      case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:  // :432-447 -> :2760-2779 (then its task, below)
+        op = MOP_RC_INSERT;
         break;
-      }
+      case CRR_EV_SIGNAL_EXTERNAL_INITIATED:  // :463-478 -> :2883-2905
+        op = MOP_SIG_INSERT;
+        break;
       case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
       case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:  // DeletePendingRequestCancel (:1181-1199)
-        T.init_delete(L, G, true, ev.ref);
+        op = MOP_RC_DELETE;
         break;
       case CRR_EV_SIGNAL_EXTERNAL_FAILED:
       case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:  // DeletePendingSignal (:1202-1220)
-        T.init_delete(L, G, false, ev.ref);
+        op = MOP_SIG_DELETE;
         break;
       case CRR_EV_WORKFLOW_EXECUTION_SIGNALED:  // :497-502 -> :3260-3267
         L.signal_count = (i32)((u32)L.signal_count + 1u);
@@ -2493,6 +2563,20 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
       default:  // :629-630
         FAIL(CRR_ERR_UNKNOWN_EVENT_TYPE, s);
     }
+  if (op != MOP_NONE && !(CRR_EXP & 256)) {
+    if constexpr (FusedMapOps<P>::value) CHECK(T.map_op(L, G, op, ev, s, batch_first_id, as));
+    else CHECK(map_op_by_method(T, L, G, op, ev, s, batch_first_id, as));
+    // what the transition does after its map operation
+    if (op == MOP_ACT_INSERT) {
+      K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks
+    } else if (op == MOP_CHILD_INSERT) {
+      K.add(L, G, CRR_TASK_START_CHILD, 0, ver, 0, id, 0, s);  // GenerateChildWorkflowTasks
+    } else if (op == MOP_RC_INSERT || op == MOP_SIG_INSERT) {
+      // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
+      if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
+      K.add(L, G, op == MOP_RC_INSERT ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0, ver, 0, id, 0, s);
+    }
+  }
 #undef CHECK
 #undef FAIL
   return CRR_OK;
@@ -2711,7 +2795,7 @@ done_events:
     it->event_id = L.vh_last_id;
     it->version = L.vh_last_ver;
   }
-  T.finalize(L, G);
+  if (!(CRR_EXP & 512)) T.finalize(L, G);
 
   crr_exec_row R;
   R.status = L.status;
@@ -2931,8 +3015,8 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
     replay_body<true>(in, out, w, wfp, G, H, S2, crc_tables);
   }
 }
-// Wide segment (CRR_IN_TIERED): lane workflows [lo, hi) whose live sets the host expects to outgrow
-// the 2-slot LDS tier.
+// Wide segment (CRR_IN_TIERED [hbm_begin, lanes)): lane workflows whose live sets the host expects to
+// outgrow the compact tiers, and loaded states (CRR_WF_FLAG_RESUME: continued in place over their rows).
 #ifndef CRR_WIDE_GLOBAL
 #define CRR_WIDE_GLOBAL 1
 #endif
@@ -2977,11 +3061,12 @@ __global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outp
   replay_lane_item(in, out, phase, w, &arena, crc_tables);
 }
 #endif
-// Compact LDS tiers (CRR_IN_TIERED segments [compact_begin, compact2_begin) and [compact2_begin,
-// wide_begin)): lane per workflow, 64 lanes per block; slot counts per map chosen by the host's live-set
-// bounds (flatten.COMPACT_TIERS).  A workflow that outgrows its tier goes to the retry pass (list 0).
+// Compact LDS tiers (CRR_IN_TIERED segments [compact_begin, compact2_begin), [compact2_begin,
+// wide_begin) and [wide_begin, hbm_begin)): lane per workflow, 64 lanes per block; slot counts per map
+// chosen by the host's live-set bounds (flatten.TIER_SLOTS).  A workflow that outgrows its tier goes to the retry pass (list 0).
 using CompactTier1 = CTier<4, 3, 2, 1, 1, 4, 64>;
 using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
+using CompactTier3 = CTier<16, 12, 8, 6, 6, 10, 64>;
 template <class TIER, bool EMIT>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   __shared__ CompactArena<TIER> arena;
@@ -3025,6 +3110,14 @@ template __global__ void replay_compact1_kernel<false>(crr_inputs, crr_outputs, 
 template __global__ void replay_compact1_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact2_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact2_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
+// tier 3 (workflows beyond tier 2 that hold no loaded state): 55-KB blocks, 2 per CU -- a segment of a
+// few hundred wavefronts, so what matters is its per-event latency (LDS, not the HBM rows' round trips)
+template <bool EMIT>
+__global__ void __launch_bounds__(64, 1) replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_compact<CompactTier3, EMIT>(in, out, phase, lo, hi);
+}
+template __global__ void replay_compact3_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact3_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
 // Long-tail workflows the host expects to outgrow the fast kernels' per-wave arenas
 // (CRR_IN_TIERED, [big_begin, n_wf)): one wavefront each with the 57 KB row arena, then HBM rows;
 // launched next to the fast kernels, so the longest of them is not replayed after them.

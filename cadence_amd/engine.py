@@ -131,7 +131,8 @@ class ReplayEngine:
         ci.big_begin = batch.n_wf
         if batch.tiers is not None:
             # segments by expected live-set size; LDS_SMALL then only places the wave tail
-            ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin, ci.big_begin = batch.tiers
+            (ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin, ci.hbm_begin,
+             ci.big_begin) = batch.tiers
             if fits_small_tier(batch, lanes=False):
                 ci.flags |= abi.IN_LDS_SMALL
         elif batch.stride == 64 and fits_small_tier(batch):

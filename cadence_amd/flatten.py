@@ -45,10 +45,10 @@ class HistoryBatch:
     wave_begin: Optional[int] = None
     # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
     emit_tasks: bool = False
-    # CRR_IN_TIERED: (large_begin, compact_begin, compact2_begin, wide_begin, big_begin) -- lane
-    # workflows ordered by expected live-set size (TIER_SLOTS); long-tail workflows no fast per-wave
-    # arena is expected to hold from big_begin on
-    tiers: Optional[Tuple[int, int, int, int, int]] = None
+    # CRR_IN_TIERED: (large_begin, compact_begin, compact2_begin, wide_begin, hbm_begin, big_begin) --
+    # lane workflows ordered by expected live-set size (TIER_SLOTS, then HBM rows); long-tail workflows
+    # no fast per-wave arena is expected to hold from big_begin on
+    tiers: Optional[Tuple[int, int, int, int, int, int]] = None
     # CRR_WF_FLAG_RESUME: the loaded mutable states (batch order) the output rows start from
     init: Optional["LoadedStates"] = None
     # per-workflow key id -> string tables (batch order): (begin, count, off, len, arena), the strings of
@@ -421,16 +421,20 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     counts = batch.wf["ev_count"].astype(np.int64)
     order = np.lexsort((np.arange(n), -counts)).astype(np.int64)
     is_long = counts[order] > long_threshold if long_threshold is not None else np.zeros(n, bool)
-    lanes = order[~is_long]
-    longs = order[is_long]
     bounds = live_set_bounds(batch) if (tiered and n) else None
     tier = tier_classes(batch, bounds) if (tiered and n) else np.zeros(n, np.int64)
     if tiered and n:
+        resumed = (batch.wf["flags"] & abi.WF_FLAG_RESUME) != 0
+        # a short history whose live sets outgrow every compact tier joins the wave tail (one
+        # wavefront, a row arena searched by 64 lanes) rather than a lane over HBM rows
+        if long_threshold is not None:
+            is_long |= (tier[order] == WIDE) & ~resumed[order]
         # a loaded state is continued in place over its HBM rows: the wide (GlobalTables) segment, and
         # in the long tail the replay_big_kernel segment (whose HBM-row pass continues it)
-        resumed = (batch.wf["flags"] & abi.WF_FLAG_RESUME) != 0
         tier = np.where(resumed, WIDE, tier)
         bounds = {k: np.where(resumed, np.iinfo(np.int32).max, v) for k, v in bounds.items()}
+    lanes = order[~is_long]
+    longs = order[is_long]
     n_big = 0
     if tiered:
         lanes = lanes[np.argsort(tier[lanes], kind="stable")]    # by tier, then longest first
@@ -582,8 +586,10 @@ LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # 
 # replay_kernel.hip CompactTier1 / CompactTier2 (u32 event IDs, 10-bit event steps: <= 1023 events)
 COMPACT1_TIER = {"act": 4, "timer": 3, "child": 2, "rc": 1, "sig": 1, "rp": 4}
 COMPACT2_TIER = {"act": 8, "timer": 6, "child": 3, "rc": 3, "sig": 3, "rp": 8}
+COMPACT3_TIER = {"act": 16, "timer": 12, "child": 8, "rc": 6, "sig": 6, "rp": 10}
 COMPACT_MAX_EVENTS = 1023
-TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER]   # tier classes 0..3; WIDE: HBM rows
+# tier classes 0..4; WIDE: HBM rows
+TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER, COMPACT3_TIER]
 WIDE = len(TIER_SLOTS)
 
 

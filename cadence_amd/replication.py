@@ -139,6 +139,7 @@ class PassiveReplication:
         # segment, the long tail in the tail / big kernels (their HBM-row pass resumes)
         if sb.tiers is not None:
             dn.c_in.large_begin = dn.c_in.compact_begin = dn.c_in.compact2_begin = dn.c_in.wide_begin = 0
+            dn.c_in.hbm_begin = 0
             dn.c_in.flags &= ~abi.IN_LDS_SMALL
         for name, *_ in abi.TABLES:                # only db's outputs are used
             dn.tensors.pop("out_" + name, None)

@@ -285,7 +285,10 @@ typedef struct crr_inputs {
          [large_begin, compact_begin)   <= 2 activities / timers / reset points (2-slot LDS tier)
          [compact_begin, compact2_begin) compact tier 1 (4 / 3 / 2 / 1 / 1 / 4 slots)
          [compact2_begin, wide_begin)    compact tier 2 (8 / 6 / 3 / 3 / 3 / 8 slots)
-         [wide_begin, lanes)             more: the workflow's own HBM rows
+         [wide_begin, hbm_begin)         compact tier 3 (16 / 12 / 8 / 6 / 6 / 10 slots)
+         [hbm_begin, lanes)              more, or a loaded state (CRR_WF_FLAG_RESUME): the workflow's
+                                         own HBM rows
+       (hbm_begin below wide_begin, e.g. 0, reads as wide_begin: no compact tier 3 segment)
        (activity / timer / child / request-cancel / signal / reset-point slots; flatten.py) */
     uint32_t                 large_begin;
     uint32_t                 compact_begin;
@@ -294,7 +297,7 @@ typedef struct crr_inputs {
     uint32_t                 big_begin;    /* long-tail workflows [big_begin, n_wf) are expected to outgrow
                                               the fast kernels' per-wave arenas (replayed concurrently
                                               with the 57-KB arena); n_wf: none */
-    uint32_t                 reserved;
+    uint32_t                 hbm_begin;
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */

@@ -155,11 +155,12 @@ def test_replay_rejects_unaligned_tier_segments():
         setattr(ci, f, dummy.value)
     ci.n_wf, ci.stride, ci.flags = 1000, 64, abi.IN_TIERED
     co = abi.COutputs(*([dummy.value] * len(abi.COutputs._fields_)))
-    for bnd in ((100, 1000, 1000, 1000), (128, 130, 1000, 1000), (3, 3, 3, 3), (128, 128, 192, 200)):
-        ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin = bnd
+    for bnd in ((100, 1000, 1000, 1000, 1000), (128, 130, 1000, 1000, 1000), (3, 3, 3, 3, 3), (128, 128, 192, 200, 1000),
+                (128, 128, 192, 256, 300)):
+        ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin, ci.hbm_begin = bnd
         assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1, bnd
     ci.stride = 1                        # tier segments are a stride-64 layout only
-    ci.large_begin = ci.compact_begin = ci.compact2_begin = ci.wide_begin = 1000
+    ci.large_begin = ci.compact_begin = ci.compact2_begin = ci.wide_begin = ci.hbm_begin = 1000
     assert lib.crr_replay(ctypes.byref(ci), ctypes.byref(co), None) == -1
 
 
@@ -197,9 +198,9 @@ def test_interleave_tier_segments():
     cnt = ib.wf["ev_count"]
     assert nl <= bb <= ib.n_wf
     assert (np.diff(cnt[nl:bb]) <= 0).all() and (np.diff(cnt[bb:]) <= 0).all()
-    for k in range(5):
+    for k in range(6):
         seg = cnt[:nl][c == k]
         assert (np.diff(seg) <= 0).all()
     # one tier only: no segments beyond the lanes
     ic = interleave(synth.activity_chain(1000, 2, 3))
-    assert ic.tiers == (ic.n_wf,) * 5
+    assert ic.tiers == (ic.n_wf,) * 6

@@ -33,6 +33,9 @@ constexpr int kBlock = 256;
 #ifndef CRR_WIDE_GLOBAL
 #define CRR_WIDE_GLOBAL 1
 #endif
+#ifndef CRR_TAIL_CRC  // as in replay_kernel.hip: the tail kernel's checksums come from a fill pass
+#define CRR_TAIL_CRC 0
+#endif
 constexpr int kWideBlock = CRR_WIDE_GLOBAL ? 256 : 64;  // replay_wide_kernel's block
 constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
 
@@ -224,6 +227,11 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_tail) {  // the long-history tail, one wavefront each
           if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+#if !CRR_TAIL_CRC
+          // the tail kernel holds no CRC tables (a third wave per SIMD): checksums in a fill pass
+          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((tail_end - n_lane + kBlock - 1) / kBlock), dim3(kBlock), 0, s_tail,
+                             *in, *out, phase, n_lane, tail_end);
+#endif
         }
         if (run_c3) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact3_kernel<true>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);

@@ -21,6 +21,7 @@
 // workflowExecutionInfo.go and execution/checksum.go.
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "cadence_replay.h"
@@ -28,7 +29,7 @@
 // Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
 // checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
 // record loads, bit 16 the start side record loads, bit 256 the pending-map operations of the dispatch
-// (MOP_*).  Bit 128 keeps outputs valid and counts shader
+// (MOP_*), bit 1024 the compact tiers' ActivityTaskStarted re-reads of the scheduled event.  Bit 128 keeps outputs valid and counts shader
 // cycles per event type in the one-wavefront-per-workflow path (crr_debug_cycles).
 #ifndef CRR_EXP
 #define CRR_EXP 0
@@ -1187,6 +1188,9 @@ struct CompactTables {
   i64 id0 = 0;
   bool have_id0 = false;
   bool retried = false;
+  // a map changed since its last batch epilogue; an unchanged map would select the same, already
+  // created, timer again (a no-op), so its epilogue is skipped (as WaveTables)
+  bool dirty_act = false, dirty_timer = false;
   __device__ __forceinline__ void load(Lane&, const Geo&) {}
 
   __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin) {
@@ -1246,12 +1250,156 @@ struct CompactTables {
 
   // Map operations (apply_event runs them after its switch, every lane at once): one pass over a map's
   // slots finds the entry an operation addresses and the first free slot, then the operation's writes.
-  __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 /*bfid*/,
+#ifndef CRR_COMPACT_UNIFIED
+#define CRR_COMPACT_UNIFIED 1
+#endif
+  __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 bfid,
                                         const crr_activity_side& as) {
+#if CRR_COMPACT_UNIFIED
+    return map_op_unified(L, G, op, ev, s, as);
+#else
     if (op <= MOP_ACT_CANCEL) return act_op(L, G, op, ev, s, as);
     if (op <= MOP_TIMER_DELETE) return timer_op(L, G, op, ev, s);
     if (op <= MOP_CHILD_DELETE) return child_op(L, G, op, ev, s);
     return init_op(L, G, op, ev, s);
+#endif
+  }
+  // One code path for every map operation, so a divergent wavefront (lanes with different event types)
+  // runs one slot scan and one write-back per step instead of one per map and operation: each lane
+  // picks its map's flag and lookup words (LDS addresses), lookup value and slot count, and the
+  // operations differ only in the words they write.  Same results as act_op / timer_op / child_op /
+  // init_op (the per-map forms, CRR_COMPACT_UNIFIED=0).
+  __device__ __forceinline__ int map_op_unified(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s,
+                                                const crr_activity_side& as) {
+    const bool is_act = op <= MOP_ACT_CANCEL;
+    const bool is_timer = op == MOP_TIMER_START || op == MOP_TIMER_DELETE;
+    const bool is_child = op >= MOP_CHILD_INSERT && op <= MOP_CHILD_DELETE;
+    const bool is_rc = op == MOP_RC_INSERT || op == MOP_RC_DELETE;
+    const bool act_by_id = op == MOP_ACT_START || op == MOP_ACT_DELETE;
+    const bool act_by_key = op == MOP_ACT_INSERT || op == MOP_ACT_CANCEL;
+    const bool by_step = act_by_id || (!is_act && !is_timer);  // ScheduleID / InitiatedID lookups
+    const bool insert = op == MOP_ACT_INSERT || op == MOP_TIMER_START || op == MOP_CHILD_INSERT ||
+                        op == MOP_RC_INSERT || op == MOP_SIG_INSERT;
+    const bool del = op == MOP_ACT_DELETE || op == MOP_TIMER_DELETE || op == MOP_CHILD_DELETE ||
+                     op == MOP_RC_DELETE || op == MOP_SIG_DELETE;
+    // word offsets into the arena (one index off M keeps the accesses in LDS; a select between
+    // pointers would turn them into flat accesses)
+    constexpr u32 kW = sizeof(u32);
+    const u32 fo = (is_act ? (u32)offsetof(Arena, a_fl) : is_timer ? (u32)offsetof(Arena, t_fl)
+                  : is_child ? (u32)offsetof(Arena, c_fl) : is_rc ? (u32)offsetof(Arena, r_fl) : (u32)offsetof(Arena, s_fl)) / kW + t;
+    const u32 co = act_by_id ? (u32)offsetof(Arena, a_src) / kW + t : act_by_key ? (u32)offsetof(Arena, a_key) / kW + t
+                 : is_timer ? (u32)offsetof(Arena, t_key) / kW + t : fo;
+    u32* const W = reinterpret_cast<u32*>(M);
+    u32* fl = W + fo;
+    const u32* cmp = W + co;
+    const i32 n = is_act ? A_SLOTS : is_timer ? T_SLOTS : is_child ? C_SLOTS : is_rc ? R_SLOTS : S_SLOTS;
+    const u32 need = act_by_key ? (CRR_ROW_LIVE | CRR_ROW_MAPPED) : CRR_ROW_LIVE;
+    const u32 sh = (by_step && !is_act) ? 8u : 0u;
+    const u32 msk = by_step ? kStepMask : 0xFFFFFFFFu;
+    // inserts of children / request-cancels / signals look nothing up (kStepMask matches no entry)
+    const u32 want = by_step ? (insert ? kStepMask : step_of(ev.ref)) : ev.key;
+    constexpr int kMax = A_SLOTS > T_SLOTS ? A_SLOTS : T_SLOTS;
+    static_assert(kMax >= C_SLOTS && kMax >= R_SLOTS && kMax >= S_SLOTS, "activity or timer map is the largest");
+    i32 hit = -1, fr = -1;
+#pragma unroll
+    for (int j = kMax - 1; j >= 0; --j) {
+      if (j < n) {
+        const u32 f = fl[j * LANES];
+        const u32 v = cmp[j * LANES];
+        if ((f & need) == need && ((v >> sh) & msk) == want) hit = j;
+        if (!(f & CRR_ROW_LIVE)) fr = j;
+      }
+    }
+    i32 d = 0;  // change of the map's live count
+    int rc = CRR_OK;
+    if (del) {
+      if (hit < 0) {
+        ++L.inconsistencies;
+      } else {
+        const u32 f = fl[hit * LANES];
+        fl[hit * LANES] = 0;
+        d = -1;
+        if (is_act && !(f & CRR_ROW_MAPPED)) {  // DeleteActivity of an entry another one's ActivityID shadows
+          const i32 m = find_act_mapped(M->a_key[hit][t]);
+          if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+          else ++L.inconsistencies;
+        }
+      }
+    } else if (insert) {
+      // TimerStarted of a live TimerID overwrites it in place (:3057-3081)
+      const bool grow = !(is_timer && hit >= 0);
+      const i32 j = grow ? fr : hit;
+      // values, not lvalues: a conditional over the members would select their addresses and keep
+      // Geo (and the output pointers in it) in scratch memory
+      const i32 ca = G.act_cap, ct = G.timer_cap, cc = G.child_cap, cr = G.rc_cap, cs = G.sig_cap;
+      const i32 cap = is_act ? ca : is_timer ? ct : is_child ? cc : is_rc ? cr : cs;
+      if (!insert_ok(ev.id, s) || j < 0) {
+        rc = CRR_INTERNAL_RETRY;
+      } else if (grow && j >= cap) {
+        rc = CRR_ERR_CAPACITY;
+      } else {
+        u32 nf = CRR_ROW_LIVE | ((u32)s << 8) | (is_child ? (kStepMask << (8 + kStepBits)) : 0u);
+        if (is_act) {
+          if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
+          // not started: ScheduleToClose and ScheduleToStart
+          i64 ct = add_seconds(ev.ts, as.schedule_to_close);
+          i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+          cand_min(ct, cy, add_seconds(ev.ts, as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+          nf = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u) | ((u32)cy << CF_CAND_SHIFT);
+          M->a_key[j][t] = ev.key;
+          M->a_src[j][t] = (u32)s | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
+          M->a_cand[j][t] = ct;
+        } else if (is_timer) {
+          M->t_exp[j][t] = add_seconds(ev.ts, ev.ref);
+          M->t_key[j][t] = ev.key;
+        }
+        fl[j * LANES] = nf;
+        d = grow ? 1 : 0;
+      }
+    } else if (op == MOP_ACT_START) {  // :2254-2276
+      rc = CRR_ERR_MISSING_ACTIVITY_INFO;
+      if (hit >= 0) rc = act_started(hit, ev, s);
+    } else if (op == MOP_CHILD_START) {  // :3485-3507
+      rc = CRR_ERR_MISSING_CHILD_INFO;
+      if (hit >= 0) {
+        const u32 f = fl[hit * LANES];
+        fl[hit * LANES] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
+        rc = CRR_OK;
+      }
+    } else if (hit >= 0) {  // MOP_ACT_CANCEL (:2444-2467)
+      M->a_fl[hit][t] |= CRR_ROW_CANCEL_REQUESTED;
+      const u32 w = M->a_src[hit][t];
+      M->a_src[hit][t] = (w & ~(kStepMask << (2 * kStepBits))) | ((u32)s << (2 * kStepBits));
+    }
+    dirty_act |= is_act && op != MOP_ACT_CANCEL;  // a cancel request changes no timer candidate
+    dirty_timer |= is_timer;
+    L.n_act += is_act ? d : 0;
+    L.n_timer += is_timer ? d : 0;
+    L.n_child += is_child ? d : 0;
+    L.n_rc += is_rc ? d : 0;
+    L.n_sig += (!is_act && !is_timer && !is_child && !is_rc) ? d : 0;
+    return rc;
+  }
+  // ActivityTaskStarted on live entry j: its cached earliest timer candidate becomes the started set's
+  __device__ __forceinline__ int act_started(i32 hit, const Ev& ev, i32 s) {
+    const u32 f = M->a_fl[hit][t];
+    if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
+    const u32 w = M->a_src[hit][t];
+#if CRR_EXP & 1024
+    const crr_activity_side sa{10, 20, 30, 0, 0, 0, 1, 0};
+    i64 ct = add_seconds(ev.ts, sa.schedule_to_close);
+#else
+    const i64 six = ix((i32)step_field(w, 0));
+    const crr_activity_side sa = in->act_side[in->ev.aux[six]];
+    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
+#endif
+    i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+    cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+    if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
+    M->a_cand[hit][t] = ct;
+    M->a_fl[hit][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
+    M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
+    return CRR_OK;
   }
   // ActivityTaskScheduled / Started / closes / CancelRequested: the live entry with ScheduleID == ref
   // (start, delete) or the mapped live entry with ActivityID == key (insert, cancel), and the first free
@@ -1291,9 +1439,14 @@ struct CompactTables {
       // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime; the
       // scheduled time and timeouts are re-read from the ActivityTaskScheduled event (not kept in LDS)
       const u32 w = M->a_src[hit][t];
+#if CRR_EXP & 1024
+      const crr_activity_side sa{10, 20, 30, 0, 0, 0, 1, 0};
+      i64 ct = add_seconds(ev.ts, sa.schedule_to_close);
+#else
       const i64 six = ix((i32)step_field(w, 0));
       const crr_activity_side sa = in->act_side[in->ev.aux[six]];
       i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
+#endif
       i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
       cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
       if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
@@ -1426,7 +1579,10 @@ struct CompactTables {
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199) over the cached heads
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
-    if (L.n_act > 0) {
+#if !CRR_COMPACT_UNIFIED
+    dirty_act = dirty_timer = true;
+#endif
+    if (L.n_act > 0 && dirty_act) {
       BestTimer B;
 #pragma unroll
       for (int j = 0; j < A_SLOTS; ++j) {
@@ -1440,7 +1596,8 @@ struct CompactTables {
         K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
       }
     }
-    if (L.n_timer > 0) {
+    dirty_act = false;
+    if (L.n_timer > 0 && dirty_timer) {
       BestTimer B;
 #pragma unroll
       for (int j = 0; j < T_SLOTS; ++j) {
@@ -1453,6 +1610,7 @@ struct CompactTables {
         K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
       }
     }
+    dirty_timer = false;
   }
   __device__ __forceinline__ bool task_writer() const { return true; }
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
@@ -1461,6 +1619,7 @@ struct CompactTables {
     for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] &= ~(0xFu << LF_TTS_SHIFT);
 #pragma unroll
     for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] &= ~TF_CREATED;
+    dirty_act = dirty_timer = true;
     epilogue(L, G, TaskSink{false, false});
   }
 
@@ -2983,7 +3142,7 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 // Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
 // the list counters, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
-template <class ST, bool EMIT = true>
+template <class ST, bool EMIT = true, bool CRC = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  WaveTables<ST>& T, const u32* crc_tables) {
   const crr_workflow* wfp = in.wf + w;
@@ -2995,7 +3154,7 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT, WaveTables<ST>, WaveSource, CRC>(in, out, w, wfp, G, T, S, crc_tables);
 }
 __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  LdsArena<HugeTier>* arena, const u32* crc_tables) {
@@ -3136,36 +3295,55 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
   }
 }
 // Long-history tail of a CRR_IN_TIERED batch ([wave_begin, big_begin), longest first): one wavefront
-// per workflow with its rows in registers, no LDS arena, so occupancy is register-limited and the
-// tail's wavefronts all run at once; a workflow that outgrows 64 slots (or resumes a loaded state)
-// is replayed again over its HBM rows.
+// per workflow over a 12-KB LDS row arena; a workflow that outgrows it (or resumes a loaded state) is
+// replayed again over its HBM rows in the same wavefront.  The checksum is left to checksum_fill_kernel
+// over the segment (CRR_TAIL_CRC=0): without the 8-KB CRC tables 13 blocks fit a CU, so with <= 168
+// VGPRs the tail runs 3 waves per SIMD -- 3072 at once, enough for config 4's tail in one round.
 #ifndef CRR_TAIL_WAVES_PER_EU
-#define CRR_TAIL_WAVES_PER_EU 2
+#define CRR_TAIL_WAVES_PER_EU 3
 #endif
 #ifndef CRR_TAIL_LDS
 #define CRR_TAIL_LDS 1
 #endif
+#ifndef CRR_TAIL_CRC
+#define CRR_TAIL_CRC 0
+#endif
+#ifndef CRR_TAIL_INPLACE
+#define CRR_TAIL_INPLACE 1
+#endif
 template <bool EMIT>
 __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(crr_inputs in, crr_outputs out, int phase,
                                                                              u32 lo, u32 hi) {
+#if CRR_TAIL_CRC
   __shared__ u32 crc_tables[8 * 256];
+#else
+  constexpr u32* crc_tables = nullptr;
+#endif
 #if CRR_TAIL_LDS
   __shared__ WaveTier<LargeTier>::Arena arena;
 #endif
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
+#if CRR_TAIL_CRC
   build_crc_tables(crc_tables);
+#endif
 #if CRR_TAIL_LDS
+#if CRR_TAIL_INPLACE
   WaveTables<LdsRows<WaveTier<LargeTier>::Arena, -1>> T;
+#else
+  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, 1>> T;  // outgrown: the retry pass's wave list
+#endif
   T.S.M = &arena;
 #else
   WaveTables<RegRows> T;
 #endif
-  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables);
+  replay_wave_item<decltype(T.S), EMIT, CRR_TAIL_CRC>(in, out, phase, w, T, crc_tables);
+#if CRR_TAIL_INPLACE || !CRR_TAIL_LDS
   if (T.retried) {
     WaveTables<HbmRows> H;
-    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables);
+    replay_wave_item<HbmRows, EMIT, CRR_TAIL_CRC>(in, out, phase, w, H, crc_tables);
   }
+#endif
 }
 template __global__ void replay_tail_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_tail_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);

@@ -33,6 +33,9 @@ constexpr int kBlock = 256;
 #ifndef CRR_WIDE_GLOBAL
 #define CRR_WIDE_GLOBAL 1
 #endif
+#ifndef CRR_SEG_PRIORITY
+#define CRR_SEG_PRIORITY 1
+#endif
 #ifndef CRR_TAIL_CRC  // as in replay_kernel.hip: the tail kernel's checksums come from a fill pass
 #define CRR_TAIL_CRC 0
 #endif
@@ -81,14 +84,30 @@ struct SideStreams {
   int device = -1;
 };
 thread_local SideStreams g_side;
+// Diagnostics (crr_segment_timing): when each side stream's tier segments of the last phase-1 launch
+// group finished, relative to the fork -- which segment is the critical path of the concurrent launch.
+struct SegmentTiming {
+  bool on = false, valid = false;
+  int device = -1;
+  hipEvent_t start = nullptr, end[kSide + 1] = {};
+};
+thread_local SegmentTiming g_seg;
 
 bool ensure_side_streams() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (g_side.device == dev) return true;
   if (g_side.device >= 0) return false;  // one device per thread (crr_set_device): keep it simple
-  for (auto& x : g_side.st)
-    if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return false;
+  // the segments with the longest-running wavefronts (compact tiers 2 and 3: their blocks hold the
+  // most LDS per lane, so the fewest fit a CU) are the critical path of the group: their streams get
+  // the higher priority, so their workgroups are dispatched first and the short, dense segments fill
+  // the CUs around them instead of ahead of them
+  int lo_prio = 0, hi_prio = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
+  for (int i = 0; i < kSide; ++i) {
+    const int prio = (CRR_SEG_PRIORITY && (i == 1 || i == 4)) ? hi_prio : lo_prio;
+    if (hipStreamCreateWithPriority(&g_side.st[i], hipStreamNonBlocking, prio) != hipSuccess) return false;
+  }
   if (hipEventCreateWithFlags(&g_side.fork, hipEventDisableTiming) != hipSuccess) return false;
   for (auto& e : g_side.join)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
@@ -155,6 +174,27 @@ size_t crr_sizeof(int which) {
 
 int crr_set_device(int device) { return (int)hipSetDevice(device); }
 
+int crr_segment_timing(int on) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (on && g_seg.device != dev) {
+    if (hipEventCreate(&g_seg.start) != hipSuccess) return -1;
+    for (auto& e : g_seg.end)
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+    g_seg.device = dev;
+  }
+  g_seg.on = on != 0;
+  g_seg.valid = false;
+  return 0;
+}
+
+int crr_segment_ms(float* out, int n) {
+  if (!g_seg.valid || n < kSide + 1) return -1;
+  for (int i = 0; i <= kSide; ++i)
+    if (hipEventElapsedTime(&out[i], g_seg.start, g_seg.end[i]) != hipSuccess) return -1;
+  return kSide + 1;
+}
+
 int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   if (!valid_inputs(in, out)) return -1;
   if (in->n_wf == 0) return 0;
@@ -218,6 +258,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
         hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s, s_tail = fork ? g_side.st[5] : s;
         if (fork) {
+          if (g_seg.on && phase == 1 && g_seg.device >= 0) (void)hipEventRecord(g_seg.start, s);
           (void)hipEventRecord(g_side.fork, s);
           for (hipStream_t x : g_side.st) (void)hipStreamWaitEvent(x, g_side.fork, 0);
         }
@@ -256,6 +297,12 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         launch_fast(s_large, false, false, lb, cb);
         launch_fast(s, true, false, 0, lb);
         if (fork) {
+          const bool seg = g_seg.on && phase == 1 && g_seg.device >= 0;
+          if (seg) {
+            for (int i = 0; i < kSide; ++i) (void)hipEventRecord(g_seg.end[i], g_side.st[i]);
+            (void)hipEventRecord(g_seg.end[kSide], s);
+            g_seg.valid = true;
+          }
           for (int i = 0; i < kSide; ++i) {
             (void)hipEventRecord(g_side.join[i], g_side.st[i]);
             (void)hipStreamWaitEvent(s, g_side.join[i], 0);

@@ -34,9 +34,13 @@
 #ifndef CRR_EXP
 #define CRR_EXP 0
 #endif
-#if CRR_EXP & 128
+#if CRR_EXP & (128 | 2048)
 // [part][event type]: part 0 prologue, 1 dispatch, 2 batch epilogue, 3 events; [4][0..2] workflow
-// cycles, workflows, cycles from the end of the event loop (finalize + checksum + row write)
+// cycles, workflows, cycles from the end of the event loop (finalize + checksum + row write).
+// Bit 2048 (lane-per-workflow kernels with LDS tiers, per wavefront): [8 * tier + k], tier by the
+// activity slot count (1, 2, 4, 8, 16 -> 0..4), k: 0 step prologue (column wait + version history),
+// 1 dispatch incl. map operation, 2 batch epilogue, 3 whole event loop, 4 after the loop, 5 wavefronts,
+// 6 steps (wavefront iterations), 7 map operations (part of 1)
 __device__ unsigned long long crr_dbg[5 * 64];
 #endif
 #ifndef CRR_LDS_ACT
@@ -183,6 +187,9 @@ struct Lane {
   i32 n_tasks;                  // transfer / timer tasks generated (CRR_IN_EMIT_TASKS)
   i64 expiration_ns;            // executionInfo.ExpirationTime (0: unset)
   i32 src_base;                 // provenance offset of this call's steps (the resumed row's src_next; 0 fresh)
+#if CRR_EXP & 2048
+  u64 dbg_t;                    // cycle counter where apply_event's map operation begins
+#endif
 };
 
 // Where this lane's output rows live in HBM: row(table, slot) = base + slot * stride.
@@ -1582,32 +1589,57 @@ struct CompactTables {
 #if !CRR_COMPACT_UNIFIED
     dirty_act = dirty_timer = true;
 #endif
+    // The order is (time, event ID, timer type); IDs are id0 + step, so steps order them, and each
+    // activity's entry is already its own earliest candidate, so (time, step) decides -- 32-bit step
+    // compares and selects, the winner's type and created bit read once afterwards.
     if (L.n_act > 0 && dirty_act) {
-      BestTimer B;
+      bool have = false;
+      i64 bt = 0;
+      u32 bs = 0;
+      i32 bj = 0;
 #pragma unroll
       for (int j = 0; j < A_SLOTS; ++j) {
         const u32 f = M->a_fl[j][t];
-        if (!(f & CRR_ROW_LIVE)) continue;
-        const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
-        B.offer(M->a_cand[j][t], id_at(M->a_src[j][t] & kStepMask), y, j, ((f >> LF_TTS_SHIFT) & timer_mask(y)) != 0);
+        const i64 c = M->a_cand[j][t];
+        const u32 st = M->a_src[j][t] & kStepMask;
+        const bool better = (f & CRR_ROW_LIVE) && (!have || c < bt || (c == bt && st < bs));
+        have = have || (f & CRR_ROW_LIVE);
+        bt = better ? c : bt;
+        bs = better ? st : bs;
+        bj = better ? j : bj;
       }
-      if (B.have && !B.created) {
-        M->a_fl[B.j][t] |= (timer_mask(B.y) << LF_TTS_SHIFT) | (B.y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
-        K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, 0, -1);
+      if (have) {
+        const u32 f = M->a_fl[bj][t];
+        const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
+        if (!((f >> LF_TTS_SHIFT) & timer_mask(y))) {
+          M->a_fl[bj][t] = f | (timer_mask(y) << LF_TTS_SHIFT) | (y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
+          K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, bt, id_at(bs), 0, -1);
+        }
       }
     }
     dirty_act = false;
     if (L.n_timer > 0 && dirty_timer) {
-      BestTimer B;
+      bool have = false;
+      i64 bt = 0;
+      u32 bs = 0;
+      i32 bj = 0;
 #pragma unroll
       for (int j = 0; j < T_SLOTS; ++j) {
         const u32 f = M->t_fl[j][t];
-        if (!(f & CRR_ROW_LIVE)) continue;
-        B.offer(M->t_exp[j][t], id_at((f >> 8) & kStepMask), 0, j, (f & TF_CREATED) != 0);
+        const i64 c = M->t_exp[j][t];
+        const u32 st = (f >> 8) & kStepMask;
+        const bool better = (f & CRR_ROW_LIVE) && (!have || c < bt || (c == bt && st < bs));
+        have = have || (f & CRR_ROW_LIVE);
+        bt = better ? c : bt;
+        bs = better ? st : bs;
+        bj = better ? j : bj;
       }
-      if (B.have && !B.created) {
-        M->t_fl[B.j][t] |= TF_CREATED;
-        K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, B.t, B.e, 0, -1);
+      if (have) {
+        const u32 f = M->t_fl[bj][t];
+        if (!(f & TF_CREATED)) {
+          M->t_fl[bj][t] = f | TF_CREATED;
+          K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, bt, id_at(bs), 0, -1);
+        }
       }
     }
     dirty_timer = false;
@@ -2345,15 +2377,37 @@ struct LaneSource {
       nx.task = 0;
     }
   }
+#ifndef CRR_LATE_PREFETCH
+#define CRR_LATE_PREFETCH 0
+#endif
   __device__ __forceinline__ Ev next(i32 s) {
     const Ev e = nx;
+#if !CRR_LATE_PREFETCH
+    issue(s);
+#endif
+    return e;
+  }
+  // the loads of step s + 1 (and the type byte of s + 2)
+  __device__ __forceinline__ void issue(i32 s) {
     if (s + 1 < n) nx = load(s + 1, et_nx);
     if (s + 2 < n) et_nx = E.etype[ix(s + 2)];
-    return e;
+  }
+  __device__ __forceinline__ void late_issue(i32 s) {
+#if CRR_LATE_PREFETCH
+    issue(s);
+#endif
   }
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[ix(step)]; }
 };
 
+// One wavefront per workflow runs the state machine on wave-uniform values.  With the event fields read
+// out of the chunk by readlane (scalar registers), all of that state is scalar: ~265 SALU instructions and
+// a stream of scalar copies / spills per event, and a CU's one scalar issue slot per cycle is shared by
+// every wavefront on it -- the long tail was bound by it.  Broadcast into VGPRs instead (the type stays
+// scalar for the dispatch), the same work issues on the vector units: config 4 24.7 -> 17.1 ms.
+#ifndef CRR_WAVE_VFIELDS
+#define CRR_WAVE_VFIELDS 1
+#endif
 struct WaveSource {
   const crr_events& E;
   i64 begin, st;
@@ -2372,6 +2426,7 @@ struct WaveSource {
     return e;
   }
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[begin + (i64)step * st]; }
+  __device__ __forceinline__ void late_issue(i32) {}
   __device__ __forceinline__ static i64 rl64(i64 v, i32 l) {
     const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
     const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
@@ -2390,10 +2445,19 @@ struct WaveSource {
     }
     Ev e;
     e.et = __builtin_amdgcn_readlane(cur.et, l);
+#if CRR_WAVE_VFIELDS
+    // event fields broadcast into VGPRs (the state they update then lives in VGPRs: VALU work instead
+    // of scalar moves and SGPR spills); the type stays scalar for the dispatch
+    e.id = __shfl((long long)cur.id, l, 64); e.ver = __shfl((long long)cur.ver, l, 64);
+    e.ts = __shfl((long long)cur.ts, l, 64); e.task = __shfl((long long)cur.task, l, 64);
+    e.ref = __shfl((long long)cur.ref, l, 64);
+    e.key = (u32)__shfl((int)cur.key, l, 64); e.aux = __shfl((int)cur.aux, l, 64);
+#else
     e.id = rl64(cur.id, l); e.ver = rl64(cur.ver, l); e.ts = rl64(cur.ts, l);
     e.task = rl64(cur.task, l); e.ref = rl64(cur.ref, l);
     e.key = __builtin_amdgcn_readlane(cur.key, l);
     e.aux = (i32)__builtin_amdgcn_readlane((u32)cur.aux, l);
+#endif
     return e;
   }
 };
@@ -2524,6 +2588,31 @@ template <class P, class = void>
 struct FusedMapOps { static constexpr bool value = false; };
 template <class P>
 struct FusedMapOps<P, decltype((void)P::kFusedMapOps)> { static constexpr bool value = P::kFusedMapOps; };
+
+// The map operation an event's transition performs, then what the transition does after it (its task,
+// a late domain check).
+template <class P>
+__device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, const u32 op, const Ev& ev, const i32 s,
+                                                const i64 batch_first_id, const crr_activity_side& as, const TaskSink& K) {
+#if CRR_EXP & 2048
+  L.dbg_t = __builtin_readcyclecounter();
+#endif
+  if (op == MOP_NONE || (CRR_EXP & 256)) return CRR_OK;
+  int rc;
+  if constexpr (FusedMapOps<P>::value) rc = T.map_op(L, G, op, ev, s, batch_first_id, as);
+  else rc = map_op_by_method(T, L, G, op, ev, s, batch_first_id, as);
+  if (rc) return rc;
+  if (op == MOP_ACT_INSERT) {
+    K.add(L, G, CRR_TASK_ACTIVITY, 0, ev.ver, 0, ev.id, 0, s);  // GenerateActivityTransferTasks
+  } else if (op == MOP_CHILD_INSERT) {
+    K.add(L, G, CRR_TASK_START_CHILD, 0, ev.ver, 0, ev.id, 0, s);  // GenerateChildWorkflowTasks
+  } else if (op == MOP_RC_INSERT || op == MOP_SIG_INSERT) {
+    // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
+    if (ev.aux == CRR_DOMAIN_UNKNOWN) return CRR_ERR_DOMAIN_NOT_FOUND;
+    K.add(L, G, op == MOP_RC_INSERT ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0, ev.ver, 0, ev.id, 0, s);
+  }
+  return CRR_OK;
+}
 
 // One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
 // code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
@@ -2722,23 +2811,127 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
       default:  // :629-630
         FAIL(CRR_ERR_UNKNOWN_EVENT_TYPE, s);
     }
-  if (op != MOP_NONE && !(CRR_EXP & 256)) {
-    if constexpr (FusedMapOps<P>::value) CHECK(T.map_op(L, G, op, ev, s, batch_first_id, as));
-    else CHECK(map_op_by_method(T, L, G, op, ev, s, batch_first_id, as));
-    // what the transition does after its map operation
-    if (op == MOP_ACT_INSERT) {
-      K.add(L, G, CRR_TASK_ACTIVITY, 0, ver, 0, id, 0, s);  // GenerateActivityTransferTasks
-    } else if (op == MOP_CHILD_INSERT) {
-      K.add(L, G, CRR_TASK_START_CHILD, 0, ver, 0, id, 0, s);  // GenerateChildWorkflowTasks
-    } else if (op == MOP_RC_INSERT || op == MOP_SIG_INSERT) {
-      // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
-      if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
-      K.add(L, G, op == MOP_RC_INSERT ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0, ver, 0, id, 0, s);
-    }
-  }
 #undef CHECK
 #undef FAIL
-  return CRR_OK;
+  return map_op_and_after(L, G, T, op, ev, s, batch_first_id, as, K);
+}
+
+#if CRR_EXP & 2048
+template <class P, class = void>
+struct DbgTier { static constexpr int value = -1; };
+template <class P>
+struct DbgTier<P, decltype((void)P::A_SLOTS)> {
+  static constexpr int value = P::A_SLOTS <= 1 ? 0 : P::A_SLOTS <= 2 ? 1 : P::A_SLOTS <= 4 ? 2 : P::A_SLOTS <= 8 ? 3 : 4;
+};
+#endif
+#ifndef CRR_LANE_DISPATCH
+#define CRR_LANE_DISPATCH 1
+#endif
+// The map operation of each event type (0: none), 4 bits per type
+constexpr u32 mop_of(int t) {
+  return t == CRR_EV_ACTIVITY_TASK_SCHEDULED ? MOP_ACT_INSERT
+       : t == CRR_EV_ACTIVITY_TASK_STARTED ? MOP_ACT_START
+       : (t == CRR_EV_ACTIVITY_TASK_COMPLETED || t == CRR_EV_ACTIVITY_TASK_FAILED || t == CRR_EV_ACTIVITY_TASK_TIMED_OUT ||
+          t == CRR_EV_ACTIVITY_TASK_CANCELED) ? MOP_ACT_DELETE
+       : t == CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED ? MOP_ACT_CANCEL
+       : t == CRR_EV_TIMER_STARTED ? MOP_TIMER_START
+       : (t == CRR_EV_TIMER_FIRED || t == CRR_EV_TIMER_CANCELED) ? MOP_TIMER_DELETE
+       : t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED ? MOP_CHILD_INSERT
+       : t == CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED ? MOP_CHILD_START
+       : (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED || (t >= CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED &&
+          t <= CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED)) ? MOP_CHILD_DELETE
+       : t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ? MOP_RC_INSERT
+       : (t == CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED) ? MOP_RC_DELETE
+       : t == CRR_EV_SIGNAL_EXTERNAL_INITIATED ? MOP_SIG_INSERT
+       : (t == CRR_EV_SIGNAL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED) ? MOP_SIG_DELETE
+       : MOP_NONE;
+}
+constexpr u64 mop_word(int w) {
+  u64 v = 0;
+  for (int k = 0; k < 16; ++k) v |= (u64)mop_of(16 * w + k) << (4 * k);
+  return v;
+}
+// types whose transition is more than a handful of field updates: the start event, the closes and
+// continue-as-new (once per run each), and anything unknown
+constexpr u64 kLaneRare = (1ull << CRR_EV_WORKFLOW_EXECUTION_STARTED) | (1ull << CRR_EV_WORKFLOW_EXECUTION_COMPLETED) |
+                          (1ull << CRR_EV_WORKFLOW_EXECUTION_FAILED) | (1ull << CRR_EV_WORKFLOW_EXECUTION_TIMED_OUT) |
+                          (1ull << CRR_EV_WORKFLOW_EXECUTION_CANCELED) | (1ull << CRR_EV_WORKFLOW_EXECUTION_TERMINATED) |
+                          (1ull << CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW) | (~0ull << CRR_EV_TYPE_COUNT);
+
+// apply_event for a wavefront whose lanes hold different event types.  The per-lane switch runs every
+// case some lane needs, one exec-masked region after another, and merges the Lane fields each case
+// writes at its exit (copies and mask bookkeeping: ~900 SALU + VALU per step on mixed histories).
+// Here the common types are one straight-line pass: each lane's effect on the decision sub-state, the
+// workflow state and the counters is a select between the old value and the new, and the map
+// operation is looked up in a table; the start / close / continue-as-new events (and task emission)
+// take apply_event under their lanes' mask.  Same updates, in the same order, with the same errors
+// (a failing event changes nothing before its Go error, except what Go itself applies first).
+template <class P>
+__device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr_outputs& out, Lane& L, const Geo& G, P& T,
+                                                 const Ev& ev, const i32 s, const i32 t, const i64 batch_first_id,
+                                                 const i64 now_ns, const TaskSink& K, const i32 retention_days) {
+  if (K.on || ((kLaneRare >> (t & 63)) & 1) || t >= 64)
+    return apply_event(in, out, L, G, T, ev, s, t, batch_first_id, now_ns, K, retention_days);
+  const bool is_ds = t == CRR_EV_DECISION_TASK_SCHEDULED, is_dt = t == CRR_EV_DECISION_TASK_STARTED;
+  const bool is_dc = t == CRR_EV_DECISION_TASK_COMPLETED;
+  const bool is_df = t == CRR_EV_DECISION_TASK_TIMED_OUT || t == CRR_EV_DECISION_TASK_FAILED;
+  // the checks that precede any update
+  int rc = CRR_OK;
+  // DecisionTaskScheduled: UpdateWorkflowStateCloseStatus(Running, None) unless Zombie (:185-208)
+  if (is_ds) rc = L.state == CRR_STATE_COMPLETED ? (int)CRR_ERR_INVALID_STATE_TRANSITION
+                : (u32)L.state > (u32)CRR_STATE_VOID ? (int)CRR_ERR_UNKNOWN_WORKFLOW_STATE : (int)CRR_OK;
+  if (is_dt && ev.ref != L.decision_schedule_id) rc = CRR_ERR_DECISION_NOT_FOUND;  // :210-228
+  crr_activity_side as{};
+  if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {  // :283-295
+#if CRR_EXP & 8
+    as = crr_activity_side{10, 20, 30, 0, 0, 0, 1, 0};
+#else
+    as = in.act_side[ev.aux];
+#endif
+    if (as.domain_status == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
+  }
+  if (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED && ev.aux == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
+  if (rc) return rc;
+  // the workflow state of DecisionTaskScheduled
+  const bool run = is_ds && L.state != CRR_STATE_ZOMBIE;
+  L.state = run ? (i32)CRR_STATE_RUNNING : L.state;
+  L.close_status = run ? (i32)CRR_CLOSE_NONE : L.close_status;
+  // the decision sub-state: UpdateDecision (decision_task_manager.go:697-721) with each type's arguments --
+  // Scheduled (:129-166), Started (:199-242), Completed = DeleteDecision (:244-249, :827-838), TimedOut /
+  // Failed = FailDecision + the transient decision (:643-676, :168-197)
+  const i64 a1 = L.decision_attempt + 1;
+  const bool tr = is_df && a1 != 0;  // the transient decision is scheduled
+  const bool dec = is_ds || is_dt || is_dc || is_df;
+  if (dec) {
+    const i64 nv = (is_ds || is_dt) ? ev.ver : tr ? L.current_version : (i64)CRR_EMPTY_VERSION;
+    const i64 nsched = is_ds ? ev.id : is_dt ? ev.ref : tr ? L.next_event_id : (i64)CRR_EMPTY_EVENT_ID;
+    const i64 nstarted = is_dt ? ev.id : (i64)CRR_EMPTY_EVENT_ID;
+    const i32 nreq = is_dt ? s : (i32)CRR_SRC_EMPTY_UUID;
+    const i32 nto = is_ds ? ev.aux : is_dt ? L.decision_timeout : tr ? L.decision_start_to_close : 0;
+    const i64 natt = is_ds ? ev.ref : is_df ? a1 : 0;
+    const i64 nsts = is_dt ? ev.ts : 0;
+    const i64 nscts = is_ds ? ev.ts : is_dt ? L.decision_scheduled_ts : is_df ? now_ns : 0;
+    const i64 nots = is_ds ? ev.ts : (is_dt || is_dc) ? L.decision_orig_scheduled_ts : 0;
+    update_decision(L, nv, nsched, nstarted, nreq, nto, natt, nsts, nscts, nots);
+  }
+  L.last_processed_event = is_dc ? ev.ref : L.last_processed_event;
+  L.signal_count = (i32)((u32)L.signal_count + (t == CRR_EV_WORKFLOW_EXECUTION_SIGNALED ? 1u : 0u));  // :497-502
+  L.flags |= t == CRR_EV_WORKFLOW_EXECUTION_CANCEL_REQUESTED ? (u32)CRR_EXEC_CANCEL_REQUESTED : 0u;  // :504-509
+  if (is_dc && ev.key != 0 && !T.rp_has(L, G, ev.key)) {  // addBinaryCheckSumIfNotExists (:1911-1974)
+    crr_reset_point_row rp;
+    rp.src = s;
+    rp.prev_index = -1;
+    rp.key = ev.key;
+    const bool resettable = L.n_child == 0 && L.n_rc == 0 && L.n_sig == 0;  // CheckResettable (:1977-1994)
+    rp.flags = CRR_ROW_LIVE | (resettable ? CRR_ROW_RESETTABLE : 0u);
+    rc = T.rp_push(L, G, rp);
+    if (rc) return rc;
+    L.flags |= CRR_EXEC_RESET_POINTS_SET;
+  }
+  constexpr u64 w0 = mop_word(0), w1 = mop_word(1), w2 = mop_word(2);
+  const u64 w = t < 16 ? w0 : t < 32 ? w1 : w2;
+  const u32 op = (u32)(w >> (4 * (t & 15))) & 15u;
+  return map_op_and_after(L, G, T, op, ev, s, batch_first_id, as, K);
 }
 
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
@@ -2754,6 +2947,10 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   // read once: a descriptor field read inside the loop is reloaded every event (stores in between may
   // alias it), and its wait drains the prefetched columns with it
   const i32 retention_days = wfp->retention_days;
+#if CRR_EXP & 2048
+  constexpr int kDbgTier = DbgTier<P>::value;
+  u64 dl_p = 0, dl_d = 0, dl_m = 0, dl_e = 0, dl_n = 0, dl_c = 0, dl_t0 = __builtin_readcyclecounter(), dl_t1 = 0;
+#endif
 #if CRR_EXP & 128
   constexpr bool kDbg = std::is_same<SRC, WaveSource>::value;
   const i32 dbg_lane = (i32)(threadIdx.x & 63);
@@ -2838,6 +3035,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 #endif
     // one loop exit for the whole prologue: the checks become a select chain (no divergent branch
     // per check), and on success vh_last = (id, ver) in every case (new item, same version, first).
+#if CRR_EXP & 2048
+    dl_c = __builtin_readcyclecounter();
+#endif
     const Ev ev = src.next(s);
     const u32 et = ev.et;
     const i64 id = ev.id;
@@ -2869,6 +3069,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       L.vh_last_ver = ver;
     }
     last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
+#if CRR_EXP & 2048
+    { const u64 c = __builtin_readcyclecounter(); dl_p += c - dl_c; dl_c = c; }
+#endif
 
     // :131-631 the 42-way dispatch.  When every active lane holds the same event type (the
     // common case: histories of one workflow type replay in lockstep) the type is wave-uniform
@@ -2884,11 +3087,18 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       if (std::is_same<SRC, WaveSource>::value || __builtin_amdgcn_ballot_w64(t != tu) == 0)  // WaveSource: readlane, uniform
         rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
                          K, retention_days);
+      else if (CRR_LANE_DISPATCH)
+        rc = apply_event_lanes(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id,
+                               now_ns, K, retention_days);
       else
         rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
                          K, retention_days);
       if (rc) FAIL(rc, s);
     }
+    src.late_issue(s);  // CRR_LATE_PREFETCH: step s+1's loads after the dispatch's own loads are consumed
+#if CRR_EXP & 2048
+    { const u64 c = __builtin_readcyclecounter(); dl_d += c - dl_c; dl_m += c - L.dbg_t; dl_c = c; }
+#endif
 #if CRR_EXP & 128
     if constexpr (kDbg) dbg_c2 = __builtin_readcyclecounter();
 #endif
@@ -2898,6 +3108,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
+#if CRR_EXP & 2048
+    { const u64 c = __builtin_readcyclecounter(); dl_e += c - dl_c; ++dl_n; }
+#endif
 #if CRR_EXP & 128
     if constexpr (kDbg) {
       const u64 c3 = __builtin_readcyclecounter();
@@ -2934,6 +3147,9 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 done_events:
 #undef CHECK
 #undef FAIL
+#if CRR_EXP & 2048
+  dl_t1 = __builtin_readcyclecounter();
+#endif
 #if CRR_EXP & 128
   if constexpr (kDbg) dbg_t1 = __builtin_readcyclecounter();
 #endif
@@ -2999,6 +3215,22 @@ done_events:
     if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
   }
   out.exec[w] = R;
+#if CRR_EXP & 2048
+  if constexpr (kDbgTier >= 0) {
+    // per wavefront: the loop runs until its longest lane is done, so the wave's maxima are its time
+    const u32 lane = threadIdx.x & 63;
+    const u64 c4 = __builtin_readcyclecounter();
+    u64 v[8] = {dl_p, dl_d, dl_e, dl_t1 - dl_t0, c4 - dl_t1, 1, dl_n, dl_m};
+    for (int k = 0; k < 8; ++k) {
+      u64 x = v[k];
+      for (int o = 32; o >= 1; o >>= 1) {
+        const u64 y = (u64)__shfl_xor((long long)x, o, 64);
+        x = x > y ? x : y;
+      }
+      if (lane == (u32)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) atomicAdd(&crr_dbg[8 * kDbgTier + k], (unsigned long long)x);
+    }
+  }
+#endif
 #if CRR_EXP & 128
   if constexpr (kDbg) {
     atomicAdd(&crr_dbg[dbg_lane], (unsigned long long)dbg_p);
@@ -3397,7 +3629,7 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   }
 }
 
-#if CRR_EXP & 128
+#if CRR_EXP & (128 | 2048)
 extern "C" int crr_debug_cycles(unsigned long long* dst, int n) {  // read and clear crr_dbg
   if (n > 5 * 64) n = 5 * 64;
   if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(crr_dbg), sizeof(unsigned long long) * n) != hipSuccess) return -1;

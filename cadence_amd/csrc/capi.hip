@@ -9,7 +9,7 @@
 namespace crr {
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-template <bool WAVE_TAIL, bool EMIT>
+template <bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
@@ -35,6 +35,9 @@ constexpr int kBlock = 256;
 #endif
 #ifndef CRR_SEG_PRIORITY
 #define CRR_SEG_PRIORITY 1
+#endif
+#ifndef CRR_CRC_GLOBAL  // as in replay_kernel.hip: in-kernel checksums, no fill passes
+#define CRR_CRC_GLOBAL 1
 #endif
 #ifndef CRR_TAIL_CRC  // as in replay_kernel.hip: the tail kernel's checksums come from a fill pass
 #define CRR_TAIL_CRC 0
@@ -223,7 +226,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       const uint32_t tail_end = ((in->flags & CRR_IN_TIERED) && in->big_begin >= n_lane && in->big_begin < in->n_wf)
                                     ? in->big_begin : in->n_wf;
       // one fast launch: the wave tail first (optional), then lane workflows [lo, hi)
-      auto launch_fast = [&](hipStream_t s, bool small_tier, bool with_tail, uint32_t lo, uint32_t hi) {
+      auto launch_fast = [&](hipStream_t s, bool small_tier, bool with_tail, uint32_t lo, uint32_t hi, bool lanes = false) {
         const unsigned wave_blocks = with_tail ? (tail_end - n_lane + kBlock / 64 - 1) / (kBlock / 64) : 0;
         const unsigned blocks = wave_blocks + (hi - lo + kBlock - 1) / kBlock;
         if (blocks == 0) return;
@@ -235,6 +238,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           else hipLaunchKernelGGL((crr::replay_lds_kernel<false, true>), g, b, 0, s, *in, *out, phase, lo, hi);
         } else {
           if (small_tier && with_tail) hipLaunchKernelGGL((crr::replay_lds_small_kernel<true, false>), g, b, 0, s, *in, *out, phase, lo, hi);
+          else if (small_tier && lanes) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, false, true>), g, b, 0, s, *in, *out, phase, lo, hi);
           else if (small_tier) hipLaunchKernelGGL((crr::replay_lds_small_kernel<false, false>), g, b, 0, s, *in, *out, phase, lo, hi);
           else if (with_tail) hipLaunchKernelGGL((crr::replay_lds_kernel<true, false>), g, b, 0, s, *in, *out, phase, lo, hi);
           else hipLaunchKernelGGL((crr::replay_lds_kernel<false, false>), g, b, 0, s, *in, *out, phase, lo, hi);
@@ -268,7 +272,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_tail) {  // the long-history tail, one wavefront each
           if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
-#if !CRR_TAIL_CRC
+#if !CRR_TAIL_CRC && !CRR_CRC_GLOBAL
           // the tail kernel holds no CRC tables (a third wave per SIMD): checksums in a fill pass
           hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((tail_end - n_lane + kBlock - 1) / kBlock), dim3(kBlock), 0, s_tail,
                              *in, *out, phase, n_lane, tail_end);
@@ -277,7 +281,8 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_c3) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact3_kernel<true>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
           else hipLaunchKernelGGL((crr::replay_compact3_kernel<false>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
-          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((hb - wb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_wide, *in, *out, phase, wb, hb);
+          if (!CRR_CRC_GLOBAL)
+            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((hb - wb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_wide, *in, *out, phase, wb, hb);
         }
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - hb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
@@ -287,15 +292,17 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_c2) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact2_kernel<true>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
           else hipLaunchKernelGGL((crr::replay_compact2_kernel<false>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
-          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((wb - c2 + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c2, *in, *out, phase, c2, wb);
+          if (!CRR_CRC_GLOBAL)
+            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((wb - c2 + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c2, *in, *out, phase, c2, wb);
         }
         if (run_c1) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
           else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
-          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((c2 - cb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c1, *in, *out, phase, cb, c2);
+          if (!CRR_CRC_GLOBAL)
+            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((c2 - cb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c1, *in, *out, phase, cb, c2);
         }
         launch_fast(s_large, false, false, lb, cb);
-        launch_fast(s, true, false, 0, lb);
+        launch_fast(s, true, false, 0, lb, true);  // a tier segment of mixed histories: divergent dispatch
         if (fork) {
           const bool seg = g_seg.on && phase == 1 && g_seg.device >= 0;
           if (seg) {

@@ -26,6 +26,12 @@
 
 #include "cadence_replay.h"
 
+// The compact tiers and the tail kernel compute checksums in-kernel from the constant-memory CRC
+// tables (1) or leave them to checksum_fill_kernel (0).
+#ifndef CRR_CRC_GLOBAL
+#define CRR_CRC_GLOBAL 1
+#endif
+
 // Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
 // checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
 // record loads, bit 16 the start side record loads, bit 256 the pending-map operations of the dispatch
@@ -144,6 +150,27 @@ struct Crc {
     return ~crc;
   }
 };
+
+// The same slicing-by-8 tables built at compile time in constant memory, for kernels that keep no CRC
+// tables in LDS (their occupancy is LDS-limited): per-lane lookups are vector loads that hit the CU's
+// L1 / the L2 (8 KB), a few hundred per workflow at its end -- cheaper than re-reading the rows in a
+// separate fill pass.
+struct CrcTab { u32 v[8 * 256]; };
+constexpr CrcTab make_crc_tab() {
+  CrcTab T{};
+  for (u32 i = 0; i < 256; ++i) {
+    u32 c = i;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    T.v[i] = c;
+  }
+  for (int t = 1; t < 8; ++t)
+    for (int i = 0; i < 256; ++i) {
+      const u32 p = T.v[(t - 1) * 256 + i];
+      T.v[t * 256 + i] = (p >> 8) ^ T.v[p & 0xff];
+    }
+  return T;
+}
+__constant__ CrcTab kCrcGlobal = make_crc_tab();
 
 // NT: the block size when the launch fixes it (no read of the dispatch packet), 0: blockDim.x
 template <int NT = 0>
@@ -753,8 +780,11 @@ struct LdsArena {
   int4 p_row[P_SLOTS][LANES];   // crr_reset_point_row
 };
 
-template <class TIER>
+template <class TIER, bool LANE_DISPATCH = false>
 struct LdsTables {
+  // divergent wavefronts through apply_event_lanes (mixed-history segments); the one-class batches
+  // (config 2) replay in lockstep and keep the plain switch, whose registers fit 3 waves per SIMD
+  static constexpr bool kLaneDispatch = LANE_DISPATCH;
   CRR_TIER_SLOTS
   static constexpr bool kResumable = false;  // rows are rebuilt from this call's events: no loaded state
   __device__ __forceinline__ static bool fits(i64) { return true; }
@@ -2827,6 +2857,10 @@ struct DbgTier<P, decltype((void)P::A_SLOTS)> {
 #ifndef CRR_LANE_DISPATCH
 #define CRR_LANE_DISPATCH 1
 #endif
+template <class P, class = void>
+struct LaneDispatch { static constexpr bool value = true; };
+template <class P>
+struct LaneDispatch<P, decltype((void)P::kLaneDispatch)> { static constexpr bool value = P::kLaneDispatch; };
 // The map operation of each event type (0: none), 4 bits per type
 constexpr u32 mop_of(int t) {
   return t == CRR_EV_ACTIVITY_TASK_SCHEDULED ? MOP_ACT_INSERT
@@ -3087,7 +3121,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       if (std::is_same<SRC, WaveSource>::value || __builtin_amdgcn_ballot_w64(t != tu) == 0)  // WaveSource: readlane, uniform
         rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
                          K, retention_days);
-      else if (CRR_LANE_DISPATCH)
+      else if (CRR_LANE_DISPATCH && LaneDispatch<P>::value)
         rc = apply_event_lanes(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id,
                                now_ns, K, retention_days);
       else
@@ -3272,7 +3306,7 @@ union BlockArena {
 
 // Fast path (stride 64): blocks [0, wave_blocks) replay the long-history tail one workflow per
 // wavefront (dispatched first, they run longest), the remaining blocks replay lane per workflow.
-template <class TIER, bool WAVE_TAIL, bool EMIT>
+template <class TIER, bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
@@ -3312,23 +3346,24 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   if (((wf_flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   uniformize_geo(G, lane);
   const i64 ev_begin = uniform64(ev_begin0 - lane) + lane;
-  LdsTables<TIER> T;
+  LdsTables<TIER, LANES> T;
   T.init(&arena.lane, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
   replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
 }
-template <bool WAVE_TAIL, bool EMIT>
+template <bool WAVE_TAIL, bool EMIT, bool LANES = false>
 #ifndef CRR_SMALL_WAVES_PER_EU
 #define CRR_SMALL_WAVES_PER_EU 3
 #endif
 __global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_lds<SmallTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi);
+  replay_lds<SmallTier, WAVE_TAIL, EMIT, LANES>(in, out, phase, lo, hi);
 }
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi);
 }
 template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_lds_small_kernel<false, false, true>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_lds_small_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_lds_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_lds_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
@@ -3479,7 +3514,11 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   CompactTables<TIER> T;
   T.init(&arena, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
+#if CRR_CRC_GLOBAL
+  replay_body<EMIT, CompactTables<TIER>, LaneSource, true>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
+#else
   replay_body<EMIT, CompactTables<TIER>, LaneSource, false>(in, out, w, wfp, G, T, S, nullptr);
+#endif
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
@@ -3548,6 +3587,8 @@ __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(
                                                                              u32 lo, u32 hi) {
 #if CRR_TAIL_CRC
   __shared__ u32 crc_tables[8 * 256];
+#elif CRR_CRC_GLOBAL
+  const u32* crc_tables = kCrcGlobal.v;
 #else
   constexpr u32* crc_tables = nullptr;
 #endif
@@ -3569,11 +3610,11 @@ __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(
 #else
   WaveTables<RegRows> T;
 #endif
-  replay_wave_item<decltype(T.S), EMIT, CRR_TAIL_CRC>(in, out, phase, w, T, crc_tables);
+  replay_wave_item<decltype(T.S), EMIT, CRR_TAIL_CRC || CRR_CRC_GLOBAL>(in, out, phase, w, T, crc_tables);
 #if CRR_TAIL_INPLACE || !CRR_TAIL_LDS
   if (T.retried) {
     WaveTables<HbmRows> H;
-    replay_wave_item<HbmRows, EMIT, CRR_TAIL_CRC>(in, out, phase, w, H, crc_tables);
+    replay_wave_item<HbmRows, EMIT, CRR_TAIL_CRC || CRR_CRC_GLOBAL>(in, out, phase, w, H, crc_tables);
   }
 #endif
 }

@@ -179,7 +179,9 @@ def config2(ctx):
     tier = "replay_lds_small_kernel" if db.c_in.flags & abi.IN_LDS_SMALL else "replay_lds_kernel"
     tail = bool(db.c_in.flags & abi.IN_WAVE_TAIL) and db.c_in.wave_begin < db.n_wf
     emit = bool(db.c_in.flags & abi.IN_EMIT_TASKS)
-    kernel_name = f"{tier}<{str(tail).lower()}, {str(emit).lower()}>"  # <WAVE_TAIL, EMIT>, as rocprofv3 names it
+    kernel_name = f"{tier}<{str(tail).lower()}, {str(emit).lower()}"  # <WAVE_TAIL, EMIT[, LANES]>, as rocprofv3 names it
+    # the small tier's third parameter (divergent dispatch) is set only for multi-segment (mixed) batches
+    kernel_name += ", false>" if tier == "replay_lds_small_kernel" else ">"
     alg_bytes = synth.algorithmic_bytes(batch, res)
     traffic = None
     if os.path.exists(PROFILE_TRAFFIC):

@@ -302,7 +302,9 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
             hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((c2 - cb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c1, *in, *out, phase, cb, c2);
         }
         launch_fast(s_large, false, false, lb, cb);
-        launch_fast(s, true, false, 0, lb, true);  // a tier segment of mixed histories: divergent dispatch
+        // the 1-slot segment of a multi-segment (mixed) batch takes the divergent dispatch; a one-class
+        // batch (config 2) replays in lockstep and keeps the plain switch
+        launch_fast(s, true, false, 0, lb, fork);
         if (fork) {
           const bool seg = g_seg.on && phase == 1 && g_seg.device >= 0;
           if (seg) {

@@ -38,7 +38,7 @@ def load(root):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("root")
-    p.add_argument("--kernel", default="replay_lds_small_kernel<false, false>")
+    p.add_argument("--kernel", default="replay_lds_small_kernel<false, false, false>")
     p.add_argument("--workflows", type=int, default=1_000_000)
     p.add_argument("--events-per-workflow", type=int, default=29)
     p.add_argument("--calib-bytes", type=int, default=1 << 30)

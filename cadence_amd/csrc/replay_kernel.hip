@@ -31,6 +31,10 @@
 #ifndef CRR_CRC_GLOBAL
 #define CRR_CRC_GLOBAL 1
 #endif
+// compact tiers: reset-point rows written to HBM at push, only their keys in LDS
+#ifndef CRR_RP_HBM
+#define CRR_RP_HBM 1
+#endif
 
 // Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
 // checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
@@ -1205,7 +1209,9 @@ struct CompactArena {
   u32 r_fl[R_SLOTS][LANES];      // LIVE | src << 8
   u32 s_fl[S_SLOTS][LANES];
   u32 p_key[P_SLOTS][LANES];
+#if !CRR_RP_HBM
   u32 p_fl[P_SLOTS][LANES];      // row flags (LIVE | RESETTABLE) | src << 8 | (prev_index + 1) << 18
+#endif
 };
 
 template <class TIER>
@@ -1599,11 +1605,20 @@ struct CompactTables {
   }
 
   __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  // Reset points are append-only (a push is final): with CRR_RP_HBM the row goes to its output slot at
+  // once and only the key the later lookups compare stays in LDS (32 B per lane less in tier 2)
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+#if CRR_RP_HBM
+    if (L.n_rp >= P_SLOTS) return CRR_INTERNAL_RETRY;
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    M->p_key[L.n_rp][t] = row.key;
+    *G.rp(L.n_rp) = row;
+#else
     if (L.n_rp >= P_SLOTS || row.prev_index >= (i32)kStepMask - 1) return CRR_INTERNAL_RETRY;
     if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
     M->p_key[L.n_rp][t] = row.key;
     M->p_fl[L.n_rp][t] = (row.flags & 0xFFu) | ((u32)row.src << 8) | ((u32)(row.prev_index + 1) << (8 + kStepBits));
+#endif
     ++L.n_rp;
     return CRR_OK;
   }
@@ -1792,6 +1807,7 @@ struct CompactTables {
       r.flags = CRR_ROW_LIVE;
       *G.sig(i) = r;
     }
+#if !CRR_RP_HBM
     for (i32 i = 0; i < L.n_rp; ++i) {
       const u32 f = M->p_fl[i][t];
       crr_reset_point_row r;
@@ -1801,6 +1817,7 @@ struct CompactTables {
       r.flags = f & 0xFFu;
       *G.rp(i) = r;
     }
+#endif
   }
   __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return id_at((M->t_fl[i][t] >> 8) & kStepMask); }
   __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return id_at(M->a_src[i][t] & kStepMask); }
@@ -3491,7 +3508,13 @@ __global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outp
 // wide_begin) and [wide_begin, hbm_begin)): lane per workflow, 64 lanes per block; slot counts per map
 // chosen by the host's live-set bounds (flatten.TIER_SLOTS).  A workflow that outgrows its tier goes to the retry pass (list 0).
 using CompactTier1 = CTier<4, 3, 2, 1, 1, 4, 64>;
+// tier 2 at 8 x 19.7 KB per CU (2 waves per SIMD): 5 timers (99 % of the config-3 shard's tier-2
+// workflows need <= 5; the rest take tier 3)
+#if CRR_RP_HBM
+using CompactTier2 = CTier<8, 5, 3, 3, 3, 8, 64>;
+#else
 using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
+#endif
 using CompactTier3 = CTier<16, 12, 8, 6, 6, 10, 64>;
 template <class TIER, bool EMIT>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {

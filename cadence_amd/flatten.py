@@ -585,7 +585,7 @@ SMALL_TIER = {"act": 1, "timer": 1, "child": 1, "rc": 1, "sig": 1, "rp": 1}
 LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # CRR_LDS_* defaults
 # replay_kernel.hip CompactTier1 / CompactTier2 (u32 event IDs, 10-bit event steps: <= 1023 events)
 COMPACT1_TIER = {"act": 4, "timer": 3, "child": 2, "rc": 1, "sig": 1, "rp": 4}
-COMPACT2_TIER = {"act": 8, "timer": 6, "child": 3, "rc": 3, "sig": 3, "rp": 8}
+COMPACT2_TIER = {"act": 8, "timer": 5, "child": 3, "rc": 3, "sig": 3, "rp": 8}
 COMPACT3_TIER = {"act": 16, "timer": 12, "child": 8, "rc": 6, "sig": 6, "rp": 10}
 COMPACT_MAX_EVENTS = 1023
 # tier classes 0..4; WIDE: HBM rows

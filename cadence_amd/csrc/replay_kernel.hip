@@ -3515,7 +3515,9 @@ using CompactTier2 = CTier<8, 5, 3, 3, 3, 8, 64>;
 #else
 using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
 #endif
-using CompactTier3 = CTier<16, 12, 8, 6, 6, 10, 64>;
+// tier 3: 29 KB per block, 5 per CU (the config-3 shard's tier-3 workflows all but ~2 % fit; the rest
+// join the wave tail)
+using CompactTier3 = CTier<12, 8, 6, 4, 4, 8, 64>;
 template <class TIER, bool EMIT>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   __shared__ CompactArena<TIER> arena;

@@ -586,7 +586,7 @@ LARGE_TIER = {"act": 2, "timer": 2, "child": 1, "rc": 1, "sig": 1, "rp": 2}   # 
 # replay_kernel.hip CompactTier1 / CompactTier2 (u32 event IDs, 10-bit event steps: <= 1023 events)
 COMPACT1_TIER = {"act": 4, "timer": 3, "child": 2, "rc": 1, "sig": 1, "rp": 4}
 COMPACT2_TIER = {"act": 8, "timer": 5, "child": 3, "rc": 3, "sig": 3, "rp": 8}
-COMPACT3_TIER = {"act": 16, "timer": 12, "child": 8, "rc": 6, "sig": 6, "rp": 10}
+COMPACT3_TIER = {"act": 12, "timer": 8, "child": 6, "rc": 4, "sig": 4, "rp": 8}
 COMPACT_MAX_EVENTS = 1023
 # tier classes 0..4; WIDE: HBM rows
 TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER, COMPACT3_TIER]

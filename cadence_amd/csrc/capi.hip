@@ -36,6 +36,9 @@ constexpr int kBlock = 256;
 #ifndef CRR_SEG_PRIORITY
 #define CRR_SEG_PRIORITY 1
 #endif
+#ifndef CRR_SEG_PRIO_MASK  // side streams with the higher priority: 1 compact tier 3, 3 compact tier 1, 4 compact tier 2
+#define CRR_SEG_PRIO_MASK 0x1A
+#endif
 #ifndef CRR_CRC_GLOBAL  // as in replay_kernel.hip: in-kernel checksums, no fill passes
 #define CRR_CRC_GLOBAL 1
 #endif
@@ -101,14 +104,14 @@ bool ensure_side_streams() {
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (g_side.device == dev) return true;
   if (g_side.device >= 0) return false;  // one device per thread (crr_set_device): keep it simple
-  // the segments with the longest-running wavefronts (compact tiers 2 and 3: their blocks hold the
-  // most LDS per lane, so the fewest fit a CU) are the critical path of the group: their streams get
-  // the higher priority, so their workgroups are dispatched first and the short, dense segments fill
-  // the CUs around them instead of ahead of them
+  // the compact tiers carry most of a mixed batch's work and tiers 2 / 3 the longest-running
+  // wavefronts (their blocks hold the most LDS per lane, so the fewest fit a CU): their streams get the
+  // higher priority, so their workgroups are dispatched first and the short, dense segments fill the
+  // CUs around them instead of ahead of them
   int lo_prio = 0, hi_prio = 0;
   if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
   for (int i = 0; i < kSide; ++i) {
-    const int prio = (CRR_SEG_PRIORITY && (i == 1 || i == 4)) ? hi_prio : lo_prio;
+    const int prio = (CRR_SEG_PRIORITY && ((CRR_SEG_PRIO_MASK >> i) & 1)) ? hi_prio : lo_prio;
     if (hipStreamCreateWithPriority(&g_side.st[i], hipStreamNonBlocking, prio) != hipSuccess) return false;
   }
   if (hipEventCreateWithFlags(&g_side.fork, hipEventDisableTiming) != hipSuccess) return false;

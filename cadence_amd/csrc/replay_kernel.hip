@@ -31,6 +31,10 @@
 #ifndef CRR_CRC_GLOBAL
 #define CRR_CRC_GLOBAL 1
 #endif
+// the LdsTables kernels (config 2's) take their CRC tables from constant memory (1) or LDS (0)
+#ifndef CRR_LDS_CRC_GLOBAL
+#define CRR_LDS_CRC_GLOBAL 0
+#endif
 // compact tiers: reset-point rows written to HBM at push, only their keys in LDS
 #ifndef CRR_RP_HBM
 #define CRR_RP_HBM 1
@@ -3327,9 +3331,13 @@ template <class TIER, bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
+#if CRR_LDS_CRC_GLOBAL
+  const u32* crc_tables = kCrcGlobal.v;  // constant-memory tables: no LDS bank conflicts, 8 KB less LDS
+#else
   __shared__ u32 crc_tables[8 * 256];
-  __shared__ BlockArena<TIER> arena;
   build_crc_tables<kBlock>(crc_tables);
+#endif
+  __shared__ BlockArena<TIER> arena;
   const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
   const u32 tail_end = WAVE_TAIL ? tail_count_end(in) : in.n_wf;  // [tail_end, n_wf): replay_big_kernel
   const u32 wave_blocks = WAVE_TAIL ? (tail_end - n_lane + kWavesPerBlock - 1) / kWavesPerBlock : 0;

@@ -165,12 +165,12 @@ def config2(ctx):
     n_wf, n_events = batch.n_wf, batch.n_events
 
     def exchange():
-        d = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
+        d = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"])
         cdist.all_reduce_digest(torch, ctx.dist, d)
 
     wall, ms = timed_steps(ctx, db, args.steps, args.warmup, per_step=exchange if ctx.world > 1 else None)
     kernel_avg_ms = float(np.mean(ms))
-    digest = cdist.digest_torch(torch, db.tensors["exec"], n_wf)
+    digest = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"])
     if ctx.world > 1:
         cdist.all_reduce_digest(torch, ctx.dist, digest)
     digest = digest.cpu().numpy()
@@ -239,7 +239,7 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
     db = eng.upload(batch)
     wall, ms = timed_steps(ctx, db, args.config_steps, 1)
     res = eng.download(db)
-    digest = cdist.digest_numpy(res.exec)
+    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"])
     tot_events, tot_wf, tot_ok = ctx.reduce([float(batch.n_events), float(batch.n_wf), float(digest[1])], op="sum")
     grp_ms = float(np.mean(ms))
     out = {"workload": workload, "value": tot_events * args.config_steps / wall, "unit": "events/s",
@@ -324,8 +324,8 @@ def end_to_end(ctx, n_wf, k, chunks=8):
         med = float(np.median([r["wall_s"] for r in runs]))
         r0 = runs[0]
         digest = np.zeros(6, np.int64)
-        for cr in sr.results():
-            digest += cdist.digest_numpy(cr.exec)
+        for cr, c in zip(sr.results(), sr.chunks):
+            digest += cdist.digest_numpy(cr.exec, c.batch.wf["ev_count"])
         fig = {"events_per_s": r0["events"] / med, "ms": med * 1e3, "events": r0["events"], "chunks": chunks,
                "h2d_bytes": r0["h2d_bytes"], "d2h_bytes": r0["d2h_bytes"], "h2d_bytes_per_event": r0["h2d_bytes"] / r0["events"],
                "h2d_GBs": r0["h2d_bytes"] / med / 1e9, "setup_s": setup, "digest": [int(x) for x in digest]}

@@ -3,6 +3,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 
 #include "cadence_replay.h"
 
@@ -19,7 +20,6 @@ __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase
 template <bool EMIT>
 __global__ void replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-__global__ void checksum_fill_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
 __global__ void replay_tail_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
@@ -30,96 +30,122 @@ __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checks
 namespace {
 
 constexpr int kBlock = 256;
-#ifndef CRR_WIDE_GLOBAL
-#define CRR_WIDE_GLOBAL 1
-#endif
-#ifndef CRR_SEG_PRIORITY
-#define CRR_SEG_PRIORITY 1
-#endif
-#ifndef CRR_SEG_PRIO_MASK  // side streams with the higher priority: 1 compact tier 3, 3 compact tier 1, 4 compact tier 2
-#define CRR_SEG_PRIO_MASK 0x1A
-#endif
-#ifndef CRR_CRC_GLOBAL  // as in replay_kernel.hip: in-kernel checksums, no fill passes
-#define CRR_CRC_GLOBAL 1
-#endif
-#ifndef CRR_TAIL_CRC  // as in replay_kernel.hip: the tail kernel's checksums come from a fill pass
-#define CRR_TAIL_CRC 0
-#endif
-constexpr int kWideBlock = CRR_WIDE_GLOBAL ? 256 : 64;  // replay_wide_kernel's block
+// side streams with the higher priority: 1 compact tier 3, 3 compact tier 1, 4 compact tier 2
+constexpr unsigned kSegPrioMask = 0x1A;
+constexpr int kWideBlock = 256;  // replay_wide_kernel's block
 constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
 
-struct Timing {
-  // [0,1] phase 0, [2,3] phase 1, [4,5] the phase-1 fast-path kernel alone
-  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  bool valid[3] = {false, false, false};
-  int device = -1;
-};
-thread_local Timing g_timing;
-
-// Per-launch record of the phase-1 fast-path kernel over a measured region (crr_timing_begin ..
-// crr_timing_read), without synchronising between launches: a ring of event pairs.
-constexpr int kRing = 512;
-struct TimingRing {
-  hipEvent_t ev[2 * kRing] = {};
-  int n = 0;          // launches recorded since crr_timing_begin
-  bool on = false;
-  int device = -1;
-};
-thread_local TimingRing g_ring;
-
-bool ensure_events() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (g_timing.ev[0] && g_timing.device == dev) return true;
-  for (auto& e : g_timing.ev) {
-    if (e) (void)hipEventDestroy(e);
-    e = nullptr;
-  }
-  for (auto& e : g_timing.ev)
-    if (hipEventCreate(&e) != hipSuccess) return false;
-  g_timing.device = dev;
-  return true;
-}
-
-// Tier segments of one phase run concurrently: side streams fork from and join back into the
-// caller's stream with events (created once per thread and device).
+// Launch state is kept per HIP device, not per host thread: a cgo caller's goroutines migrate between
+// OS threads, and one thread may drive several devices.  Each device's state is created on first use
+// and guarded by its mutex for the whole enqueue of a call (the fork / join events and the timing
+// events are shared by every call on that device); crr_release() destroys it.
+constexpr int kMaxDevices = 64;
+constexpr int kRing = 512;   // per-launch records of a measured region (crr_timing_begin .. _read)
 constexpr int kSide = 6;
-struct SideStreams {
-  hipStream_t st[kSide] = {};
-  hipEvent_t fork = nullptr, join[kSide] = {};
-  int device = -1;
-};
-thread_local SideStreams g_side;
-// Diagnostics (crr_segment_timing): when each side stream's tier segments of the last phase-1 launch
-// group finished, relative to the fork -- which segment is the critical path of the concurrent launch.
-struct SegmentTiming {
-  bool on = false, valid = false;
-  int device = -1;
-  hipEvent_t start = nullptr, end[kSide + 1] = {};
-};
-thread_local SegmentTiming g_seg;
 
-bool ensure_side_streams() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (g_side.device == dev) return true;
-  if (g_side.device >= 0) return false;  // one device per thread (crr_set_device): keep it simple
-  // the compact tiers carry most of a mixed batch's work and tiers 2 / 3 the longest-running
-  // wavefronts (their blocks hold the most LDS per lane, so the fewest fit a CU): their streams get the
-  // higher priority, so their workgroups are dispatched first and the short, dense segments fill the
-  // CUs around them instead of ahead of them
-  int lo_prio = 0, hi_prio = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
-  for (int i = 0; i < kSide; ++i) {
-    const int prio = (CRR_SEG_PRIORITY && ((CRR_SEG_PRIO_MASK >> i) & 1)) ? hi_prio : lo_prio;
-    if (hipStreamCreateWithPriority(&g_side.st[i], hipStreamNonBlocking, prio) != hipSuccess) return false;
+struct DeviceState {
+  std::mutex mu;
+  int device = -1;
+  // crr_last_kernel_ms: [0,1] phase 0, [2,3] phase 1, [4,5] the phase-1 fast-path kernel alone
+  hipEvent_t ev[6] = {};
+  bool valid[3] = {false, false, false};
+  bool events = false;
+  // measured region: a ring of event pairs around each launch's fast group, no synchronisation between
+  hipEvent_t ring[2 * kRing] = {};
+  int ring_n = 0;
+  bool ring_on = false, ring_events = false;
+  // tier segments of one phase run concurrently: side streams fork from and join back into the
+  // caller's stream
+  hipStream_t side[kSide] = {};
+  hipEvent_t fork = nullptr, join[kSide] = {};
+  bool sides = false;
+  // diagnostics (crr_segment_timing): when each side stream's segments of the last phase-1 group
+  // finished, relative to the fork
+  bool seg_on = false, seg_valid = false, seg_events = false;
+  hipEvent_t seg_start = nullptr, seg_end[kSide + 1] = {};
+
+  bool ensure_events() {
+    if (events) return true;
+    for (auto& e : ev)
+      if (hipEventCreate(&e) != hipSuccess) return false;
+    return events = true;
   }
-  if (hipEventCreateWithFlags(&g_side.fork, hipEventDisableTiming) != hipSuccess) return false;
-  for (auto& e : g_side.join)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-  g_side.device = dev;
-  return true;
+  bool ensure_ring() {
+    if (ring_events) return true;
+    for (auto& e : ring)
+      if (hipEventCreate(&e) != hipSuccess) return false;
+    return ring_events = true;
+  }
+  bool ensure_side_streams() {
+    if (sides) return true;
+    // the compact tiers carry most of a mixed batch's work and tiers 2 / 3 the longest-running
+    // wavefronts (their blocks hold the most LDS per lane, so the fewest fit a CU): their streams get
+    // the higher priority, so their workgroups are dispatched first and the short, dense segments fill
+    // the CUs around them instead of ahead of them
+    int lo_prio = 0, hi_prio = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
+    for (int i = 0; i < kSide; ++i) {
+      const int prio = ((kSegPrioMask >> i) & 1) ? hi_prio : lo_prio;
+      if (hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, prio) != hipSuccess) return false;
+    }
+    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return false;
+    for (auto& e : join)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+    return sides = true;
+  }
+  bool ensure_seg_events() {
+    if (seg_events) return true;
+    if (hipEventCreate(&seg_start) != hipSuccess) return false;
+    for (auto& e : seg_end)
+      if (hipEventCreate(&e) != hipSuccess) return false;
+    return seg_events = true;
+  }
+  // destroys everything (the device must be current); the state can be rebuilt by a later call
+  void release() {
+    auto drop_ev = [](hipEvent_t& e) { if (e) (void)hipEventDestroy(e); e = nullptr; };
+    if (sides) {
+      for (auto& x : side) { if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); } x = nullptr; }
+    }
+    for (auto& e : ev) drop_ev(e);
+    for (auto& e : ring) drop_ev(e);
+    drop_ev(fork);
+    for (auto& e : join) drop_ev(e);
+    drop_ev(seg_start);
+    for (auto& e : seg_end) drop_ev(e);
+    events = ring_events = sides = seg_events = false;
+    valid[0] = valid[1] = valid[2] = false;
+    ring_n = 0;
+    ring_on = seg_on = seg_valid = false;
+  }
+};
+DeviceState g_dev[kMaxDevices];
+
+// The state of the current device (hipGetDevice: HIP's device selection is per host thread).
+DeviceState* current_state() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  g_dev[dev].device = dev;
+  return &g_dev[dev];
 }
+
+// A call on a non-NULL stream runs on that stream's device whatever this thread has selected (a cgo
+// goroutine may have moved to a thread that never called crr_set_device); the selection is restored.
+struct StreamDevice {
+  int prev = -1;
+  bool ok = true;
+  explicit StreamDevice(hipStream_t s) {
+    if (!s) return;
+    int cur = 0, dev = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &dev) != hipSuccess) { ok = false; return; }
+    if (dev != cur) {
+      if (hipSetDevice(dev) != hipSuccess) { ok = false; return; }
+      prev = cur;
+    }
+  }
+  ~StreamDevice() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!in || !out) return false;
@@ -181,23 +207,22 @@ size_t crr_sizeof(int which) {
 int crr_set_device(int device) { return (int)hipSetDevice(device); }
 
 int crr_segment_timing(int on) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return -1;
-  if (on && g_seg.device != dev) {
-    if (hipEventCreate(&g_seg.start) != hipSuccess) return -1;
-    for (auto& e : g_seg.end)
-      if (hipEventCreate(&e) != hipSuccess) return -1;
-    g_seg.device = dev;
-  }
-  g_seg.on = on != 0;
-  g_seg.valid = false;
+  DeviceState* d = current_state();
+  if (!d) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  if (on && !d->ensure_seg_events()) return -1;
+  d->seg_on = on != 0;
+  d->seg_valid = false;
   return 0;
 }
 
 int crr_segment_ms(float* out, int n) {
-  if (!g_seg.valid || n < kSide + 1) return -1;
+  DeviceState* d = current_state();
+  if (!d) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  if (!d->seg_valid || n < kSide + 1) return -1;
   for (int i = 0; i <= kSide; ++i)
-    if (hipEventElapsedTime(&out[i], g_seg.start, g_seg.end[i]) != hipSuccess) return -1;
+    if (hipEventElapsedTime(&out[i], d->seg_start, d->seg_end[i]) != hipSuccess) return -1;
   return kSide + 1;
 }
 
@@ -205,24 +230,28 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   if (!valid_inputs(in, out)) return -1;
   if (in->n_wf == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  StreamDevice on_dev(s);
+  if (!on_dev.ok) return (int)hipErrorInvalidHandle;
+  DeviceState* d = current_state();
+  if (!d) return (int)hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(d->mu);
   // inside a crr_timing_begin region the ring's event pair is the only record: the per-call
   // phase events (crr_last_kernel_ms) would add four event packets to every measured step
-  const bool timed = !g_ring.on && ensure_events();
+  const bool timed = !d->ring_on && d->ensure_events();
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
-  // fast-path grid: one block per 4 long (wave-tail) workflows, then one per 256 lane workflows
   const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
-  g_timing.valid[0] = g_timing.valid[1] = g_timing.valid[2] = false;
+  d->valid[0] = d->valid[1] = d->valid[2] = false;
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
-    if (timed) (void)hipEventRecord(g_timing.ev[2 * phase], s);
+    if (timed) (void)hipEventRecord(d->ev[2 * phase], s);
     if (in->stride == 64) {
       // fast path (LDS-held tables), then one retry pass for the workflows it handed back; the
       // scratch counters are zero on entry (zero-filled by the caller, reset by the retry pass)
       const bool tail = n_lane < in->n_wf;
       const bool small = (in->flags & CRR_IN_LDS_SMALL) != 0;
-      if (timed && phase == 1) (void)hipEventRecord(g_timing.ev[4], s);
-      const bool ring = phase == 1 && g_ring.on && g_ring.n < kRing;
-      if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n], s);
+      if (timed && phase == 1) (void)hipEventRecord(d->ev[4], s);
+      const bool ring = phase == 1 && d->ring_on && d->ring_n < kRing;
+      if (ring) (void)hipEventRecord(d->ring[2 * d->ring_n], s);
       // task emission is a separate instantiation: the plain replay loop carries none of its registers
       const bool emit = (in->flags & CRR_IN_EMIT_TASKS) != 0;
       // long-tail workflows [tail_end, n_wf) that no fast per-wave arena is expected to hold
@@ -248,8 +277,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         }
       };
       if (in->flags & CRR_IN_TIERED) {
-        // segments by expected live-set size: 1 entry per map | 2 | compact tier 1 | compact tier 2 |
-        // more (HBM rows); CRR_IN_LDS_SMALL picks the kernel whose per-wave arenas take the long-history tail
+        // segments by expected live-set size: 1 entry per map | 2 | compact tiers 1-3 | more (HBM rows)
         auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
         const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
         const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
@@ -260,14 +288,15 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
         const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_c3 + (int)run_wide +
-                              (int)run_big + (int)run_tail > 1 &&
-                          ensure_side_streams();
-        hipStream_t s_large = fork ? g_side.st[0] : s, s_wide = fork ? g_side.st[1] : s, s_big = fork ? g_side.st[2] : s;
-        hipStream_t s_c1 = fork ? g_side.st[3] : s, s_c2 = fork ? g_side.st[4] : s, s_tail = fork ? g_side.st[5] : s;
+                              (int)run_big + (int)run_tail > 1;
+        if (fork && !d->ensure_side_streams()) return fail_reset(out, s, hipErrorOutOfMemory);
+        hipStream_t s_large = fork ? d->side[0] : s, s_wide = fork ? d->side[1] : s, s_big = fork ? d->side[2] : s;
+        hipStream_t s_c1 = fork ? d->side[3] : s, s_c2 = fork ? d->side[4] : s, s_tail = fork ? d->side[5] : s;
+        const bool seg = fork && d->seg_on && phase == 1 && d->seg_events;
         if (fork) {
-          if (g_seg.on && phase == 1 && g_seg.device >= 0) (void)hipEventRecord(g_seg.start, s);
-          (void)hipEventRecord(g_side.fork, s);
-          for (hipStream_t x : g_side.st) (void)hipStreamWaitEvent(x, g_side.fork, 0);
+          if (seg) (void)hipEventRecord(d->seg_start, s);
+          (void)hipEventRecord(d->fork, s);
+          for (hipStream_t x : d->side) (void)hipStreamWaitEvent(x, d->fork, 0);
         }
         if (run_big)  // the longest histories first
           hipLaunchKernelGGL(crr::replay_big_kernel, dim3(in->n_wf - tail_end), dim3(64), 0, s_big, *in, *out, phase,
@@ -275,49 +304,35 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         if (run_tail) {  // the long-history tail, one wavefront each
           if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
-#if !CRR_TAIL_CRC && !CRR_CRC_GLOBAL
-          // the tail kernel holds no CRC tables (a third wave per SIMD): checksums in a fill pass
-          hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((tail_end - n_lane + kBlock - 1) / kBlock), dim3(kBlock), 0, s_tail,
-                             *in, *out, phase, n_lane, tail_end);
-#endif
         }
         if (run_c3) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact3_kernel<true>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
           else hipLaunchKernelGGL((crr::replay_compact3_kernel<false>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
-          if (!CRR_CRC_GLOBAL)
-            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((hb - wb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_wide, *in, *out, phase, wb, hb);
         }
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - hb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, hb, n_lane);
-        // the compact tiers leave the checksum to a fill pass over their segment (their blocks then hold
-        // no CRC tables: more of them per CU)
         if (run_c2) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact2_kernel<true>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
           else hipLaunchKernelGGL((crr::replay_compact2_kernel<false>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
-          if (!CRR_CRC_GLOBAL)
-            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((wb - c2 + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c2, *in, *out, phase, c2, wb);
         }
         if (run_c1) {
           if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
           else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
-          if (!CRR_CRC_GLOBAL)
-            hipLaunchKernelGGL(crr::checksum_fill_kernel, dim3((c2 - cb + kBlock - 1) / kBlock), dim3(kBlock), 0, s_c1, *in, *out, phase, cb, c2);
         }
         launch_fast(s_large, false, false, lb, cb);
         // the 1-slot segment of a multi-segment (mixed) batch takes the divergent dispatch; a one-class
         // batch (config 2) replays in lockstep and keeps the plain switch
         launch_fast(s, true, false, 0, lb, fork);
         if (fork) {
-          const bool seg = g_seg.on && phase == 1 && g_seg.device >= 0;
           if (seg) {
-            for (int i = 0; i < kSide; ++i) (void)hipEventRecord(g_seg.end[i], g_side.st[i]);
-            (void)hipEventRecord(g_seg.end[kSide], s);
-            g_seg.valid = true;
+            for (int i = 0; i < kSide; ++i) (void)hipEventRecord(d->seg_end[i], d->side[i]);
+            (void)hipEventRecord(d->seg_end[kSide], s);
+            d->seg_valid = true;
           }
           for (int i = 0; i < kSide; ++i) {
-            (void)hipEventRecord(g_side.join[i], g_side.st[i]);
-            (void)hipStreamWaitEvent(s, g_side.join[i], 0);
+            (void)hipEventRecord(d->join[i], d->side[i]);
+            (void)hipStreamWaitEvent(s, d->join[i], 0);
           }
         }
       } else {
@@ -326,10 +341,13 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       hipError_t err = hipGetLastError();
       if (err != hipSuccess) return fail_reset(out, s, err);
       if (timed && phase == 1) {
-        (void)hipEventRecord(g_timing.ev[5], s);
-        g_timing.valid[2] = true;
+        (void)hipEventRecord(d->ev[5], s);
+        d->valid[2] = true;
       }
-      if (ring) (void)hipEventRecord(g_ring.ev[2 * g_ring.n++ + 1], s);
+      if (ring) {
+        (void)hipEventRecord(d->ring[2 * d->ring_n + 1], s);
+        ++d->ring_n;
+      }
       const unsigned retry_grid = in->n_wf < kRetryGrid ? in->n_wf : kRetryGrid;
       hipLaunchKernelGGL(crr::replay_retry_kernel, dim3(retry_grid), dim3(64), 0, s, *in, *out, phase);
     } else {
@@ -338,8 +356,8 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return in->stride == 64 ? fail_reset(out, s, err) : (int)err;
     if (timed) {
-      (void)hipEventRecord(g_timing.ev[2 * phase + 1], s);
-      g_timing.valid[phase] = true;
+      (void)hipEventRecord(d->ev[2 * phase + 1], s);
+      d->valid[phase] = true;
     }
   }
   return 0;
@@ -349,43 +367,59 @@ int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksu
   if (!valid_inputs(in, out) || (!checksums && in->n_wf)) return -1;
   if (in->n_wf == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  StreamDevice on_dev(s);
+  if (!on_dev.ok) return (int)hipErrorInvalidHandle;
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(crr::checksum_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, checksums);
   return (int)hipGetLastError();
 }
 
 float crr_last_kernel_ms(int which) {
-  if (which < 0 || which > 2 || !g_timing.valid[which]) return -1.0f;
+  DeviceState* d = current_state();
+  if (!d || which < 0 || which > 2) return -1.0f;
+  std::lock_guard<std::mutex> lk(d->mu);
+  if (!d->valid[which]) return -1.0f;
   float ms = -1.0f;
-  if (hipEventElapsedTime(&ms, g_timing.ev[2 * which], g_timing.ev[2 * which + 1]) != hipSuccess) return -1.0f;
+  if (hipEventElapsedTime(&ms, d->ev[2 * which], d->ev[2 * which + 1]) != hipSuccess) return -1.0f;
   return ms;
 }
 
 int crr_timing_begin(void) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return -1;
-  if (g_ring.device != dev) {
-    for (auto& e : g_ring.ev) {
-      if (e) (void)hipEventDestroy(e);
-      e = nullptr;
-    }
-    for (auto& e : g_ring.ev)
-      if (hipEventCreate(&e) != hipSuccess) return -1;
-    g_ring.device = dev;
-  }
-  g_ring.n = 0;
-  g_ring.on = true;
+  DeviceState* d = current_state();
+  if (!d) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  if (!d->ensure_ring()) return -1;
+  d->ring_n = 0;
+  d->ring_on = true;
   return 0;
 }
 
 int crr_timing_read(float* ms, int cap) {
-  g_ring.on = false;
-  int n = g_ring.n < cap ? g_ring.n : cap;
+  DeviceState* d = current_state();
+  if (!d) return -1;
+  std::lock_guard<std::mutex> lk(d->mu);
+  d->ring_on = false;
+  int n = d->ring_n < cap ? d->ring_n : cap;
   for (int i = 0; i < n; ++i) {
-    if (hipEventSynchronize(g_ring.ev[2 * i + 1]) != hipSuccess) return -1;
-    if (hipEventElapsedTime(&ms[i], g_ring.ev[2 * i], g_ring.ev[2 * i + 1]) != hipSuccess) return -1;
+    if (hipEventSynchronize(d->ring[2 * i + 1]) != hipSuccess) return -1;
+    if (hipEventElapsedTime(&ms[i], d->ring[2 * i], d->ring[2 * i + 1]) != hipSuccess) return -1;
   }
   return n;
+}
+
+int crr_release(void) {
+  int cur = -1;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  int rc = 0;
+  for (int i = 0; i < kMaxDevices; ++i) {
+    DeviceState& d = g_dev[i];
+    std::lock_guard<std::mutex> lk(d.mu);
+    if (!(d.events || d.ring_events || d.sides || d.seg_events)) continue;
+    if (hipSetDevice(i) != hipSuccess) { rc = -1; continue; }
+    d.release();
+  }
+  if (have_cur) (void)hipSetDevice(cur);
+  return rc;
 }
 
 uint32_t crr_crc32_ieee(const uint8_t* data, size_t len) {

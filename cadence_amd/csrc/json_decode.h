@@ -5,9 +5,15 @@
 // []*types.HistoryEvent.  This restates what that yields for the fields ApplyEvents reads: the
 // common/types JSON tags (common/types/shared.go:3662-3710 HistoryEvent and the *EventAttributes
 // structs), keys matched case-insensitively as encoding/json does, the last of duplicate keys
-// winning, enum values as their names (case-insensitive, EventType / TimeoutType /
-// ContinueAsNewInitiator UnmarshalText) or numbers, null as absent, unknown keys skipped, and any
-// malformed value or type mismatch an error (json.Unmarshal fails the whole blob).
+// winning, enum values as JSON strings only (EventType / TimeoutType / ContinueAsNewInitiator
+// implement UnmarshalText alone: a name, case-insensitive, or strconv.ParseInt's decimal text; a bare
+// number is encoding/json's UnmarshalTypeError), null as absent, unknown keys skipped, nesting deeper
+// than encoding/json's scanner allows (maxNestingDepth = 10000) an error, and a malformed value or a
+// type mismatch in a field the replay reads an error (json.Unmarshal fails the whole blob).
+//
+// Narrower than json.Unmarshal (documented, pinned by tests/test_decode_json.py): fields the replay
+// never reads are checked for JSON syntax only, not against their Go types, and a duplicated
+// attributes object replaces the earlier one instead of merging into it.
 #pragma once
 
 #include <cstring>
@@ -35,15 +41,19 @@ class JsonReader {
     if (p_ >= end_) fail();
     return *p_;
   }
+  // '{' / '[' open a level, '}' / ']' close one (encoding/json's scanner: at most kMaxDepth levels)
   void expect(char c) {
     if (peek() != c) fail();
     ++p_;
+    level(c);
   }
   bool consume(char c) {
     if (peek() != c) return false;
     ++p_;
+    level(c);
     return true;
   }
+  static constexpr int kMaxDepth = 10000;
   bool null() {  // a JSON null (Go: the pointer / field stays unset)
     if (peek() != 'n') return false;
     lit("null");
@@ -111,30 +121,40 @@ class JsonReader {
     if (sv < (__int128)std::numeric_limits<T>::min() || sv > (__int128)std::numeric_limits<T>::max()) fail();
     return (T)sv;
   }
-  // an enum: its name (case-insensitive, `names`) or a number, as a string; or a bare number
+  // an enum (UnmarshalText): a JSON string holding its name (case-insensitive, `names`) or a decimal
+  // int32; any other token is an UnmarshalTypeError
   int enum_value(const char* const* names, int n) {
-    if (peek() != '"') return integer<int32_t>();
+    if (peek() != '"') fail();
     const std::string s = str();
     for (int i = 0; i < n; ++i)
       if (iequal(s, names[i])) return i;
-    // UnmarshalText's default: strconv.ParseInt(s, 10, 32)
-    JsonReader r(s.data(), s.data() + s.size());
-    const int32_t v = r.integer<int32_t>();
-    if (r.p_ != r.end_) fail();
-    return v;
+    // UnmarshalText's default: strconv.ParseInt(s, 10, 32) -- an optional sign, decimal digits
+    size_t i = 0;
+    bool neg = false;
+    if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+    if (i == s.size()) fail();
+    int64_t v = 0;
+    for (; i < s.size(); ++i) {
+      if (s[i] < '0' || s[i] > '9') fail();
+      v = v * 10 + (s[i] - '0');
+      if (v > (int64_t)1 << 31) fail();
+    }
+    if (neg) v = -v;
+    if (v < std::numeric_limits<int32_t>::min() || v > std::numeric_limits<int32_t>::max()) fail();
+    return (int)v;
   }
   void skip() {  // any value
     const char c = peek();
     if (c == '"') { (void)str(); return; }
     if (c == '{') {
-      ++p_;
+      expect('{');
       if (consume('}')) return;
       do { (void)str(); expect(':'); skip(); } while (consume(','));
       expect('}');
       return;
     }
     if (c == '[') {
-      ++p_;
+      expect('[');
       if (consume(']')) return;
       do { skip(); } while (consume(','));
       expect(']');
@@ -164,13 +184,34 @@ class JsonReader {
     if ((size_t)(end_ - p_) < n || strncmp(p_, w, n) != 0) fail();
     p_ += n;
   }
+  void level(char c) {
+    if (c == '{' || c == '[') {
+      if (++depth_ > kMaxDepth) fail();
+    } else if (c == '}' || c == ']') {
+      --depth_;
+    }
+  }
+  bool digit() const { return p_ < end_ && *p_ >= '0' && *p_ <= '9'; }
+  // the JSON number grammar: -? (0 | [1-9][0-9]*) (. [0-9]+)? ([eE] [+-]? [0-9]+)?
   void number() {
     ws();
     if (p_ < end_ && *p_ == '-') ++p_;
-    if (p_ >= end_ || *p_ < '0' || *p_ > '9') fail();
-    while (p_ < end_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' || *p_ == '+' ||
-                         *p_ == '-'))
+    if (!digit()) fail();
+    if (*p_ == '0') ++p_;
+    else while (digit()) ++p_;
+    if (p_ < end_ && *p_ == '.') {
       ++p_;
+      if (!digit()) fail();
+      while (digit()) ++p_;
+    }
+    if (p_ < end_ && (*p_ == 'e' || *p_ == 'E')) {
+      ++p_;
+      if (p_ < end_ && (*p_ == '+' || *p_ == '-')) ++p_;
+      if (!digit()) fail();
+      while (digit()) ++p_;
+    }
+    if (p_ < end_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == '+' || *p_ == '-' || *p_ == 'e' || *p_ == 'E'))
+      fail();
   }
   uint32_t hex4() {
     if (end_ - p_ < 4) fail();
@@ -201,6 +242,7 @@ class JsonReader {
   }
   const char* p_;
   const char* end_;
+  int depth_ = 0;
 };
 
 // Decode one JSON batch (a JSON array of HistoryEvent objects) into `out`.

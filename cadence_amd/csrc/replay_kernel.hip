@@ -26,37 +26,10 @@
 
 #include "cadence_replay.h"
 
-// The compact tiers and the tail kernel compute checksums in-kernel from the constant-memory CRC
-// tables (1) or leave them to checksum_fill_kernel (0).
-#ifndef CRR_CRC_GLOBAL
-#define CRR_CRC_GLOBAL 1
-#endif
-// the LdsTables kernels (config 2's) take their CRC tables from constant memory (1) or LDS (0)
-#ifndef CRR_LDS_CRC_GLOBAL
-#define CRR_LDS_CRC_GLOBAL 0
-#endif
-// compact tiers: reset-point rows written to HBM at push, only their keys in LDS
-#ifndef CRR_RP_HBM
-#define CRR_RP_HBM 1
-#endif
-
-// Timing experiments only (outputs NOT valid, never built by __graft_entry__): bit 1 skips the
-// checksum, bit 2 the per-batch timer epilogue, bit 4 the per-type dispatch, bit 8 the activity side
-// record loads, bit 16 the start side record loads, bit 256 the pending-map operations of the dispatch
-// (MOP_*), bit 1024 the compact tiers' ActivityTaskStarted re-reads of the scheduled event.  Bit 128 keeps outputs valid and counts shader
-// cycles per event type in the one-wavefront-per-workflow path (crr_debug_cycles).
-#ifndef CRR_EXP
-#define CRR_EXP 0
-#endif
-#if CRR_EXP & (128 | 2048)
-// [part][event type]: part 0 prologue, 1 dispatch, 2 batch epilogue, 3 events; [4][0..2] workflow
-// cycles, workflows, cycles from the end of the event loop (finalize + checksum + row write).
-// Bit 2048 (lane-per-workflow kernels with LDS tiers, per wavefront): [8 * tier + k], tier by the
-// activity slot count (1, 2, 4, 8, 16 -> 0..4), k: 0 step prologue (column wait + version history),
-// 1 dispatch incl. map operation, 2 batch epilogue, 3 whole event loop, 4 after the loop, 5 wavefronts,
-// 6 steps (wavefront iterations), 7 map operations (part of 1)
-__device__ unsigned long long crr_dbg[5 * 64];
-#endif
+// Checksums: the LdsTables kernels (config 2's) keep their CRC tables in LDS; the compact tiers and
+// the tail kernel, whose occupancy is LDS-limited, read the same tables from constant memory
+// (kCrcGlobal).  The compact tiers write reset-point rows to HBM at push and keep only their keys in LDS.
+// (Experiment variants measured and not kept are described in DESIGN.md §4; they are not in this source.)
 #ifndef CRR_LDS_ACT
 #define CRR_LDS_ACT 2
 #endif
@@ -161,8 +134,7 @@ struct Crc {
 
 // The same slicing-by-8 tables built at compile time in constant memory, for kernels that keep no CRC
 // tables in LDS (their occupancy is LDS-limited): per-lane lookups are vector loads that hit the CU's
-// L1 / the L2 (8 KB), a few hundred per workflow at its end -- cheaper than re-reading the rows in a
-// separate fill pass.
+// L1 / the L2 (8 KB), a few hundred per workflow at its end.
 struct CrcTab { u32 v[8 * 256]; };
 constexpr CrcTab make_crc_tab() {
   CrcTab T{};
@@ -222,9 +194,6 @@ struct Lane {
   i32 n_tasks;                  // transfer / timer tasks generated (CRR_IN_EMIT_TASKS)
   i64 expiration_ns;            // executionInfo.ExpirationTime (0: unset)
   i32 src_base;                 // provenance offset of this call's steps (the resumed row's src_next; 0 fresh)
-#if CRR_EXP & 2048
-  u64 dbg_t;                    // cycle counter where apply_event's map operation begins
-#endif
 };
 
 // Where this lane's output rows live in HBM: row(table, slot) = base + slot * stride.
@@ -1213,9 +1182,6 @@ struct CompactArena {
   u32 r_fl[R_SLOTS][LANES];      // LIVE | src << 8
   u32 s_fl[S_SLOTS][LANES];
   u32 p_key[P_SLOTS][LANES];
-#if !CRR_RP_HBM
-  u32 p_fl[P_SLOTS][LANES];      // row flags (LIVE | RESETTABLE) | src << 8 | (prev_index + 1) << 18
-#endif
 };
 
 template <class TIER>
@@ -1297,19 +1263,9 @@ struct CompactTables {
 
   // Map operations (apply_event runs them after its switch, every lane at once): one pass over a map's
   // slots finds the entry an operation addresses and the first free slot, then the operation's writes.
-#ifndef CRR_COMPACT_UNIFIED
-#define CRR_COMPACT_UNIFIED 1
-#endif
   __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 bfid,
                                         const crr_activity_side& as) {
-#if CRR_COMPACT_UNIFIED
     return map_op_unified(L, G, op, ev, s, as);
-#else
-    if (op <= MOP_ACT_CANCEL) return act_op(L, G, op, ev, s, as);
-    if (op <= MOP_TIMER_DELETE) return timer_op(L, G, op, ev, s);
-    if (op <= MOP_CHILD_DELETE) return child_op(L, G, op, ev, s);
-    return init_op(L, G, op, ev, s);
-#endif
   }
   // One code path for every map operation, so a divergent wavefront (lanes with different event types)
   // runs one slot scan and one write-back per step instead of one per map and operation: each lane
@@ -1432,14 +1388,9 @@ struct CompactTables {
     const u32 f = M->a_fl[hit][t];
     if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
     const u32 w = M->a_src[hit][t];
-#if CRR_EXP & 1024
-    const crr_activity_side sa{10, 20, 30, 0, 0, 0, 1, 0};
-    i64 ct = add_seconds(ev.ts, sa.schedule_to_close);
-#else
     const i64 six = ix((i32)step_field(w, 0));
     const crr_activity_side sa = in->act_side[in->ev.aux[six]];
     i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
-#endif
     i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
     cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
     if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
@@ -1448,181 +1399,15 @@ struct CompactTables {
     M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
     return CRR_OK;
   }
-  // ActivityTaskScheduled / Started / closes / CancelRequested: the live entry with ScheduleID == ref
-  // (start, delete) or the mapped live entry with ActivityID == key (insert, cancel), and the first free
-  // slot (insert)
-  __device__ __forceinline__ int act_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, const crr_activity_side& as) {
-    const bool by_id = op == MOP_ACT_START || op == MOP_ACT_DELETE;
-    const u32 want = by_id ? step_of(ev.ref) : ev.key;
-    const u32 need = by_id ? CRR_ROW_LIVE : (CRR_ROW_LIVE | CRR_ROW_MAPPED);
-    i32 hit = -1, fr = -1;
-#pragma unroll
-    for (int j = A_SLOTS - 1; j >= 0; --j) {
-      const u32 f = M->a_fl[j][t];
-      const u32 v = by_id ? (M->a_src[j][t] & kStepMask) : M->a_key[j][t];
-      if ((f & need) == need && v == want) hit = j;
-      if (!(f & CRR_ROW_LIVE)) fr = j;
-    }
-    if (op == MOP_ACT_INSERT) {
-      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
-      if (fr >= G.act_cap) return CRR_ERR_CAPACITY;
-      if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
-      // not started: ScheduleToClose and ScheduleToStart
-      i64 ct = add_seconds(ev.ts, as.schedule_to_close);
-      i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-      cand_min(ct, cy, add_seconds(ev.ts, as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
-      const u32 fl = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
-      M->a_key[fr][t] = ev.key;
-      M->a_fl[fr][t] = fl | ((u32)cy << CF_CAND_SHIFT);
-      M->a_src[fr][t] = (u32)s | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
-      M->a_cand[fr][t] = ct;
-      ++L.n_act;
-      return CRR_OK;
-    }
-    if (op == MOP_ACT_START) {  // :2254-2276
-      if (hit < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
-      const u32 f = M->a_fl[hit][t];
-      if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
-      // started: ScheduleToClose, StartToClose and (HeartbeatTimeout > 0) Heartbeat from StartedTime; the
-      // scheduled time and timeouts are re-read from the ActivityTaskScheduled event (not kept in LDS)
-      const u32 w = M->a_src[hit][t];
-#if CRR_EXP & 1024
-      const crr_activity_side sa{10, 20, 30, 0, 0, 0, 1, 0};
-      i64 ct = add_seconds(ev.ts, sa.schedule_to_close);
-#else
-      const i64 six = ix((i32)step_field(w, 0));
-      const crr_activity_side sa = in->act_side[in->ev.aux[six]];
-      i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
-#endif
-      i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-      cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
-      if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
-      M->a_cand[hit][t] = ct;
-      M->a_fl[hit][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
-      M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
-      return CRR_OK;
-    }
-    if (op == MOP_ACT_CANCEL) {  // :2444-2467
-      if (hit < 0) return CRR_OK;
-      M->a_fl[hit][t] |= CRR_ROW_CANCEL_REQUESTED;
-      const u32 w = M->a_src[hit][t];
-      M->a_src[hit][t] = (w & ~(kStepMask << (2 * kStepBits))) | ((u32)s << (2 * kStepBits));
-      return CRR_OK;
-    }
-    // MOP_ACT_DELETE (DeleteActivity, mutable_state_builder.go:1310-1339)
-    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
-    const u32 f = M->a_fl[hit][t];
-    const u32 key = M->a_key[hit][t];
-    M->a_fl[hit][t] = 0;
-    --L.n_act;
-    if (f & CRR_ROW_MAPPED) return CRR_OK;
-    const i32 m = find_act_mapped(key);
-    if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
-    else ++L.inconsistencies;
-    return CRR_OK;
-  }
-  // TimerStarted (an existing TimerID is overwritten) / Fired / Canceled (:3057-3081, :1390-1419)
-  __device__ __forceinline__ int timer_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
-    i32 hit = -1, fr = -1;
-#pragma unroll
-    for (int j = T_SLOTS - 1; j >= 0; --j) {
-      const u32 f = M->t_fl[j][t];
-      if ((f & CRR_ROW_LIVE) && M->t_key[j][t] == ev.key) hit = j;
-      if (!(f & CRR_ROW_LIVE)) fr = j;
-    }
-    if (op == MOP_TIMER_DELETE) {
-      if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
-      M->t_fl[hit][t] = 0;
-      --L.n_timer;
-      return CRR_OK;
-    }
-    if (!insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
-    i32 j = hit;
-    if (j < 0) {
-      if (fr < 0) return CRR_INTERNAL_RETRY;
-      if (fr >= G.timer_cap) return CRR_ERR_CAPACITY;
-      j = fr;
-      ++L.n_timer;
-    }
-    M->t_exp[j][t] = add_seconds(ev.ts, ev.ref);
-    M->t_key[j][t] = ev.key;
-    M->t_fl[j][t] = CRR_ROW_LIVE | ((u32)s << 8);
-    return CRR_OK;
-  }
-  // StartChildWorkflowExecutionInitiated / ChildWorkflowExecutionStarted / its closes (:3417-3453,
-  // :3485-3507, DeletePendingChildExecution :1160-1178): entries by InitiatedID == ref
-  __device__ __forceinline__ int child_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
-    const u32 want = op == MOP_CHILD_INSERT ? kStepMask : step_of(ev.ref);
-    i32 hit = -1, fr = -1;
-#pragma unroll
-    for (int j = C_SLOTS - 1; j >= 0; --j) {
-      const u32 f = M->c_fl[j][t];
-      if ((f & (CRR_ROW_LIVE | (kStepMask << 8))) == (CRR_ROW_LIVE | (want << 8))) hit = j;
-      if (!(f & CRR_ROW_LIVE)) fr = j;
-    }
-    if (op == MOP_CHILD_INSERT) {
-      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
-      if (fr >= G.child_cap) return CRR_ERR_CAPACITY;
-      M->c_fl[fr][t] = CRR_ROW_LIVE | ((u32)s << 8) | (kStepMask << (8 + kStepBits));
-      ++L.n_child;
-      return CRR_OK;
-    }
-    if (op == MOP_CHILD_START) {
-      if (hit < 0) return CRR_ERR_MISSING_CHILD_INFO;
-      const u32 f = M->c_fl[hit][t];
-      M->c_fl[hit][t] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
-      return CRR_OK;
-    }
-    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
-    M->c_fl[hit][t] = 0;
-    --L.n_child;
-    return CRR_OK;
-  }
-  // RequestCancelExternal / SignalExternal initiated and their resolutions (:2760-2779, :2883-2905,
-  // DeletePendingRequestCancel :1181-1199, DeletePendingSignal :1202-1220)
-  template <int N>
-  __device__ __forceinline__ int initiated_op(u32 (*fl)[LANES], i32& n, i32 cap, bool insert, const Ev& ev, i32 s,
-                                              Lane& L) {
-    const u32 want = insert ? kStepMask : step_of(ev.ref);
-    i32 hit = -1, fr = -1;
-#pragma unroll
-    for (int j = N - 1; j >= 0; --j) {
-      const u32 f = fl[j][t];
-      if ((f & (CRR_ROW_LIVE | (kStepMask << 8))) == (CRR_ROW_LIVE | (want << 8))) hit = j;
-      if (!(f & CRR_ROW_LIVE)) fr = j;
-    }
-    if (insert) {
-      if (fr < 0 || !insert_ok(ev.id, s)) return CRR_INTERNAL_RETRY;
-      if (fr >= cap) return CRR_ERR_CAPACITY;
-      fl[fr][t] = CRR_ROW_LIVE | ((u32)s << 8);
-      ++n;
-      return CRR_OK;
-    }
-    if (hit < 0) { ++L.inconsistencies; return CRR_OK; }
-    fl[hit][t] = 0;
-    --n;
-    return CRR_OK;
-  }
-  __device__ __forceinline__ int init_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s) {
-    if (op <= MOP_RC_DELETE) return initiated_op<R_SLOTS>(M->r_fl, L.n_rc, G.rc_cap, op == MOP_RC_INSERT, ev, s, L);
-    return initiated_op<S_SLOTS>(M->s_fl, L.n_sig, G.sig_cap, op == MOP_SIG_INSERT, ev, s, L);
-  }
 
   __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
   // Reset points are append-only (a push is final): with CRR_RP_HBM the row goes to its output slot at
   // once and only the key the later lookups compare stays in LDS (32 B per lane less in tier 2)
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
-#if CRR_RP_HBM
     if (L.n_rp >= P_SLOTS) return CRR_INTERNAL_RETRY;
     if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
     M->p_key[L.n_rp][t] = row.key;
     *G.rp(L.n_rp) = row;
-#else
-    if (L.n_rp >= P_SLOTS || row.prev_index >= (i32)kStepMask - 1) return CRR_INTERNAL_RETRY;
-    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
-    M->p_key[L.n_rp][t] = row.key;
-    M->p_fl[L.n_rp][t] = (row.flags & 0xFFu) | ((u32)row.src << 8) | ((u32)(row.prev_index + 1) << (8 + kStepBits));
-#endif
     ++L.n_rp;
     return CRR_OK;
   }
@@ -1635,9 +1420,6 @@ struct CompactTables {
   }
   // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199) over the cached heads
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
-#if !CRR_COMPACT_UNIFIED
-    dirty_act = dirty_timer = true;
-#endif
     // The order is (time, event ID, timer type); IDs are id0 + step, so steps order them, and each
     // activity's entry is already its own earliest candidate, so (time, step) decides -- 32-bit step
     // compares and selects, the winner's type and created bit read once afterwards.
@@ -1811,17 +1593,6 @@ struct CompactTables {
       r.flags = CRR_ROW_LIVE;
       *G.sig(i) = r;
     }
-#if !CRR_RP_HBM
-    for (i32 i = 0; i < L.n_rp; ++i) {
-      const u32 f = M->p_fl[i][t];
-      crr_reset_point_row r;
-      r.src = (i32)((f >> 8) & kStepMask);
-      r.prev_index = (i32)((f >> (8 + kStepBits)) & kStepMask) - 1;
-      r.key = M->p_key[i][t];
-      r.flags = f & 0xFFu;
-      *G.rp(i) = r;
-    }
-#endif
   }
   __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return id_at((M->t_fl[i][t] >> 8) & kStepMask); }
   __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return id_at(M->a_src[i][t] & kStepMask); }
@@ -1876,7 +1647,7 @@ __device__ __forceinline__ void wave_sync_global() {  // ... and its global-memo
 
 template <class ARENA, int LIST>
 struct LdsRows {
-  static constexpr bool kLds = true, kReg = false;
+  static constexpr bool kLds = true;
   static constexpr int kList = LIST;  // scratch list a workflow that outgrows the arena is handed to
   static constexpr i32 A = ARENA::A, T = ARENA::T, C = ARENA::C, R = ARENA::R, S = ARENA::S, P = ARENA::P;
   ARENA* M;
@@ -1887,30 +1658,8 @@ struct LdsRows {
   __device__ __forceinline__ crr_initiated_row& sig(i32 j) const { return M->sig[j]; }
   __device__ __forceinline__ crr_reset_point_row& rp(i32 j) const { return M->rp[j]; }
 };
-// Rows in registers: slot j < 64 is held by lane j (every accessor returns the calling lane's own
-// row; WaveTables reads another slot only through bcast, a readlane from its owner).  No LDS and no
-// memory round trip per lookup: a find is a compare and a ballot.  A workflow that outgrows 64
-// slots of a map is replayed again over HBM rows by the caller (kList < 0).  Built with
-// CRR_TAIL_LDS=0 only: measured slower than the LDS arena on the long tail (the 70 row registers are
-// copied around the loop's merge points, ~4x the VALU instructions per event, and spill).
-struct RegRows {
-  static constexpr bool kLds = false, kReg = true;
-  static constexpr int kList = -1;
-  static constexpr i32 A = 64, T = 64, C = 64, R = 64, S = 64, P = 64;
-  mutable crr_activity_row a;
-  mutable crr_timer_row t;
-  mutable crr_child_row c;
-  mutable crr_initiated_row r, s;
-  mutable crr_reset_point_row p;
-  __device__ __forceinline__ crr_activity_row& act(i32) const { return a; }
-  __device__ __forceinline__ crr_timer_row& timer(i32) const { return t; }
-  __device__ __forceinline__ crr_child_row& child(i32) const { return c; }
-  __device__ __forceinline__ crr_initiated_row& rc(i32) const { return r; }
-  __device__ __forceinline__ crr_initiated_row& sig(i32) const { return s; }
-  __device__ __forceinline__ crr_reset_point_row& rp(i32) const { return p; }
-};
 struct HbmRows {
-  static constexpr bool kLds = false, kReg = false;
+  static constexpr bool kLds = false;
   static constexpr int kList = -1;    // never outgrown
   static constexpr i32 A = 0x3fffffff, T = A, C = A, R = A, S = A, P = A;
   Geo G;
@@ -1924,7 +1673,7 @@ struct HbmRows {
 
 template <class ST>
 struct WaveTables {
-  static constexpr bool kResumable = !ST::kLds && !ST::kReg;  // HbmRows continue a loaded state in place
+  static constexpr bool kResumable = !ST::kLds;  // HbmRows continue a loaded state in place
   __device__ __forceinline__ static bool fits(i64) { return true; }
   ST S;
   i32 lane;
@@ -2281,32 +2030,8 @@ struct WaveTables {
     }
     wave_sync_global();
   }
-  // RegRows: each lane's live row -> HBM slot rank (number of smaller live IDs, from the other
-  // lanes' IDs by readlane); the checksum then reads the IDs back from the HBM rows
-  template <class R, class IdOf>
-  __device__ __forceinline__ void scatter_reg(const R& r, i32 hw, R* (Geo::*dst)(i32) const, const Geo& G,
-                                              IdOf id_of) const {
-    const bool live = lane < hw && (r.flags & CRR_ROW_LIVE);
-    const i64 id = id_of(r);
-    u64 m = __builtin_amdgcn_ballot_w64(live);
-    i32 rank = 0;
-    while (m) {
-      const i32 l = (i32)__builtin_ctzll(m);
-      m &= m - 1;
-      rank += readlane64(id, l) < id ? 1 : 0;
-    }
-    if (live) *(G.*dst)(rank) = r;
-  }
   __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
-    if constexpr (ST::kReg) {
-      scatter_reg(S.a, hw_act, &Geo::act, G, [](const crr_activity_row& r) { return r.schedule_id; });
-      scatter_reg(S.t, hw_timer, &Geo::timer, G, [](const crr_timer_row& r) { return r.started_id; });
-      scatter_reg(S.c, hw_child, &Geo::child, G, [](const crr_child_row& r) { return r.initiated_id; });
-      scatter_reg(S.r, hw_rc, &Geo::rc, G, [](const crr_initiated_row& r) { return r.initiated_id; });
-      scatter_reg(S.s, hw_sig, &Geo::sig, G, [](const crr_initiated_row& r) { return r.initiated_id; });
-      if (lane < L.n_rp) *G.rp(lane) = S.p;
-      wave_sync_global();
-    } else if constexpr (ST::kLds) {
+    if constexpr (ST::kLds) {
       i64* ids = S.M->ids;
       constexpr i32 oT = ST::A, oC = oT + ST::T, oR = oC + ST::C, oS = oR + ST::R;
       scatter<crr_activity_row>(A_(), hw_act, ids, &Geo::act, G, [](const crr_activity_row& r) { return r.schedule_id; });
@@ -2428,25 +2153,15 @@ struct LaneSource {
       nx.task = 0;
     }
   }
-#ifndef CRR_LATE_PREFETCH
-#define CRR_LATE_PREFETCH 0
-#endif
   __device__ __forceinline__ Ev next(i32 s) {
     const Ev e = nx;
-#if !CRR_LATE_PREFETCH
     issue(s);
-#endif
     return e;
   }
   // the loads of step s + 1 (and the type byte of s + 2)
   __device__ __forceinline__ void issue(i32 s) {
     if (s + 1 < n) nx = load(s + 1, et_nx);
     if (s + 2 < n) et_nx = E.etype[ix(s + 2)];
-  }
-  __device__ __forceinline__ void late_issue(i32 s) {
-#if CRR_LATE_PREFETCH
-    issue(s);
-#endif
   }
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[ix(step)]; }
 };
@@ -2456,9 +2171,6 @@ struct LaneSource {
 // a stream of scalar copies / spills per event, and a CU's one scalar issue slot per cycle is shared by
 // every wavefront on it -- the long tail was bound by it.  Broadcast into VGPRs instead (the type stays
 // scalar for the dispatch), the same work issues on the vector units: config 4 24.7 -> 17.1 ms.
-#ifndef CRR_WAVE_VFIELDS
-#define CRR_WAVE_VFIELDS 1
-#endif
 struct WaveSource {
   const crr_events& E;
   i64 begin, st;
@@ -2477,7 +2189,6 @@ struct WaveSource {
     return e;
   }
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[begin + (i64)step * st]; }
-  __device__ __forceinline__ void late_issue(i32) {}
   __device__ __forceinline__ static i64 rl64(i64 v, i32 l) {
     const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
     const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
@@ -2496,19 +2207,12 @@ struct WaveSource {
     }
     Ev e;
     e.et = __builtin_amdgcn_readlane(cur.et, l);
-#if CRR_WAVE_VFIELDS
     // event fields broadcast into VGPRs (the state they update then lives in VGPRs: VALU work instead
     // of scalar moves and SGPR spills); the type stays scalar for the dispatch
     e.id = __shfl((long long)cur.id, l, 64); e.ver = __shfl((long long)cur.ver, l, 64);
     e.ts = __shfl((long long)cur.ts, l, 64); e.task = __shfl((long long)cur.task, l, 64);
     e.ref = __shfl((long long)cur.ref, l, 64);
     e.key = (u32)__shfl((int)cur.key, l, 64); e.aux = __shfl((int)cur.aux, l, 64);
-#else
-    e.id = rl64(cur.id, l); e.ver = rl64(cur.ver, l); e.ts = rl64(cur.ts, l);
-    e.task = rl64(cur.task, l); e.ref = rl64(cur.ref, l);
-    e.key = __builtin_amdgcn_readlane(cur.key, l);
-    e.aux = (i32)__builtin_amdgcn_readlane((u32)cur.aux, l);
-#endif
     return e;
   }
 };
@@ -2645,10 +2349,7 @@ struct FusedMapOps<P, decltype((void)P::kFusedMapOps)> { static constexpr bool v
 template <class P>
 __device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, const u32 op, const Ev& ev, const i32 s,
                                                 const i64 batch_first_id, const crr_activity_side& as, const TaskSink& K) {
-#if CRR_EXP & 2048
-  L.dbg_t = __builtin_readcyclecounter();
-#endif
-  if (op == MOP_NONE || (CRR_EXP & 256)) return CRR_OK;
+  if (op == MOP_NONE) return CRR_OK;
   int rc;
   if constexpr (FusedMapOps<P>::value) rc = T.map_op(L, G, op, ev, s, batch_first_id, as);
   else rc = map_op_by_method(T, L, G, op, ev, s, batch_first_id, as);
@@ -2679,11 +2380,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
     switch (t) {
       case CRR_EV_WORKFLOW_EXECUTION_STARTED: {  // :132-183 -> mutable_state_builder.go:1751-1829
-#if CRR_EXP & 16
-        crr_start_side ss{10, 100, 0, -1, 0, 0, -1, 0};
-#else
         const crr_start_side ss = in.start_side[ev.aux];
-#endif
         if (ss.parent_domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         L.decision_start_to_close = ss.decision_start_to_close;
         L.start_src = s;
@@ -2762,11 +2459,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
           K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, L.start_src);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
-#if CRR_EXP & 8
-        as = crr_activity_side{10, 20, 30, 0, 0, 0, 1, 0};
-#else
         as = in.act_side[ev.aux];
-#endif
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         op = MOP_ACT_INSERT;  // then GenerateActivityTransferTasks (below)
         break;
@@ -2867,17 +2560,6 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
   return map_op_and_after(L, G, T, op, ev, s, batch_first_id, as, K);
 }
 
-#if CRR_EXP & 2048
-template <class P, class = void>
-struct DbgTier { static constexpr int value = -1; };
-template <class P>
-struct DbgTier<P, decltype((void)P::A_SLOTS)> {
-  static constexpr int value = P::A_SLOTS <= 1 ? 0 : P::A_SLOTS <= 2 ? 1 : P::A_SLOTS <= 4 ? 2 : P::A_SLOTS <= 8 ? 3 : 4;
-};
-#endif
-#ifndef CRR_LANE_DISPATCH
-#define CRR_LANE_DISPATCH 1
-#endif
 template <class P, class = void>
 struct LaneDispatch { static constexpr bool value = true; };
 template <class P>
@@ -2938,11 +2620,7 @@ __device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr
   if (is_dt && ev.ref != L.decision_schedule_id) rc = CRR_ERR_DECISION_NOT_FOUND;  // :210-228
   crr_activity_side as{};
   if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {  // :283-295
-#if CRR_EXP & 8
-    as = crr_activity_side{10, 20, 30, 0, 0, 0, 1, 0};
-#else
     as = in.act_side[ev.aux];
-#endif
     if (as.domain_status == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
   }
   if (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED && ev.aux == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
@@ -2991,9 +2669,8 @@ __device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr
 
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
 // the replay loop of a launch that does not ask for tasks carries none of its registers.
-// CRC (compile time): the checksum computed here; without it the caller's launch is followed by
-// checksum_fill_kernel over the same workflows (no CRC tables in the kernel's LDS).
-template <bool EMIT, class P, class SRC, bool CRC = true>
+// CRC (compile time): the checksum computed here (every product launch sets it).
+template <bool EMIT, class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
                                             const Geo& G, P& T, SRC& src, const u32* crc_tables) {
   const i32 n_ev = wfp->ev_count;
@@ -3002,16 +2679,6 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   // read once: a descriptor field read inside the loop is reloaded every event (stores in between may
   // alias it), and its wait drains the prefetched columns with it
   const i32 retention_days = wfp->retention_days;
-#if CRR_EXP & 2048
-  constexpr int kDbgTier = DbgTier<P>::value;
-  u64 dl_p = 0, dl_d = 0, dl_m = 0, dl_e = 0, dl_n = 0, dl_c = 0, dl_t0 = __builtin_readcyclecounter(), dl_t1 = 0;
-#endif
-#if CRR_EXP & 128
-  constexpr bool kDbg = std::is_same<SRC, WaveSource>::value;
-  const i32 dbg_lane = (i32)(threadIdx.x & 63);
-  u64 dbg_p = 0, dbg_d = 0, dbg_e = 0, dbg_n = 0, dbg_c0 = 0, dbg_c1 = 0, dbg_c2 = 0, dbg_t0 = 0, dbg_t1 = 0;
-  if constexpr (kDbg) dbg_t0 = __builtin_readcyclecounter();
-#endif
 
   // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
   Lane L;
@@ -3085,14 +2752,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 
   src.start();
   for (i32 s = 0; s < n_ev; ++s) {
-#if CRR_EXP & 128
-    if constexpr (kDbg) dbg_c0 = __builtin_readcyclecounter();
-#endif
     // one loop exit for the whole prologue: the checks become a select chain (no divergent branch
     // per check), and on success vh_last = (id, ver) in every case (new item, same version, first).
-#if CRR_EXP & 2048
-    dl_c = __builtin_readcyclecounter();
-#endif
     const Ev ev = src.next(s);
     const u32 et = ev.et;
     const i64 id = ev.id;
@@ -3124,58 +2785,32 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       L.vh_last_ver = ver;
     }
     last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
-#if CRR_EXP & 2048
-    { const u64 c = __builtin_readcyclecounter(); dl_p += c - dl_c; dl_c = c; }
-#endif
 
     // :131-631 the 42-way dispatch.  When every active lane holds the same event type (the
     // common case: histories of one workflow type replay in lockstep) the type is wave-uniform
     // and the switch runs on a scalar register -- scalar branches, no exec-mask tree; otherwise
     // the per-lane switch.
-#if CRR_EXP & 128
-    if constexpr (kDbg) dbg_c1 = __builtin_readcyclecounter();
-#endif
     {
       int rc;
       const i32 tu = uniform32(t);
       const i32 ps = s + L.src_base;  // provenance step of the event (rows' *_src)
       if (std::is_same<SRC, WaveSource>::value || __builtin_amdgcn_ballot_w64(t != tu) == 0)  // WaveSource: readlane, uniform
-        rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : tu, batch_first_id, now_ns,
+        rc = apply_event(in, out, L, G, T, ev, ps, tu, batch_first_id, now_ns,
                          K, retention_days);
-      else if (CRR_LANE_DISPATCH && LaneDispatch<P>::value)
-        rc = apply_event_lanes(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id,
+      else if (LaneDispatch<P>::value)
+        rc = apply_event_lanes(in, out, L, G, T, ev, ps, t, batch_first_id,
                                now_ns, K, retention_days);
       else
-        rc = apply_event(in, out, L, G, T, ev, ps, (CRR_EXP & 4) ? (i32)CRR_EV_MARKER_RECORDED : t, batch_first_id, now_ns,
+        rc = apply_event(in, out, L, G, T, ev, ps, t, batch_first_id, now_ns,
                          K, retention_days);
       if (rc) FAIL(rc, s);
     }
-    src.late_issue(s);  // CRR_LATE_PREFETCH: step s+1's loads after the dispatch's own loads are consumed
-#if CRR_EXP & 2048
-    { const u64 c = __builtin_readcyclecounter(); dl_d += c - dl_c; dl_m += c - L.dbg_t; dl_c = c; }
-#endif
-#if CRR_EXP & 128
-    if constexpr (kDbg) dbg_c2 = __builtin_readcyclecounter();
-#endif
 
     if (et & CRR_ETYPE_BATCH_LAST) {
-      if (!(CRR_EXP & 2)) T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
+      T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
       L.last_first_event_id = batch_first_id;  // :642-643
       L.next_event_id = id + 1;
     }
-#if CRR_EXP & 2048
-    { const u64 c = __builtin_readcyclecounter(); dl_e += c - dl_c; ++dl_n; }
-#endif
-#if CRR_EXP & 128
-    if constexpr (kDbg) {
-      const u64 c3 = __builtin_readcyclecounter();
-      const bool mine = dbg_lane == t;
-      dbg_p += mine ? dbg_c1 - dbg_c0 : 0;
-      dbg_d += mine ? dbg_c2 - dbg_c1 : 0;
-      dbg_e += mine ? c3 - dbg_c2 : 0;
-      dbg_n += mine ? 1 : 0;
-    }
-#endif
   }
   {
     // what the tail reads from HBM -- the last TaskID, the token and rebuild fields of the descriptor --
@@ -3202,12 +2837,6 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 done_events:
 #undef CHECK
 #undef FAIL
-#if CRR_EXP & 2048
-  dl_t1 = __builtin_readcyclecounter();
-#endif
-#if CRR_EXP & 128
-  if constexpr (kDbg) dbg_t1 = __builtin_readcyclecounter();
-#endif
   if (!task_read && last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
   if (L.status == CRR_OK && K.on && L.n_tasks > G.task_cap) L.status = CRR_ERR_CAPACITY;
@@ -3217,7 +2846,7 @@ done_events:
     return;
   }
   // the checksum's branch-token words go out before the row write-back, whose work hides their latency
-  const bool want_crc = CRC && L.status == CRR_OK && !(CRR_EXP & 1);
+  const bool want_crc = L.status == CRR_OK;
   TokenWords TW;
   TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
   if (L.vh_n > 0) {
@@ -3225,7 +2854,7 @@ done_events:
     it->event_id = L.vh_last_id;
     it->version = L.vh_last_ver;
   }
-  if (!(CRR_EXP & 512)) T.finalize(L, G);
+  T.finalize(L, G);
 
   crr_exec_row R;
   R.status = L.status;
@@ -3266,40 +2895,8 @@ done_events:
   R.expiration_ns = L.expiration_ns;
   R.src_next = L.src_base + n_ev;
   R.reserved = 0;
-  if constexpr (CRC) {
-    if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
-  }
+  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
   out.exec[w] = R;
-#if CRR_EXP & 2048
-  if constexpr (kDbgTier >= 0) {
-    // per wavefront: the loop runs until its longest lane is done, so the wave's maxima are its time
-    const u32 lane = threadIdx.x & 63;
-    const u64 c4 = __builtin_readcyclecounter();
-    u64 v[8] = {dl_p, dl_d, dl_e, dl_t1 - dl_t0, c4 - dl_t1, 1, dl_n, dl_m};
-    for (int k = 0; k < 8; ++k) {
-      u64 x = v[k];
-      for (int o = 32; o >= 1; o >>= 1) {
-        const u64 y = (u64)__shfl_xor((long long)x, o, 64);
-        x = x > y ? x : y;
-      }
-      if (lane == (u32)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) atomicAdd(&crr_dbg[8 * kDbgTier + k], (unsigned long long)x);
-    }
-  }
-#endif
-#if CRR_EXP & 128
-  if constexpr (kDbg) {
-    atomicAdd(&crr_dbg[dbg_lane], (unsigned long long)dbg_p);
-    atomicAdd(&crr_dbg[64 + dbg_lane], (unsigned long long)dbg_d);
-    atomicAdd(&crr_dbg[128 + dbg_lane], (unsigned long long)dbg_e);
-    atomicAdd(&crr_dbg[192 + dbg_lane], (unsigned long long)dbg_n);
-    const u64 c4 = __builtin_readcyclecounter();
-    if (dbg_lane == 0) {
-      atomicAdd(&crr_dbg[256], (unsigned long long)(c4 - dbg_t0));
-      atomicAdd(&crr_dbg[257], 1ull);
-      atomicAdd(&crr_dbg[258], (unsigned long long)(c4 - dbg_t1));
-    }
-  }
-#endif
 }
 
 // ---- kernels ---------------------------------------------------------------------------------------
@@ -3331,12 +2928,8 @@ template <class TIER, bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
-#if CRR_LDS_CRC_GLOBAL
-  const u32* crc_tables = kCrcGlobal.v;  // constant-memory tables: no LDS bank conflicts, 8 KB less LDS
-#else
   __shared__ u32 crc_tables[8 * 256];
   build_crc_tables<kBlock>(crc_tables);
-#endif
   __shared__ BlockArena<TIER> arena;
   const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
   const u32 tail_end = WAVE_TAIL ? tail_count_end(in) : in.n_wf;  // [tail_end, n_wf): replay_big_kernel
@@ -3434,7 +3027,7 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 // Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
 // the list counters, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
-template <class ST, bool EMIT = true, bool CRC = true>
+template <class ST, bool EMIT = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  WaveTables<ST>& T, const u32* crc_tables) {
   const crr_workflow* wfp = in.wf + w;
@@ -3446,7 +3039,7 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body<EMIT, WaveTables<ST>, WaveSource, CRC>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT, WaveTables<ST>, WaveSource>(in, out, w, wfp, G, T, S, crc_tables);
 }
 __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  LdsArena<HugeTier>* arena, const u32* crc_tables) {
@@ -3468,10 +3061,6 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
 }
 // Wide segment (CRR_IN_TIERED [hbm_begin, lanes)): lane workflows whose live sets the host expects to
 // outgrow the compact tiers, and loaded states (CRR_WF_FLAG_RESUME: continued in place over their rows).
-#ifndef CRR_WIDE_GLOBAL
-#define CRR_WIDE_GLOBAL 1
-#endif
-#if CRR_WIDE_GLOBAL
 // Lane per workflow over the workflows' own HBM rows (GlobalTables: no LDS, so the occupancy is the
 // register-limited one; interleaved rows keep slot j of a group one coalesced run).
 #ifndef CRR_WIDE_WAVES_PER_EU
@@ -3500,29 +3089,13 @@ __global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_ker
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, (in.flags & CRR_IN_EMIT_TASKS) != 0);
   replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
 }
-#else
-// Lane per workflow with the 8/8/4/4/4/8-slot LDS tier (64 per block); a lane that outgrows it
-// replays again at once over HBM rows.
-__global__ void __launch_bounds__(64) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  __shared__ u32 crc_tables[8 * 256];
-  __shared__ LdsArena<HugeTier> arena;
-  build_crc_tables(crc_tables);
-  const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
-  if (w >= hi) return;
-  replay_lane_item(in, out, phase, w, &arena, crc_tables);
-}
-#endif
 // Compact LDS tiers (CRR_IN_TIERED segments [compact_begin, compact2_begin), [compact2_begin,
 // wide_begin) and [wide_begin, hbm_begin)): lane per workflow, 64 lanes per block; slot counts per map
 // chosen by the host's live-set bounds (flatten.TIER_SLOTS).  A workflow that outgrows its tier goes to the retry pass (list 0).
 using CompactTier1 = CTier<4, 3, 2, 1, 1, 4, 64>;
 // tier 2 at 8 x 19.7 KB per CU (2 waves per SIMD): 5 timers (99 % of the config-3 shard's tier-2
 // workflows need <= 5; the rest take tier 3)
-#if CRR_RP_HBM
 using CompactTier2 = CTier<8, 5, 3, 3, 3, 8, 64>;
-#else
-using CompactTier2 = CTier<8, 6, 3, 3, 3, 8, 64>;
-#endif
 // tier 3: 29 KB per block, 5 per CU (the config-3 shard's tier-3 workflows all but ~2 % fit; the rest
 // join the wave tail)
 using CompactTier3 = CTier<12, 8, 6, 4, 4, 8, 64>;
@@ -3547,11 +3120,7 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   CompactTables<TIER> T;
   T.init(&arena, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-#if CRR_CRC_GLOBAL
-  replay_body<EMIT, CompactTables<TIER>, LaneSource, true>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
-#else
-  replay_body<EMIT, CompactTables<TIER>, LaneSource, false>(in, out, w, wfp, G, T, S, nullptr);
-#endif
+  replay_body<EMIT, CompactTables<TIER>, LaneSource>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
@@ -3600,56 +3169,26 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
 }
 // Long-history tail of a CRR_IN_TIERED batch ([wave_begin, big_begin), longest first): one wavefront
 // per workflow over a 12-KB LDS row arena; a workflow that outgrows it (or resumes a loaded state) is
-// replayed again over its HBM rows in the same wavefront.  The checksum is left to checksum_fill_kernel
-// over the segment (CRR_TAIL_CRC=0): without the 8-KB CRC tables 13 blocks fit a CU, so with <= 168
-// VGPRs the tail runs 3 waves per SIMD -- 3072 at once, enough for config 4's tail in one round.
+// replayed again over its HBM rows in the same wavefront.  The checksum reads the constant-memory CRC
+// tables: without 8 KB of CRC tables in LDS 13 blocks fit a CU, so with <= 168 VGPRs the tail runs 3
+// waves per SIMD -- 3072 at once, enough for config 4's tail in one round.
 #ifndef CRR_TAIL_WAVES_PER_EU
 #define CRR_TAIL_WAVES_PER_EU 3
-#endif
-#ifndef CRR_TAIL_LDS
-#define CRR_TAIL_LDS 1
-#endif
-#ifndef CRR_TAIL_CRC
-#define CRR_TAIL_CRC 0
-#endif
-#ifndef CRR_TAIL_INPLACE
-#define CRR_TAIL_INPLACE 1
 #endif
 template <bool EMIT>
 __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(crr_inputs in, crr_outputs out, int phase,
                                                                              u32 lo, u32 hi) {
-#if CRR_TAIL_CRC
-  __shared__ u32 crc_tables[8 * 256];
-#elif CRR_CRC_GLOBAL
   const u32* crc_tables = kCrcGlobal.v;
-#else
-  constexpr u32* crc_tables = nullptr;
-#endif
-#if CRR_TAIL_LDS
   __shared__ WaveTier<LargeTier>::Arena arena;
-#endif
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
-#if CRR_TAIL_CRC
-  build_crc_tables(crc_tables);
-#endif
-#if CRR_TAIL_LDS
-#if CRR_TAIL_INPLACE
   WaveTables<LdsRows<WaveTier<LargeTier>::Arena, -1>> T;
-#else
-  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, 1>> T;  // outgrown: the retry pass's wave list
-#endif
   T.S.M = &arena;
-#else
-  WaveTables<RegRows> T;
-#endif
-  replay_wave_item<decltype(T.S), EMIT, CRR_TAIL_CRC || CRR_CRC_GLOBAL>(in, out, phase, w, T, crc_tables);
-#if CRR_TAIL_INPLACE || !CRR_TAIL_LDS
+  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables);
   if (T.retried) {
     WaveTables<HbmRows> H;
-    replay_wave_item<HbmRows, EMIT, CRR_TAIL_CRC || CRR_CRC_GLOBAL>(in, out, phase, w, H, crc_tables);
+    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables);
   }
-#endif
 }
 template __global__ void replay_tail_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_tail_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
@@ -3665,9 +3204,6 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   const u32 n0 = min(__hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
   const u32 n1 = min(__hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
   if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
-#if CRR_EXP & 64  // diagnostics only: leave the handed-back workflows at CRR_INTERNAL_RETRY
-  return;
-#endif
   build_crc_tables(crc_tables);
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
@@ -3703,36 +3239,7 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   }
 }
 
-#if CRR_EXP & (128 | 2048)
-extern "C" int crr_debug_cycles(unsigned long long* dst, int n) {  // read and clear crr_dbg
-  if (n > 5 * 64) n = 5 * 64;
-  if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(crr_dbg), sizeof(unsigned long long) * n) != hipSuccess) return -1;
-  static const unsigned long long zero[5 * 64] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(crr_dbg), zero, sizeof(zero)) == hipSuccess ? n : -1;
-}
-#endif
 
-// The checksum of the workflows [lo, hi) a CRC-less launch (replay_body<..., false>) just replayed
-// in this phase: the same payload_crc over the rows it wrote, stored into their exec rows.
-__global__ void __launch_bounds__(kBlock) checksum_fill_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  __shared__ u32 crc_tables[8 * 256];
-  build_crc_tables(crc_tables);
-  const u32 w = lo + blockIdx.x * kBlock + threadIdx.x;
-  if (w >= hi) return;
-  const crr_workflow* wfp = in.wf + w;
-  if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
-  crr_exec_row* R = out.exec + w;
-  if (R->status != CRR_OK) return;  // failed (no checksum) or handed to the retry pass (it computes its own)
-  Geo G;
-  load_geo(G, wfp, out, wf_stride(in, w));
-  GlobalTables ids;
-  TokenWords TW;
-  TW.issue(token_desc(wfp), R->token_src, in.arena);
-  u32 len = 0;
-  const u32 crc = payload_crc(*R, ids, G, TW, in.arena, crc_tables, &len);
-  R->checksum = crc;
-  R->payload_len = len;
-}
 
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).
 __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {

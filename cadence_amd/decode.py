@@ -146,7 +146,9 @@ def _decode_call(L, args, n_threads: int):
     return h
 
 
-ENCODINGS = {"thriftrw": 0, "json": 1, "unknow": 2, "unknown": 2, "": 3}   # common.EncodingType -> CRR_ENCODING_*
+# common.EncodingType (common/constants.go:60-67) -> CRR_ENCODING_*; EncodingTypeUnknown is the literal
+# "unknow", so a blob tagged "unknown" is an unknown encoding (NewUnknownEncodingTypeError), not json
+ENCODINGS = {"thriftrw": 0, "json": 1, "unknow": 2, "": 3}
 
 
 def _prepare(sources: Sequence[WorkflowSource], known_domains: Optional[Iterable[str]]):

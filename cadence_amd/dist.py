@@ -18,7 +18,6 @@ EXEC_ROW_WORDS = abi.EXEC_ROW.itemsize // 4
 W_STATUS = abi.EXEC_ROW.fields["status"][1] // 4
 W_INCONS = abi.EXEC_ROW.fields["inconsistencies"][1] // 4
 W_CHECKSUM = abi.EXEC_ROW.fields["checksum"][1] // 4
-Q_NEXT_EVENT_ID = abi.EXEC_ROW.fields["next_event_id"][1] // 8
 DIGEST_LEN = 6
 GOLDEN = 0x9E3779B1
 
@@ -61,16 +60,22 @@ def workflow_mask(shard_ids: np.ndarray, rank: int, world: int) -> np.ndarray:
     return (shard_ids % world) == rank
 
 
-def digest_torch(torch, exec_bytes, n_wf: int):
-    """Device-side digest of a replayed shard from the raw exec-row buffer (int64[6]):
-    [events replayed, workflows ok, workflows failed, sum(crc of ok), sum(crc*phi mod 2^32), inconsistencies]."""
+WF_WORDS = abi.WORKFLOW.itemsize // 4
+W_EV_COUNT = abi.WORKFLOW.fields["ev_count"][1] // 4
+
+
+def digest_torch(torch, exec_bytes, n_wf: int, wf_bytes):
+    """Device-side digest of a replayed shard from the raw exec-row and descriptor buffers (int64[6]):
+    [events applied by OK workflows (each one's ev_count: the events of this call, so a resumed --
+    passive-replication -- or continue-as-new run counts what it replayed, not its NextEventID), workflows
+    ok, workflows failed, sum(crc of ok), sum(crc*phi mod 2^32), inconsistencies]."""
     raw = exec_bytes[: n_wf * EXEC_ROW_WORDS * 4]
     rows = raw.view(torch.int32).view(n_wf, EXEC_ROW_WORDS)
-    nxt = raw.view(torch.int64).view(n_wf, EXEC_ROW_WORDS // 2)[:, Q_NEXT_EVENT_ID]   # the whole int64 field
+    ev = wf_bytes[: n_wf * WF_WORDS * 4].view(torch.int32).view(n_wf, WF_WORDS)[:, W_EV_COUNT].to(torch.int64)
     ok = (rows[:, W_STATUS] == 0).to(torch.int64)
     crc = rows[:, W_CHECKSUM].to(torch.int64) & 0xFFFFFFFF
     return torch.stack([
-        ((nxt - 1) * ok).sum(),
+        (ev * ok).sum(),
         ok.sum(),
         n_wf - ok.sum(),
         (crc * ok).sum(),
@@ -79,12 +84,12 @@ def digest_torch(torch, exec_bytes, n_wf: int):
     ])
 
 
-def digest_numpy(exec_rows: np.ndarray) -> np.ndarray:
-    """Same digest from host exec rows (abi.EXEC_ROW)."""
+def digest_numpy(exec_rows: np.ndarray, ev_count: np.ndarray) -> np.ndarray:
+    """Same digest from host exec rows (abi.EXEC_ROW) and the descriptors' ev_count (same order)."""
     ok = (exec_rows["status"] == 0).astype(np.int64)
     crc = exec_rows["checksum"].astype(np.int64)
-    nxt = exec_rows["next_event_id"].astype(np.int64)
-    return np.array([((nxt - 1) * ok).sum(), ok.sum(), len(exec_rows) - ok.sum(), (crc * ok).sum(),
+    ev = np.asarray(ev_count, np.int64)
+    return np.array([(ev * ok).sum(), ok.sum(), len(exec_rows) - ok.sum(), (crc * ok).sum(),
                      ((crc * GOLDEN) & 0xFFFFFFFF).sum(), exec_rows["inconsistencies"].astype(np.int64).sum()],
                     dtype=np.int64)
 

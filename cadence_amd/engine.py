@@ -39,6 +39,7 @@ def lib():
         L.crr_checksum.restype = ctypes.c_int
         L.crr_set_device.argtypes = [ctypes.c_int]
         L.crr_set_device.restype = ctypes.c_int
+        L.crr_release.restype = ctypes.c_int
         L.crr_abi_version.restype = ctypes.c_int
         L.crr_crc32_ieee.argtypes = [vp, ctypes.c_size_t]
         L.crr_crc32_ieee.restype = ctypes.c_uint32

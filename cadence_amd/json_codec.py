@@ -40,7 +40,7 @@ def attributes_json(e: HistoryEvent) -> Dict:
         o["executionStartToCloseTimeoutSeconds"] = g("execution_start_to_close_timeout_seconds", 0)
         o["taskStartToCloseTimeoutSeconds"] = g("task_start_to_close_timeout_seconds", 0)
         if a.get("initiator") is not None:
-            o["initiator"] = INITIATOR_NAMES[a["initiator"]] if 0 <= a["initiator"] < 3 else a["initiator"]
+            o["initiator"] = INITIATOR_NAMES[a["initiator"]] if 0 <= a["initiator"] < 3 else str(a["initiator"])
         if g("attempt", 0):
             o["attempt"] = g("attempt")
         if g("expiration_timestamp", 0):
@@ -96,8 +96,10 @@ def attributes_json(e: HistoryEvent) -> Dict:
 
 def event_json(e: HistoryEvent) -> Dict:
     known = e.event_type in ET._value2member_map_
-    # an out-of-range type is written as its number (UnmarshalText's numeric fallback reads it back)
-    d = {"eventId": e.id, "timestamp": e.timestamp, "eventType": ET(e.event_type).name if known else int(e.event_type),
+    # an out-of-range type is written as its decimal text in a JSON string (UnmarshalText's
+    # strconv.ParseInt fallback reads it back; Go's MarshalText would write "EventType(n)", which its
+    # own UnmarshalText rejects)
+    d = {"eventId": e.id, "timestamp": e.timestamp, "eventType": ET(e.event_type).name if known else str(int(e.event_type)),
          "version": e.version, "taskId": e.task_id}
     if known:
         d[attributes_key(e.event_type)] = attributes_json(e)

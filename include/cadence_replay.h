@@ -521,8 +521,22 @@ int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksu
 /* Batched prepareVersionHistory over device arrays (one result per task). */
 int crr_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* results, crr_vh_item* out_items, void* stream);
 
-/* Select the HIP device for subsequent calls from this thread. */
+/* Select the HIP device for subsequent calls from this thread (hipSetDevice: HIP's selection is per
+ * host thread).
+ *
+ * Thread model.  Every entry point may be called from any host thread, concurrently.  A call on a
+ * non-NULL stream runs on that stream's device whatever the calling thread has selected (the thread's
+ * selection is restored on return), so a cgo caller whose goroutine migrates between OS threads needs
+ * no runtime.LockOSThread as long as it passes its own stream; with a NULL stream the call uses the
+ * thread's current device (pin the goroutine: INTEGRATION.md §4).  Launch state -- the side streams the
+ * tier segments fork onto, the timing events -- is kept per device, created on first use and guarded
+ * by a per-device mutex for the duration of a call's enqueue; crr_last_kernel_ms / crr_timing_* /
+ * crr_segment_* report the last calls on the current device.  crr_release destroys that state. */
 int crr_set_device(int device);
+
+/* Teardown: synchronise and destroy every device's side streams and events (no call may be in flight).
+ * A later call recreates what it needs.  Returns 0, or -1 if a device could not be selected. */
+int crr_release(void);
 
 /* Library / ABI version; struct sizes for binding-time layout checks. */
 int crr_abi_version(void);

@@ -1,17 +1,17 @@
 #!/bin/bash
-# GPU parity tests of the in-tree library, kernel timing of config 2 and of the mixed workload,
-# then kernel timing of build/variants/lib_<v>.so ($VARIANTS)
+# GPU suite then the headline bench (config 2 only), each step under its own time limit; stops at the
+# first failure.  TESTS=<pytest node ids> narrows the suite; NO_BENCH=1 skips the bench.
 set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python tools/prof_kernel.py --reps 7 >> gpurun_out/check.jsonl 2>> gpurun_out/check.err
-rc=$?; echo "config2 timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python tools/prof_kernel.py --mixed --wf ${MIXED_WF:-200000} --reps 5 >> gpurun_out/check.jsonl 2>> gpurun_out/check.err
-rc=$?; echo "mixed timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
-if [ -n "${LT_N:-}" ]; then
-  timeout -k 10 400 python -u tools/prof_longtail.py --n $LT_N --thresholds 256 >> gpurun_out/check_lt.jsonl 2>> gpurun_out/check.err
-  rc=$?; echo "longtail timing rc=$rc" >> gpurun_out/status.log; [ $rc -ne 0 ] && exit $rc
+log() { echo "$(date +%T) $*" >> "$R/gpurun_out/status.log"; }
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 240 --timeout-method thread \
+  > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; log "pytest rc=$rc"; [ $rc -ne 0 ] && { tail -30 gpurun_out/pytest_gpu.log; exit $rc; }
+tail -3 gpurun_out/pytest_gpu.log
+if [ -z "${NO_BENCH:-}" ]; then
+  timeout -k 10 300 python -u bench.py --headline-only --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench_headline.log 2>&1
+  rc=$?; log "bench rc=$rc"; [ $rc -ne 0 ] && { tail -30 gpurun_out/bench_headline.log; exit $rc; }
+  tail -c 1500 gpurun_out/bench_headline.log
 fi
-bash scripts/gpu_exp.sh
+exit 0

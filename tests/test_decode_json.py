@@ -42,7 +42,7 @@ def test_json_histories_decode_like_flatten():
     assert_same_batch(decode_histories(json_sources(hs), known_domains=KNOWN), flatten(hs, known_domains=KNOWN))
 
 
-@pytest.mark.parametrize("encoding", ["", "unknown"])   # EncodingTypeEmpty / Unknown: json.Unmarshal too
+@pytest.mark.parametrize("encoding", ["", "unknow"])   # EncodingTypeEmpty / Unknown ("unknow", constants.go:66)
 def test_backward_compatible_encodings_decode_as_json(encoding):
     hs = synth_mixed.mixed_histories(50, 33, multi_version=True)
     assert_same_batch(decode_histories(json_sources(hs, encoding), known_domains=KNOWN), flatten(hs, known_domains=KNOWN))
@@ -72,8 +72,9 @@ def _events():
 
 
 def test_go_json_conventions():
-    """encoding/json: keys match case-insensitively, enums by name in any case or as numbers, null
-    leaves a field unset, unknown keys are ignored, the last of duplicate keys wins."""
+    """encoding/json: keys match case-insensitively, enums by name in any case or as decimal text (in
+    a JSON string: UnmarshalText), null leaves a field unset, unknown keys are ignored, the last of
+    duplicate keys wins."""
     evs = _events()
     raw = [event_json(e) for e in evs]
     raw[0] = {k.upper(): v for k, v in raw[0].items()}              # "EVENTID", "EVENTTYPE", ...
@@ -81,7 +82,7 @@ def test_go_json_conventions():
     attrs = raw[0]["WORKFLOWEXECUTIONSTARTEDEVENTATTRIBUTES"]
     attrs["initiator"] = "retrypolicy"
     attrs["somethingNew"] = {"nested": [1, 2.5e3, None, True, "x\\u00e9"]}
-    raw[1]["eventType"] = 4                                          # numeric EventType
+    raw[1]["eventType"] = "+4"                                       # UnmarshalText: strconv.ParseInt
     raw[1]["decisionTaskScheduledEventAttributes"]["attempt"] = None   # null: stays 0
     raw[2]["decisionTaskTimedOutEventAttributes"]["timeoutType"] = "3"  # UnmarshalText's numeric fallback
     text = json.dumps(raw).replace('"version": 7', '"version": 99, "version": 7', 1)   # duplicate: last wins
@@ -93,7 +94,17 @@ def test_go_json_conventions():
 
 @pytest.mark.parametrize("blob", [b'[{"eventId": 1.5}]', b'[{"eventId": "1"}]', b'[{"eventId": 1}', b'[null]',
                                   b'[{"eventType": "NoSuchEvent"}]', b'[{"eventId": 99999999999999999999}]',
-                                  b'{"eventId": 1}', b'[{"eventId": 1}] x'])
+                                  b'{"eventId": 1}', b'[{"eventId": 1}] x',
+                                  # enums implement UnmarshalText only: a bare number is a type error, and
+                                  # so is Go's own MarshalText of an out-of-range type
+                                  b'[{"eventType": 4}]', b'[{"eventType": "EventType(99)"}]',
+                                  b'[{"eventType": " 4"}]', b'[{"eventType": "4294967296"}]',
+                                  # the JSON number grammar, inside a skipped value too
+                                  b'[{"eventId": 1, "x": 1-2e}]', b'[{"eventId": 1, "x": 01}]',
+                                  b'[{"eventId": 1, "x": 1.}]', b'[{"eventId": 1, "x": 1e+}]',
+                                  # nesting past encoding/json's maxNestingDepth (10000)
+                                  b'[{"eventId": 1, "x": ' + b'[' * 10001 + b']' * 10001 + b'}]',
+                                  b'[{"eventId": 1, "x": ' + b'[' * 1000000 + b'}]'])
 def test_json_errors_are_deserialization_errors(blob):
     src = [WorkflowSource(blobs=[json.dumps([event_json(e) for e in _events()]).encode(), blob],
                           encodings=["json", "json"])]
@@ -102,11 +113,34 @@ def test_json_errors_are_deserialization_errors(blob):
     assert ei.value.code == -5 and ei.value.blob == 1
 
 
-def test_unknown_encoding_rejected():   # NewUnknownEncodingTypeError (serializer.go:326-327)
-    src = [WorkflowSource(blobs=[b"[]"], encodings=["gob"])]
+@pytest.mark.parametrize("encoding", ["gob", "unknown"])
+def test_unknown_encoding_rejected(encoding):   # NewUnknownEncodingTypeError (serializer.go:326-327)
+    src = [WorkflowSource(blobs=[b"[]"], encodings=[encoding])]
     with pytest.raises(DeserializationError) as ei:
         decode_histories(src)
     assert ei.value.code == -6
+
+
+def test_unread_attributes_are_syntax_checked_only():
+    """Documented narrowing (json_decode.h): an attributes object of another event type is checked for
+    JSON syntax, not decoded into its Go struct, so a type error json.Unmarshal would report there (a
+    bare-number timeoutType under decisionTaskTimedOutEventAttributes of a DecisionTaskScheduled event)
+    is accepted.  Pinned so a change in either direction is deliberate."""
+    blob = (b'[{"eventId": 2, "version": 7, "eventType": "DecisionTaskScheduled", '
+            b'"decisionTaskTimedOutEventAttributes": {"timeoutType": 3}}]')
+    got = decode_histories([WorkflowSource(blobs=[blob], encodings=["json"])])
+    assert got.n_events == 1
+
+
+def test_nesting_within_the_depth_limit_is_accepted():
+    """A skipped value nested to exactly encoding/json's limit decodes (10000 levels with the batch
+    array and the event object)."""
+    evs = _events()
+    text = json.dumps([event_json(e) for e in evs])
+    deep = b'[' * 9998 + b']' * 9998
+    blob = text.encode().replace(b'"eventId": 1,', b'"eventId": 1, "x": ' + deep + b',', 1)
+    got = decode_histories([WorkflowSource(blobs=[blob], encodings=["json"])])
+    assert_same_batch(got, flatten([WorkflowHistory(batches=[evs])]))
 
 
 def test_empty_json_blob_is_an_empty_batch():   # DeserializeBatchEvents: len(data) == 0 -> no events

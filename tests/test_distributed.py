@@ -30,10 +30,11 @@ def _worker(rank, world, port, q):
     res = oracle.replay(batch, 1)
     # the digest code the GPU ranks run (dist.digest_torch over the raw exec-row bytes), here on CPU tensors
     raw = torch.from_numpy(np.ascontiguousarray(res.exec[mine]).view(np.uint8).reshape(-1).copy())
-    t = cdist.digest_torch(torch, raw, int(mine.sum()))
-    assert (t.numpy() == cdist.digest_numpy(res.exec[mine])).all()
+    wfb = torch.from_numpy(np.ascontiguousarray(batch.wf[mine]).view(np.uint8).reshape(-1).copy())
+    t = cdist.digest_torch(torch, raw, int(mine.sum()), wfb)
+    assert (t.numpy() == cdist.digest_numpy(res.exec[mine], batch.wf["ev_count"][mine])).all()
     cdist.all_reduce_digest(torch, dist, t)
-    q.put((rank, t.numpy().tolist(), cdist.digest_numpy(res.exec).tolist()))
+    q.put((rank, t.numpy().tolist(), cdist.digest_numpy(res.exec, batch.wf["ev_count"]).tolist()))
     dist.destroy_process_group()
 
 

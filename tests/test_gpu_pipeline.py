@@ -102,12 +102,40 @@ def test_streaming_pipeline_matches_oracle(eng, wire):
 
 @pytest.mark.gpu
 def test_device_digest_equals_host_digest(eng):
+    """Device digest == host digest on a batch with failures and continue-as-new runs (each new run is
+    its own workflow row), and on a passive-replication step (ApplyEvents onto loaded states): the
+    events field counts the events each call applied."""
     import torch
     from cadence_amd import dist
-    b = interleave(_mixed(2000, 5, mean_len=50, invalid_rate=0.1))
+    b = interleave(_mixed(2000, 5, mean_len=50, invalid_rate=0.1, can_rate=0.3))
     db = eng.upload(b)
     eng.launch(db)
-    d_dev = dist.digest_torch(torch, db.tensors["exec"], b.n_wf).cpu().numpy()
+    d_dev = dist.digest_torch(torch, db.tensors["exec"], b.n_wf, db.tensors["wf"]).cpu().numpy()
     res = eng.download(db)
-    assert (d_dev == dist.digest_numpy(res.exec)).all()
+    assert (d_dev == dist.digest_numpy(res.exec, b.wf["ev_count"])).all()
     assert d_dev[1] + d_dev[2] == b.n_wf and d_dev[2] > 0
+    ok = res.exec["status"] == 0
+    assert d_dev[0] == int(b.wf["ev_count"][ok].sum())
+    assert (b.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()
+
+
+@pytest.mark.gpu
+def test_device_digest_counts_resumed_events(eng):
+    import torch
+    from cadence_amd import dist
+    from cadence_amd.replication import PassiveReplication
+    b = interleave(_mixed(1500, 9, mean_len=40))
+    pr = PassiveReplication(eng, b)
+    pr.setup()
+    pr.restore()
+    pr.step()
+    n = pr.batch.n_wf
+    exec_t, wf_t = pr.db.tensors["exec"], pr.db_new.tensors["wf"]     # loaded rows updated in place
+    d_dev = dist.digest_torch(torch, exec_t, n, wf_t).cpu().numpy()
+    res = eng.download(pr.db)
+    wf = wf_t[: n * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
+    assert (d_dev == dist.digest_numpy(res.exec, wf["ev_count"])).all()
+    ok = res.exec["status"] == 0
+    assert d_dev[0] == int(wf["ev_count"][ok].sum()) and 0 < d_dev[0] <= pr.n_events
+    # NextEventID - 1 would count the loaded prefix too
+    assert d_dev[0] < int((res.exec["next_event_id"][ok] - 1).sum())

@@ -33,6 +33,21 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
+def test_release_without_device_state_is_a_no_op():
+    """crr_release (teardown of the per-device launch state) is safe to call before any launch, with no
+    GPU visible: there is no state, so it touches no device and returns 0; the timing read-outs then
+    report nothing rather than stale values."""
+    lib = ctypes.CDLL(LIB)
+    lib.crr_release.restype = ctypes.c_int
+    lib.crr_last_kernel_ms.restype = ctypes.c_float
+    lib.crr_last_kernel_ms.argtypes = [ctypes.c_int]
+    assert lib.crr_release() == 0
+    assert lib.crr_release() == 0
+    assert lib.crr_last_kernel_ms(1) == -1.0
+    assert lib.crr_last_kernel_ms(7) == -1.0
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")
 def test_library_crc32_matches_zlib():
     import zlib
     from cadence_amd.engine import crc32
@@ -127,17 +142,22 @@ def test_flatten_capacities_bound_live_sets():
 
 
 def test_digest_numpy_matches_torch():
+    """The digest's events field is each OK workflow's ev_count (the events this call applied), not its
+    NextEventID: a resumed run (passive replication) and a continue-as-new run start past event 1."""
     import torch
     from cadence_amd import dist
     rows = np.zeros(5, abi.EXEC_ROW)
     rows["status"] = [0, 0, 3, 0, 0]
     rows["checksum"] = [1, 0xFFFFFFFF, 7, 12345, 0x80000000]
-    rows["next_event_id"] = [30, 24, 5, 2 ** 31 + 7, 2 ** 40 + 2]   # IDs past the low int32 word too
+    rows["next_event_id"] = [30, 24, 5, 2 ** 31 + 7, 2 ** 40 + 2]   # resumed rows: NextEventID != events + 1
     rows["inconsistencies"] = [0, 1, 0, 2, 0]
+    wf = np.zeros(5, abi.WORKFLOW)
+    wf["ev_count"] = [29, 23, 4, 3, 2 ** 31 - 1]
     raw = torch.from_numpy(rows.view(np.uint8).copy())
-    d = dist.digest_numpy(rows)
-    assert (dist.digest_torch(torch, raw, 5).numpy() == d).all()
-    assert d[0] == 29 + 23 + 2 ** 31 + 6 + 2 ** 40 + 1
+    d = dist.digest_numpy(rows, wf["ev_count"])
+    assert (dist.digest_torch(torch, raw, 5, torch.from_numpy(wf.view(np.uint8).copy())).numpy() == d).all()
+    assert d[0] == 29 + 23 + 3 + 2 ** 31 - 1
+    assert d[1] == 4 and d[2] == 1 and d[5] == 3
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")

@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--config-steps", type=int, default=5, help="timed steps of the config 3 / 4 / replication lines")
     p.add_argument("--c3-workflows", type=int, default=1_250_000, help="config 3 mixed workflows per GPU")
     p.add_argument("--c4-workflows", type=int, default=2000, help="config 4 logical workflows per GPU")
+    p.add_argument("--c5-workflows", type=int, default=1_000_000, help="config 5 multi-version workflows per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the CPUs this process may use)")
     p.add_argument("--cpu-sample", type=int, default=1_000_000, help="config 2 workflows in the CPU baseline sample")
@@ -301,6 +302,246 @@ def _resume_bytes(pr):
     return int(pr.n_events * abi.BYTES_PER_EVENT + b.n_wf * (abi.WORKFLOW.itemsize + 2 * abi.EXEC_ROW.itemsize + 96) + 2 * rows)
 
 
+# ---- config 5: NDC / XDC -----------------------------------------------------------------------------------------
+def config5(ctx, n_wf, shard):
+    """BASELINE config 5 on this rank's shards: (a) multi-version mixed histories rebuilt onto a reset
+    branch (Rebuild: the target branch token, the last-item check, RefreshTasks) -- failover versions at
+    batch boundaries give 1-4 VersionHistory items; (b) crr_ndc_prepare over one replication task per
+    workflow against its replayed VersionHistory (append / new branch / duplicate / out-of-order); (c)
+    crr_checksum, the Load verify path, over the replayed rows.  Each with its roofline and an oracle
+    parity check."""
+    from cadence_amd import ndc, synth, synth_native
+    from cadence_amd.flatten import interleave
+    args, torch, eng = ctx.args, ctx.torch, ctx.eng
+    t0 = time.time()
+    canon = as_rebuilds(synth_native.mixed(n_wf * ctx.world, multi_version=True, shard=shard, seed=0xCAD00005), 0xCAD00005)
+    batch = interleave(canon)
+    db = eng.upload(batch)
+    setup = time.time() - t0
+    wall, ms = timed_steps(ctx, db, args.config_steps, 1)
+    res = eng.download(db)
+    from cadence_amd import dist as cdist
+    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"])
+    tot_ev, tot_wf = ctx.reduce([float(batch.n_events), float(batch.n_wf)], op="sum")
+    out = {"workload": f"config 5: {n_wf} multi-version mixed histories per GPU rebuilt onto reset branches "
+                       "(state_rebuilder.go:97-191: target branch token, last-item check, RefreshTasks), failover "
+                       "versions at batch boundaries",
+           "rebuild": {"value": tot_ev * args.config_steps / wall, "unit": "events/s",
+                       "workflows_rebuilt_per_s": tot_wf * args.config_steps / wall,
+                       "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
+                       "events_per_gpu": batch.n_events, "workflows_per_gpu": batch.n_wf,
+                       "workflows_ok": int(digest[1]),
+                       "vh_items_per_workflow": float(res.exec["n_vh_items"][res.exec["status"] == 0].mean()),
+                       "roofline": roofline(synth.algorithmic_bytes(batch, res), float(np.mean(ms)), FAST_GROUP),
+                       "setup_s": setup}}
+    if ctx.rank == 0:
+        from oracle import oracle
+        from cadence_amd.result import diff_results
+        sample = as_rebuilds(synth_native.mixed(20_000, multi_version=True, seed=0xCAD00015), 0xCAD00015)
+        b = interleave(sample)
+        d = diff_results(b, eng.replay(b), sample, oracle.replay(sample, host_cpus()))
+        out["rebuild"]["parity_sample"] = {"workflows": sample.n_wf, "bit_exact": not d, "first_diffs": d[:3]}
+    # (b) NDC branch decisions
+    e, v, c = ndc.version_histories(canon)
+    nb = ndc.tasks_from_histories(e, v, c, 0xCAD00025 + ctx.rank)
+    out["ndc_prepare"] = ndc_line(ctx, nb)
+    # (c) Load verify
+    out["checksum_verify"] = checksum_line(ctx, db, batch, res)
+    del db
+    return out
+
+
+def as_rebuilds(canon, seed):
+    """Rebuild inputs for every workflow of a canonical batch: StateRebuilder.Rebuild replays the history
+    onto a new branch whose token it installs (state_rebuilder.go:150), checks the last VersionHistory item
+    against the requested (event ID, version) (:160-176; 2 % are given a mismatching one) and refreshes the
+    tasks (:183)."""
+    from cadence_amd import abi, synth
+    rng = np.random.default_rng(seed)
+    n = canon.n_wf
+    cnt = canon.wf["ev_count"].astype(np.int64)
+    last = canon.wf["ev_begin"].astype(np.int64) + np.maximum(cnt - 1, 0)
+    tree = canon.arena[(canon.wf["start_token_off"].astype(np.int64)[:, None] + 8 + np.arange(36)[None, :])]
+    tok = synth.branch_tokens(tree, synth.uuid_ascii(rng, n))
+    base = canon.arena.size
+    canon.arena = np.concatenate([canon.arena, tok.reshape(-1)])
+    canon.wf["final_token_off"] = base + np.arange(n, dtype=np.int64) * 96
+    canon.wf["final_token_len"] = 96
+    ok = cnt > 0
+    canon.wf["rebuild_last_event_id"] = np.where(ok, canon.cols["event_id"][last], 0) + (rng.random(n) < 0.02)
+    canon.wf["rebuild_last_event_version"] = np.where(ok, canon.cols["version"][last], 0)
+    canon.wf["flags"] |= abi.WF_FLAG_REFRESH_TASKS
+    return canon
+
+
+def ndc_line(ctx, nb):
+    from cadence_amd import abi, ndc
+    from oracle import oracle
+    torch, eng, args = ctx.torch, ctx.eng, ctx.args
+    dev = eng.dev
+    n = len(nb.tasks)
+
+    def up(a):
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        t = torch.empty(max(raw.size, 1), dtype=torch.uint8, device=dev)
+        t[:raw.size].copy_(torch.from_numpy(raw))
+        return t
+
+    T = {"tasks": up(nb.tasks), "branches": up(nb.branches), "items": up(nb.items)}
+    res = torch.zeros(max(n, 1) * abi.NDC_RESULT.itemsize, dtype=torch.uint8, device=dev)
+    out = torch.zeros(nb.n_out_items * abi.VH_ITEM.itemsize, dtype=torch.uint8, device=dev)
+    ci = abi.CNdcInputs()
+    ci.tasks, ci.branches, ci.items = T["tasks"].data_ptr(), T["branches"].data_ptr(), T["items"].data_ptr()
+    ci.n_tasks = n
+    import ctypes
+    s = torch.cuda.current_stream(dev)
+
+    def launch():
+        rc = eng.lib.crr_ndc_prepare(ctypes.byref(ci), ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_ndc_prepare failed: {rc}")
+
+    launch()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.config_steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(s)
+        launch()
+        b.record(s)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = ctx.reduce([time.perf_counter() - t0])[0]
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    got = res.cpu().numpy().view(abi.NDC_RESULT)[:n]
+    tot = ctx.reduce([float(n)], op="sum")[0]
+    # algorithmic bytes: the task, its branch descriptors and every item read, the result and the new
+    # branch's items written
+    alg = (n * (abi.NDC_TASK.itemsize + abi.NDC_RESULT.itemsize) + int(nb.tasks["branch_count"].sum()) * abi.NDC_BRANCH.itemsize
+           + int(nb.branches["item_count"].sum() + nb.tasks["incoming_count"].sum()) * abi.VH_ITEM.itemsize
+           + int(got["new_item_count"].clip(0).sum()) * abi.VH_ITEM.itemsize)
+    line = {"workload": "one replication task per workflow against its replayed VersionHistories: prepareVersionHistory "
+                        "(ndc/branch_manager.go:87-149) -- LCA, appendable / fork, DuplicateUntilLCAItem, AddVersionHistory, "
+                        "verifyEventsOrder, IsRebuilt",
+            "value": tot * args.config_steps / wall, "unit": "replication tasks/s", "tasks_per_gpu": n,
+            "outcomes": {k: int(v) for k, v in zip(("append", "new_branch", "duplicate", "retry_task", "error"),
+                                                   (((got["status"] == 0) & (got["action"] == abi.NDC_APPEND)).sum(),
+                                                    ((got["status"] == 0) & (got["action"] == abi.NDC_NEW_BRANCH)).sum(),
+                                                    ((got["status"] == 0) & (got["action"] == abi.NDC_DUPLICATE)).sum(),
+                                                    (got["status"] == abi.Status.NDC_RETRY_TASK).sum(),
+                                                    ((got["status"] != 0) & (got["status"] != abi.Status.NDC_RETRY_TASK)).sum()))},
+            "roofline": roofline(alg, k_ms, "crr::ndc_prepare_kernel")}
+    if ctx.rank == 0:
+        m = min(n, 200_000)
+        sub = ndc.NdcBatch(tasks=nb.tasks[:m], branches=nb.branches, items=nb.items, n_out_items=nb.n_out_items)
+        want, _ = oracle.ndc_prepare(sub)
+        line["parity_sample"] = {"tasks": m, "bit_exact": bool((got[:m].tobytes() == want.tobytes()))}
+    return line
+
+
+def checksum_line(ctx, db, batch, res):
+    """crr_checksum (mutable_state_builder.go:334-348 -> checksum.go:45-54, the Load verify path) over the
+    replayed rows, HBM-resident: every workflow's thriftrw payload rebuilt from its rows and CRC'd."""
+    import ctypes
+    torch, eng, args = ctx.torch, ctx.eng, ctx.args
+    n = db.n_wf
+    out = torch.zeros(max(n, 1), dtype=torch.int32, device=eng.dev)
+    s = torch.cuda.current_stream(eng.dev)
+
+    def launch():
+        rc = eng.lib.crr_checksum(ctypes.byref(db.c_in), ctypes.byref(db.c_out), ctypes.c_void_p(out.data_ptr()),
+                                  ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_checksum failed: {rc}")
+
+    launch()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.config_steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(s)
+        launch()
+        b.record(s)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = ctx.reduce([time.perf_counter() - t0])[0]
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    got = out.cpu().numpy().view(np.uint32)[:n]
+    ok = res.exec["status"] == 0
+    ex = res.exec
+    rows = (8 * (ex["n_activity"].astype(np.int64) + ex["n_timer"] + ex["n_child"] + ex["n_rc"] + ex["n_signal"])
+            + 16 * ex["n_vh_items"].astype(np.int64))[ok].sum()
+    alg = int(n * (208 + 168 + 4) + int(rows) + int(np.minimum(batch.wf["start_token_len"], 4096)[ok].sum()))
+    tot = ctx.reduce([float(n)], op="sum")[0]
+    return {"workload": "Load verify: the mutable-state checksum recomputed from the replayed rows of every workflow",
+            "value": tot * args.config_steps / wall, "unit": "workflows verified/s",
+            "matches_replay_checksums": bool((got[ok] == ex["checksum"][ok]).all()), "verified": int(ok.sum()),
+            "roofline": roofline(alg, k_ms, "crr::checksum_kernel")}
+
+
+# ---- persisted blobs -> rows (rank 0, N = 1) ---------------------------------------------------------------------
+def blob_to_rows(ctx, canon, resident_digest, name, chunks=8):
+    """The real input path end to end: persisted thriftrw blobs (one per ApplyEvents batch, as
+    persistence returns them: serializer.go:109-119) in pinned host memory -> H2D -> device ingest
+    (crr_ingest_plan + crr_ingest_layout: decode, intern, order, interleave) -> crr_replay ->
+    crr_compact_rows -> D2H of the exec rows + live rows; chunked, uploads ahead of the work, two compute
+    streams.  Every host and device stage is inside the clock; the blob encoding itself (what
+    persistence stores) is setup.  Beside it `device_resident`: the same with the blobs already in HBM
+    (ingest + replay + compaction, no PCIe)."""
+    from cadence_amd import abi
+    from cadence_amd import dist as cdist
+    from cadence_amd.blobs import encode_batch
+    from cadence_amd.pipeline import BlobStreamingReplay, split_blobs
+    t0 = time.time()
+    bs = encode_batch(canon)
+    parts = split_blobs(bs, chunks)
+    enc_s = time.time() - t0
+    sr = BlobStreamingReplay(ctx.eng, parts)
+    setup = time.time() - t0
+    sr.run()
+    runs = [sr.run() for _ in range(3)]
+    med = float(np.median([r["wall_s"] for r in runs]))
+    digest = np.zeros(6, np.int64)
+    for cr, evc in zip(sr.results(), sr.ev_counts()):
+        digest += cdist.digest_numpy(cr.exec, evc)
+    r0 = runs[0]
+    fig = {"workload": name, "events_per_s": r0["events"] / med, "ms": med * 1e3, "events": r0["events"],
+           "workflows": bs.n_wf, "blobs": bs.n_blobs, "blob_bytes": bs.n_bytes,
+           "blob_bytes_per_event": bs.n_bytes / max(r0["events"], 1), "chunks": len(parts),
+           "h2d_bytes": r0["h2d_bytes"], "h2d_GBs": r0["h2d_bytes"] / med / 1e9, "d2h_bytes": r0["d2h_bytes"],
+           "digest": [int(x) for x in digest], "setup_s": {"encode": enc_s, "upload_plan_alloc": setup - enc_s},
+           "note": "median of 3 passes; blobs in pinned host buffers as read from persistence; every stage timed"}
+    if resident_digest is not None:
+        fig["matches_resident_digest"] = fig["digest"] == [int(x) for x in resident_digest]
+    # the same work with the blobs already resident in HBM: device-side stages only
+    torch, eng = ctx.torch, ctx.eng
+    torch.cuda.synchronize()
+    tt = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        for i, p in enumerate(sr.parts):
+            s = sr.comp[i % 2]
+            S = p["ing"].plan(p["db"], s)
+            out = p["out"]
+            with torch.cuda.stream(s):
+                for k in ["exec", "scratch"] + ["out_" + t[0] for t in abi.TABLES]:
+                    out.tensors[k].zero_()
+            p["ing"].layout(p["db"], S, s, out=out)
+            eng.launch(out, s)
+            eng.compact(out, s)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - tt) / reps
+    fig["device_resident"] = {"events_per_s": r0["events"] / dt, "ms": dt * 1e3,
+                              "note": "blobs already in HBM: ingest (plan with its two stream syncs + layout) + replay + "
+                                      "compaction per chunk, no transfers"}
+    del sr
+    torch.cuda.empty_cache()
+    return fig
+
+
 # ---- rank 0, N = 1: end to end, host ingest, CPU baseline ---------------------------------------------------
 def end_to_end(ctx, n_wf, k, chunks=8):
     """Config 2 from host buffers: pinned staging, `chunks` chunks overlapped on three streams, the event
@@ -437,16 +678,32 @@ def main():
             lambda: synth_native.long_tail(60, shard=shard))
         del db4, b4, r4
         torch.cuda.empty_cache()
-        line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr}
+        c5 = config5(ctx, args.c5_workflows, shard)
+        torch.cuda.empty_cache()
+        line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr,
+                           "config5_ndc": c5}
     if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
         line["pcie_inclusive"] = end_to_end(ctx, args.workflows, args.activities)
         e2e = line["pcie_inclusive"]
         e2e["matches_resident_digest"] = e2e["digest"] == line["digest"] and e2e["columns_wide"]["digest"] == line["digest"]
         line["host_ingest"] = host_ingest(ctx, flat_s, flat_ev)
+        from cadence_amd import synth
+        c2_canon = synth.activity_chain(args.workflows, args.activities, synth.SEED_C2, with_keys=True,
+                                        wf_ids=np.arange(args.workflows))
+        line["blob_to_rows"] = {"config2": blob_to_rows(
+            ctx, c2_canon, line["digest"],
+            f"config 2 persisted: {args.workflows} activity-chain workflows, one thriftrw blob per ApplyEvents batch")}
+        del c2_canon
+        c3_canon = synth_native.mixed(args.c3_workflows, shard=(cdist.NUM_SHARDS, 1, 0))
+        line["blob_to_rows"]["config3_shard"] = blob_to_rows(
+            ctx, c3_canon, None, f"config 3 shard persisted: {args.c3_workflows} mixed histories, one thriftrw blob per batch")
+        del c3_canon
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ctx, res2, batch2, args.activities)
         if "pcie_inclusive" in line:
             line["pcie_inclusive"]["vs_cpu_baseline"] = line["pcie_inclusive"]["events_per_s"] / line["cpu_baseline"]["value"]
+        for k, fig in line.get("blob_to_rows", {}).items():
+            fig["vs_cpu_baseline"] = fig["events_per_s"] / line["cpu_baseline"]["value"]
     if ctx.rank == 0:
         print(json.dumps(line), flush=True)
     if ctx.world > 1:

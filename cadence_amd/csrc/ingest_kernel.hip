@@ -1,0 +1,1476 @@
+// ingest_kernel.hip -- persisted thriftrw history blobs in HBM -> the replay engine's wave-interleaved,
+// tiered crr_inputs, on the GPU (include/cadence_ingest.h).
+//
+// The host path this restates, step for step (byte-identical output, tests/test_gpu_ingest.py):
+//   cadence_amd/csrc/history_decode.cpp   the thriftrw walk (read_event / read_attributes / skip)
+//   cadence_amd/csrc/host_flatten.h       WfFlattener::add / batch_end / finish (columns, side records,
+//                                         interned keys, capacities, branch tokens)
+//   cadence_amd/flatten.py                live_set_bounds, tier_classes, interleave, _interleave_side
+//
+// Pipeline (crr_ingest_plan, then crr_ingest_layout once the caller has sized its buffers):
+//   1 blob_wf_kernel       blob -> workflow map
+//   2 blob_count_kernel    lane per blob: full thrift walk, counts (events, activity / start side
+//                          records, key strings); the first failing blob's error
+//   3 multi_scan           exclusive prefixes of the counts: every blob's slice of the canonical
+//                          (stride-1, workflow-order) scratch columns
+//   4 blob_decode_kernel   lane per blob: the same walk, writing columns, side records and key-string
+//                          references; domain names resolved against a device hash set
+//   5 wf_pass_kernel       lane per workflow: interning (per-workflow open-addressed table over string
+//                          hashes, exact byte compares), capacities, VH items, tasks, live-set bounds
+//                          (valid deletes through a second table), tier class, sort key
+//   6 radix sort (hipCUB)  device order = (long, tier | big, -length, index)
+//   7 geometry             per-group maxima (one wavefront per group), prefixes over groups and the
+//                          tail, tier boundaries, the summary
+//   layout                 interleaved columns + side records (block per group / tail workflow),
+//                          descriptors, branch tokens, reset keys
+//
+// Parsing is integer / byte work: lanes walk their own blob through a 16-byte register window (one
+// aligned dwordx4 load per 16 bytes instead of a dependent byte load each), no MFMA, no LDS staging.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cadence_ingest.h"
+#include "cadence_decode.h"
+
+namespace crr_ingest {
+
+using i64 = int64_t;
+using i32 = int32_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using u8 = uint8_t;
+
+enum : u32 { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10, T_STRING = 11,
+             T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15 };
+
+constexpr int kBlock = 256;
+constexpr i32 kLongHistory = 256;       // flatten.LONG_HISTORY
+constexpr i32 kCompactMaxEvents = 1023;  // flatten.COMPACT_MAX_EVENTS
+constexpr int kWide = 5;                 // flatten.WIDE
+constexpr int kMaps = 6;                 // act, timer, child, rc, sig, rp
+// flatten.TIER_SLOTS (act, timer, child, rc, sig, rp)
+__constant__ i32 kTierSlots[5][kMaps] = {{1, 1, 1, 1, 1, 1}, {2, 2, 1, 1, 1, 2}, {4, 3, 2, 1, 1, 4},
+                                         {8, 5, 3, 3, 3, 8}, {12, 8, 6, 4, 4, 8}};
+__constant__ i32 kWaveSmallTier[kMaps] = {40, 32, 16, 8, 8, 24};   // flatten.WAVE_SMALL_TIER
+constexpr i32 kWaveBigCap = 64;                                     // flatten.WAVE_BIG_CAPS
+// host_flatten.h kTasksPerEvent
+__constant__ int8_t kTasksPerEvent[CRR_EV_TYPE_COUNT] = {
+    3, 2, 2, 2, 1, 1, 0, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+    0, 2, 1, 0, 0, 0, 0, 2, 2, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 1};
+
+// ---- scratch layout ------------------------------------------------------------------------------------
+// Per blob counts (u32): events, activity side records, start side records, key strings.
+constexpr int kCnt = 4;
+struct KeyRef {     // one string to intern, in parse order: an event's key or a previous reset point
+  u64 off;          // byte offset of the string in `bytes`
+  u32 len;
+  u32 is_reset;     // 0: key column of event `dst`; 1: reset_keys[dst]
+  u64 dst;
+};
+
+struct Plan {       // pointers into the caller's scratch (carved by carve())
+  u32* blob_wf;              // [n_blobs]
+  u32* cnt;                  // [kCnt][n_blobs]
+  u64* off;                  // [kCnt][n_blobs + 1] exclusive prefixes
+  u64* err;                  // [1] (blob << 8) | -code, min wins
+  u64* tile;                 // scan tiles
+  // canonical scratch columns [max_events]
+  u8* etype; i64* id; i64* ver; i64* ts; i64* task; i64* ref; u32* key; i32* aux;
+  crr_activity_side* act;    // [max_events]
+  crr_start_side* start;     // [max_events]
+  KeyRef* keys;              // [2 * max_events] key entries (event keys + previous reset points)
+  u32* entry_id;             // [2 * max_events] interned id of each key entry
+  u32* reset_flag;           // [2 * max_events] 1: a reset-point entry (scan input)
+  u64* reset_pos;            // [2 * max_events + 1] its reset_keys index (exclusive prefix)
+  u64* table;                // per-workflow hash tables [2 * max_events + 64 * n_wf]
+  // per workflow (canonical order)
+  i32* wf_info;              // [kWfInfo][n_wf]
+  u64* sort_in; u64* sort_out;     // [n_wf]
+  void* sort_tmp; size_t sort_tmp_bytes;
+  u32* perm; u32* inv;       // [n_wf]
+  u64* arena_off;            // [n_wf + 1]
+  u64* gvals;                // [kGeo][n_groups]   group maxima, then exclusive prefixes in place
+  u64* tvals;                // [kGeo][n_wf]       tail values, then prefixes
+  u64* gpre; u64* tpre;
+  u32* counters;             // [16]
+  u32* dom_table; u32 dom_cap;
+  u32 n_blobs, n_wf;
+  u64 max_events;
+};
+// per-workflow info words (canonical index)
+enum { WI_COUNT = 0, WI_EMPTY_AT, WI_ACT, WI_TIMER, WI_CHILD, WI_RC, WI_SIG, WI_VH, WI_RP, WI_TASKS, WI_STARTED,
+       WI_TIER, WI_LONG, WI_BIG, kWfInfo };
+// geometry values per device position: count, 8 table caps, activity / start side counts
+enum { GV_LEN = 0, GV_CAP0 = 1, GV_ACT_SIDE = 9, GV_START_SIDE = 10, kGeo = 11 };
+// counters
+enum { C_N_LANE = 0, C_N_BIG = 1, C_TIER0 = 2 /* .. C_TIER0 + 5 */, C_SMALL_TAIL_BAD = 8, C_NEW_RUN = 9 };
+
+__host__ __device__ inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t kDomainBytes = 64 * 1024;   // the known-domain set (<= 8192 names)
+constexpr i32 kErrScratch = -100;            // CRR_INGEST_SCRATCH_TOO_SMALL
+
+// ---- byte reader over one blob: a 16-byte aligned window in registers ----------------------------------
+struct Rd {
+  const u8* b;
+  u64 p, end;
+  u64 wb;            // window base (aligned), ~0: none
+  uint4 w;
+  int err;           // CRR_DECODE_* (0 ok)
+
+  __device__ __forceinline__ void init(const u8* bytes, u64 begin, u64 e) {
+    b = bytes; p = begin; end = e; wb = ~0ull; err = 0;
+  }
+  __device__ __forceinline__ bool need(u64 n) {
+    if (err) return false;
+    if (end - p < n) { err = CRR_DECODE_TRUNCATED; return false; }
+    return true;
+  }
+  __device__ __forceinline__ u32 at(u64 q) {   // byte q (caller checked bounds)
+    const u64 a = q & ~15ull;
+    if (a != wb) {
+      w = *reinterpret_cast<const uint4*>(b + a);
+      wb = a;
+    }
+    const u32 o = (u32)(q & 15);
+    const u32 word = (o < 8) ? ((o < 4) ? w.x : w.y) : ((o < 12) ? w.z : w.w);
+    return (word >> ((o & 3) * 8)) & 0xff;
+  }
+  __device__ __forceinline__ u32 u8_() {
+    if (!need(1)) return 0;
+    return at(p++);
+  }
+  __device__ __forceinline__ i32 be16() {
+    if (!need(2)) return 0;
+    const u32 v = (at(p) << 8) | at(p + 1);
+    p += 2;
+    return (i32)(int16_t)v;
+  }
+  __device__ __forceinline__ i32 be32() {
+    if (!need(4)) return 0;
+    u32 v = 0;
+    for (int i = 0; i < 4; ++i) v = (v << 8) | at(p + i);
+    p += 4;
+    return (i32)v;
+  }
+  __device__ __forceinline__ i64 be64() {
+    if (!need(8)) return 0;
+    u64 v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | at(p + i);
+    p += 8;
+    return (i64)v;
+  }
+  // a thrift string: its (offset, length) in the blob bytes
+  __device__ __forceinline__ void str(u64& off, u32& len) {
+    const i32 n = be32();
+    if (err) return;
+    if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+    if (!need((u64)n)) return;
+    off = p;
+    len = (u32)n;
+    p += (u64)n;
+  }
+  // skip one value of `type` (history_decode.cpp Reader::skip: nesting deeper than 64 is BAD_TYPE),
+  // iteratively: a stack of open containers (struct: until its stop byte; list / set / map: remaining
+  // elements and their types)
+  __device__ void skip(u32 type) {
+    struct Lvl { u8 kind, t1, t2, pad; i32 rem; };
+    Lvl st[66];
+    int d = 0;          // depth of the value about to be skipped
+    u32 t = type;
+    for (;;) {
+      if (err) return;
+      if (d > 64) { err = CRR_DECODE_BAD_TYPE; return; }
+      bool pushed = false;
+      switch (t) {
+        case T_BOOL: case T_BYTE: if (need(1)) p += 1; break;
+        case T_I16: if (need(2)) p += 2; break;
+        case T_I32: if (need(4)) p += 4; break;
+        case T_DOUBLE: case T_I64: if (need(8)) p += 8; break;
+        case T_STRING: {
+          const i32 n = be32();
+          if (err) return;
+          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+          if (need((u64)n)) p += (u64)n;
+          break;
+        }
+        case T_STRUCT: st[d] = Lvl{T_STRUCT, 0, 0, 0, 0}; pushed = true; break;
+        case T_MAP: {
+          const u32 kt = u8_(), vt = u8_();
+          const i32 n = be32();
+          if (err) return;
+          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+          st[d] = Lvl{T_MAP, (u8)kt, (u8)vt, 0, 2 * n};
+          pushed = true;
+          break;
+        }
+        case T_SET: case T_LIST: {
+          const u32 et = u8_();
+          const i32 n = be32();
+          if (err) return;
+          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+          st[d] = Lvl{T_LIST, (u8)et, (u8)et, 0, n};
+          pushed = true;
+          break;
+        }
+        default: err = CRR_DECODE_BAD_TYPE; return;
+      }
+      if (err) return;
+      if (pushed) ++d;
+      // the next value to skip: the innermost open container's next element, popping finished ones
+      for (;;) {
+        if (d == 0) return;
+        Lvl& L = st[d - 1];
+        if (L.kind == T_STRUCT) {
+          const u32 ft = u8_();
+          if (err) return;
+          if (ft == T_STOP) { --d; continue; }
+          (void)be16();
+          t = ft;
+          break;
+        }
+        if (L.rem == 0) { --d; continue; }
+        t = (L.kind == T_MAP && (L.rem & 1) == 0) ? L.t1 : L.t2;
+        if (L.kind != T_MAP) t = L.t1;
+        --L.rem;
+        break;
+      }
+    }
+  }
+  __device__ __forceinline__ bool want(u32 got, u32 expect) {   // Reader::want
+    if (got == expect) return true;
+    skip(got);
+    return false;
+  }
+};
+
+// The fields of one event ApplyEvents reads (host_flatten.h Attr / Event), strings as blob references.
+struct Attr {
+  i64 ref;
+  i32 aux;
+  u64 key_off; u32 key_len;
+  u64 dom_off; u32 dom_len;
+  i32 s2s, s2c, st2c, hb, has_retry, expiration;
+  i32 task_s2c, exec_s2c, backoff, initiator, attempt;
+  i64 expiration_ts;
+  i32 prev_mode;       // -1 nil, -2 Points nil, 0 list
+  u64 prev_pos;        // the final Points list: first element's byte offset, count, element type
+  i32 prev_n;
+  u32 prev_et;
+};
+struct Event {
+  i64 id, ts, ver, task;
+  i32 type;
+  Attr a;
+};
+
+__device__ __forceinline__ void attr_init(Attr& a) {
+  a.ref = 0; a.aux = 0; a.key_off = 0; a.key_len = 0; a.dom_off = 0; a.dom_len = 0;
+  a.s2s = a.s2c = a.st2c = a.hb = a.has_retry = a.expiration = 0;
+  a.task_s2c = a.exec_s2c = a.backoff = 0; a.initiator = CRR_INITIATOR_NIL; a.attempt = 0;
+  a.expiration_ts = 0; a.prev_mode = -1; a.prev_pos = 0; a.prev_n = 0; a.prev_et = 0;
+}
+
+__device__ __forceinline__ int attr_type_of_field(i32 id) {
+  if (id < 40 || id > 450 || id % 10) return -1;
+  return (id - 40) / 10;
+}
+
+// RetryPolicy{60 ExpirationIntervalInSeconds i32}
+__device__ void read_retry_policy(Rd& r, Attr& a) {
+  a.has_retry = 1;
+  for (;;) {
+    const u32 ft = r.u8_();
+    if (r.err || ft == T_STOP) return;
+    const i32 id = r.be16();
+    if (id == 60 && r.want(ft, T_I32)) a.expiration = r.be32();
+    else if (id != 60) r.skip(ft);
+  }
+}
+
+// ResetPoints{10 Points list<ResetPointInfo{10 BinaryChecksum}>}: only the final list's position is
+// kept; its strings are read once the event is complete (WfFlattener::add interns them there)
+__device__ void read_reset_points(Rd& r, Attr& a) {
+  a.prev_mode = -2;
+  for (;;) {
+    const u32 ft = r.u8_();
+    if (r.err || ft == T_STOP) return;
+    const i32 id = r.be16();
+    if (id == 10 && ft == T_LIST) {
+      const u32 et = r.u8_();
+      const i32 n = r.be32();
+      if (r.err) return;
+      if (n < 0) { r.err = CRR_DECODE_TRUNCATED; return; }
+      a.prev_mode = 0;
+      a.prev_pos = r.p;
+      a.prev_n = n;
+      a.prev_et = et;
+      for (i32 i = 0; i < n && !r.err; ++i) {
+        if (et != T_STRUCT) { r.skip(et); continue; }
+        for (;;) {
+          const u32 t2 = r.u8_();
+          if (r.err || t2 == T_STOP) break;
+          const i32 id2 = r.be16();
+          if (id2 == 10 && t2 == T_STRING) { u64 o; u32 l; r.str(o, l); }
+          else r.skip(t2);
+        }
+      }
+    } else {
+      r.skip(ft);
+    }
+  }
+}
+
+// history_decode.cpp read_attributes
+__device__ void read_attributes(Rd& r, int t, Attr& a) {
+  for (;;) {
+    const u32 ft = r.u8_();
+    if (r.err || ft == T_STOP) return;
+    const i32 id = r.be16();
+    if (r.err) return;
+    bool used = true;
+    switch (t) {
+      case CRR_EV_WORKFLOW_EXECUTION_STARTED:
+        if (id == 12 && ft == T_STRING) r.str(a.dom_off, a.dom_len);
+        else if (id == 40 && ft == T_I32) a.exec_s2c = r.be32();
+        else if (id == 50 && ft == T_I32) a.task_s2c = r.be32();
+        else if (id == 55 && ft == T_I32) a.initiator = r.be32();
+        else if (id == 80 && ft == T_I32) a.attempt = r.be32();
+        else if (id == 90 && ft == T_I64) a.expiration_ts = r.be64();
+        else if (id == 110 && ft == T_I32) a.backoff = r.be32();
+        else if (id == 130 && ft == T_STRUCT) read_reset_points(r, a);
+        else used = false;
+        break;
+      case CRR_EV_DECISION_TASK_SCHEDULED:
+        if (id == 20 && ft == T_I32) a.aux = r.be32();
+        else if (id == 30 && ft == T_I64) a.ref = r.be64();
+        else used = false;
+        break;
+      case CRR_EV_DECISION_TASK_STARTED:
+        if (id == 10 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_DECISION_TASK_COMPLETED:
+        if (id == 30 && ft == T_I64) a.ref = r.be64();
+        else if (id == 50 && ft == T_STRING) r.str(a.key_off, a.key_len);
+        else used = false;
+        break;
+      case CRR_EV_DECISION_TASK_TIMED_OUT:
+        if (id == 30 && ft == T_I32) a.aux = r.be32(); else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_SCHEDULED:
+        if (id == 10 && ft == T_STRING) r.str(a.key_off, a.key_len);
+        else if (id == 25 && ft == T_STRING) r.str(a.dom_off, a.dom_len);
+        else if (id == 45 && ft == T_I32) a.s2c = r.be32();
+        else if (id == 50 && ft == T_I32) a.s2s = r.be32();
+        else if (id == 55 && ft == T_I32) a.st2c = r.be32();
+        else if (id == 60 && ft == T_I32) a.hb = r.be32();
+        else if (id == 110 && ft == T_STRUCT) read_retry_policy(r, a);
+        else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_STARTED:
+      case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
+        if (id == 10 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_COMPLETED:
+        if (id == 20 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_FAILED:
+      case CRR_EV_ACTIVITY_TASK_CANCELED:
+        if (id == 30 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED:
+      case CRR_EV_TIMER_FIRED:
+      case CRR_EV_TIMER_CANCELED:
+        if (id == 10 && ft == T_STRING) r.str(a.key_off, a.key_len); else used = false;
+        break;
+      case CRR_EV_TIMER_STARTED:
+        if (id == 10 && ft == T_STRING) r.str(a.key_off, a.key_len);
+        else if (id == 20 && ft == T_I64) a.ref = r.be64();
+        else used = false;
+        break;
+      case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:
+        if (id == 10 && ft == T_STRING) r.str(a.dom_off, a.dom_len); else used = false;
+        break;
+      case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
+      case CRR_EV_SIGNAL_EXTERNAL_INITIATED:
+        if (id == 20 && ft == T_STRING) r.str(a.dom_off, a.dom_len); else used = false;
+        break;
+      case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED:
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED:
+        if (id == 60 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:
+        if (id == 20 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
+      case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
+      case CRR_EV_SIGNAL_EXTERNAL_FAILED:
+        if (id == 50 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED:
+        if (id == 40 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:
+      case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:
+        if (id == 10 && ft == T_I64) a.ref = r.be64(); else used = false;
+        break;
+      default:
+        used = false;
+    }
+    if (!used) r.skip(ft);
+  }
+}
+
+// history_decode.cpp read_event: an attribute struct that arrives before the type is re-read after it
+__device__ void read_event(Rd& r, Event& e) {
+  e.id = e.ts = e.ver = e.task = 0;
+  e.type = 0;
+  attr_init(e.a);
+  u64 attr_at = 0;
+  bool have_attr_at = false;
+  int attr_t = -1;
+  bool have_type = false;
+  for (;;) {
+    const u32 ft = r.u8_();
+    if (r.err || ft == T_STOP) break;
+    const i32 id = r.be16();
+    if (r.err) return;
+    if (id == 10 && ft == T_I64) e.id = r.be64();
+    else if (id == 20 && ft == T_I64) e.ts = r.be64();
+    else if (id == 30 && ft == T_I32) { e.type = r.be32(); have_type = true; }
+    else if (id == 35 && ft == T_I64) e.ver = r.be64();
+    else if (id == 36 && ft == T_I64) e.task = r.be64();
+    else if (ft == T_STRUCT && attr_type_of_field(id) >= 0) {
+      const int at = attr_type_of_field(id);
+      if (have_type && at == e.type) {
+        read_attributes(r, at, e.a);
+      } else {
+        if (!have_type) { attr_at = r.p; have_attr_at = true; attr_t = at; }
+        r.skip(ft);
+      }
+    } else {
+      r.skip(ft);
+    }
+  }
+  if (r.err) return;
+  if (have_attr_at && attr_t == e.type) {
+    Rd r2;
+    r2.init(r.b, attr_at, r.end);
+    read_attributes(r2, attr_t, e.a);
+    if (r2.err) r.err = r2.err;
+  }
+}
+
+__device__ __forceinline__ bool keyed_type(i32 t) {
+  return t == CRR_EV_DECISION_TASK_COMPLETED || t == CRR_EV_ACTIVITY_TASK_SCHEDULED ||
+         t == CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED || t == CRR_EV_TIMER_STARTED || t == CRR_EV_TIMER_FIRED ||
+         t == CRR_EV_TIMER_CANCELED;
+}
+
+__device__ __forceinline__ u32 fnv1a(const u8* b, u64 off, u32 len) {
+  u32 h = 2166136261u;
+  for (u32 i = 0; i < len; ++i) h = (h ^ b[off + i]) * 16777619u;
+  return h;
+}
+
+// ---- domain-cache stand-in: the known domain names as an open-addressed set -----------------------------
+__device__ __forceinline__ bool bytes_equal(const u8* a, u64 ao, const u8* b, u64 bo, u32 n) {
+  for (u32 i = 0; i < n; ++i)
+    if (a[ao + i] != b[bo + i]) return false;
+  return true;
+}
+
+__global__ void domains_build_kernel(crr_blob_batch in, u32* table, u32 cap) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= in.n_domains) return;
+  u32 h = fnv1a(in.strings, in.domain_off[i], in.domain_len[i]) & (cap - 1);
+  for (u32 probe = 0; probe < cap; ++probe) {
+    const u32 prev = atomicCAS(table + h, 0u, i + 1);
+    if (prev == 0) return;
+    h = (h + 1) & (cap - 1);
+  }
+}
+
+// WfFlattener::domain_status
+__device__ __forceinline__ i32 domain_status(const crr_blob_batch& in, const u32* table, u32 cap, u64 off, u32 len) {
+  if (len == 0) return CRR_DOMAIN_NOT_SET;
+  if (in.n_domains == 0xFFFFFFFFu) return CRR_DOMAIN_RESOLVED;
+  if (cap == 0) return CRR_DOMAIN_UNKNOWN;
+  u32 h = fnv1a(in.bytes, off, len) & (cap - 1);
+  for (u32 probe = 0; probe < cap; ++probe) {
+    const u32 e = table[h];
+    if (e == 0) return CRR_DOMAIN_UNKNOWN;
+    const u32 d = e - 1;
+    if (in.domain_len[d] == len && bytes_equal(in.bytes, off, in.strings, in.domain_off[d], len)) return CRR_DOMAIN_RESOLVED;
+    h = (h + 1) & (cap - 1);
+  }
+  return CRR_DOMAIN_UNKNOWN;
+}
+
+// every blob decoded and the canonical scratch large enough: the later passes may read it
+__device__ __forceinline__ bool plan_ok(const Plan& P) {
+  const u64 NB = (u64)P.n_blobs + 1;
+  return *P.err == ~0ull && P.off[0 * NB + P.n_blobs] <= P.max_events && P.off[3 * NB + P.n_blobs] <= 2 * P.max_events;
+}
+
+// ---- 1: blob -> workflow ---------------------------------------------------------------------------------
+__global__ void blob_wf_kernel(crr_blob_batch in, u32* blob_wf, u64* err) {
+  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= in.n_wf) return;
+  const crr_blob_wf s = in.wf[w];
+  for (u32 b = 0; b < s.blob_count && s.blob_begin + b < in.n_blobs; ++b) blob_wf[s.blob_begin + b] = w;
+  // the consecutive-ranges contract (cadence_ingest.h); a violation fails the plan
+  const u32 expect = w == 0 ? 0u : in.wf[w - 1].blob_begin + in.wf[w - 1].blob_count;
+  if (s.blob_begin != expect || (w + 1 == in.n_wf && s.blob_begin + s.blob_count != in.n_blobs))
+    atomicMin((unsigned long long*)err, ((u64)0 << 8) | (u64)(-CRR_DECODE_BAD_ARGUMENT));
+}
+
+__device__ __forceinline__ void record_error(u64* err, u32 blob, int code) {
+  atomicMin((unsigned long long*)err, ((u64)blob << 8) | (u64)(-code));
+}
+
+// ---- 2 / 4: the thrift walk over one blob ---------------------------------------------------------------
+// WRITE = false: counts only (events, activity side, start side, key strings); true: writes the
+// canonical columns at the blob's prefixes.
+template <bool WRITE>
+__device__ void walk_blob(const crr_blob_batch& in, const Plan& P, u32 bi, u32 cnt[kCnt]) {
+  cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
+  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
+  if (b1 <= b0) return;   // an empty blob: an empty batch
+  Rd r;
+  r.init(in.bytes, b0, b1);
+  if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
+  u64 ev_at = 0, act_at = 0, st_at = 0, key_at = 0;
+  i32 new_run = -1;
+  if (WRITE) {
+    ev_at = P.off[0 * (P.n_blobs + 1) + bi];
+    act_at = P.off[1 * (P.n_blobs + 1) + bi];
+    st_at = P.off[2 * (P.n_blobs + 1) + bi];
+    key_at = P.off[3 * (P.n_blobs + 1) + bi];
+    new_run = in.wf[P.blob_wf[bi]].new_run_wf;
+  }
+  const u64 ev_first = ev_at;
+  Event e;
+  for (;;) {
+    const u32 ft = r.u8_();
+    if (r.err || ft == T_STOP) break;
+    const i32 id = r.be16();
+    if (r.err) break;
+    if (id != 10 || ft != T_LIST) { r.skip(ft); continue; }
+    const u32 et = r.u8_();
+    const i32 n = r.be32();
+    if (r.err) break;
+    if (n < 0) { r.err = CRR_DECODE_TRUNCATED; break; }
+    if (et != T_STRUCT && n > 0) { r.err = CRR_DECODE_BAD_TYPE; break; }
+    for (i32 i = 0; i < n; ++i) {
+      read_event(r, e);
+      if (r.err) break;
+      const i32 t = e.type;
+      const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
+      const Attr& a = e.a;
+      if (WRITE) {
+        const u64 x = ev_at;
+        P.etype[x] = (u8)(valid ? t : CRR_EV_PAD - 1);
+        P.id[x] = e.id; P.ver[x] = e.ver; P.ts[x] = e.ts; P.task[x] = e.task;
+        i64 ref = 0;
+        i32 aux = 0;
+        switch (valid ? t : -1) {
+          case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
+            crr_start_side ss;
+            ss.decision_start_to_close = a.task_s2c;
+            ss.workflow_timeout = a.exec_s2c;
+            ss.first_decision_backoff = a.backoff;
+            ss.initiator = a.initiator;
+            ss.parent_domain_status = domain_status(in, P.dom_table, P.dom_cap, a.dom_off, a.dom_len);
+            ss.attempt = a.attempt;
+            ss.expiration_ns = a.expiration_ts;
+            ss.reserved = 0;
+            if (a.prev_mode == 0) {
+              ss.prev_reset_key_off = 0;   // the global reset_keys index, set below
+              ss.prev_reset_count = a.prev_n;
+            } else {
+              ss.prev_reset_key_off = 0;
+              ss.prev_reset_count = a.prev_mode;
+            }
+            aux = (i32)st_at;          // canonical start-side index (remapped by the layout)
+            if (a.prev_mode == 0) {
+              // the final Points list's strings, in order, as reset-key entries (key_of at add time); the
+              // record holds its first entry's index until fix_start_side_kernel makes it a reset_keys index
+              ss.prev_reset_key_off = (u32)key_at;
+              Rd r2;
+              r2.init(in.bytes, a.prev_pos, r.end);
+              for (i32 k = 0; k < a.prev_n; ++k) {
+                u64 so = 0; u32 sl = 0;
+                if (a.prev_et != T_STRUCT) {
+                  r2.skip(a.prev_et);
+                } else {
+                  for (;;) {
+                    const u32 t2 = r2.u8_();
+                    if (r2.err || t2 == T_STOP) break;
+                    const i32 id2 = r2.be16();
+                    if (id2 == 10 && t2 == T_STRING) r2.str(so, sl);   // the last BinaryChecksum wins
+                    else r2.skip(t2);
+                  }
+                }
+                KeyRef kr;
+                kr.off = so; kr.len = sl; kr.is_reset = 1; kr.dst = 0;
+                P.keys[key_at++] = kr;
+              }
+            }
+            P.start[st_at++] = ss;
+            break;
+          }
+          case CRR_EV_DECISION_TASK_SCHEDULED: ref = a.ref; aux = a.aux; break;
+          case CRR_EV_DECISION_TASK_STARTED: ref = a.ref; break;
+          case CRR_EV_DECISION_TASK_COMPLETED: ref = a.ref; break;
+          case CRR_EV_DECISION_TASK_TIMED_OUT: aux = a.aux; break;
+          case CRR_EV_ACTIVITY_TASK_SCHEDULED: {
+            crr_activity_side as;
+            as.schedule_to_start = a.s2s; as.schedule_to_close = a.s2c; as.start_to_close = a.st2c;
+            as.heartbeat = a.hb; as.has_retry_policy = a.has_retry; as.expiration_interval = a.expiration;
+            as.domain_status = domain_status(in, P.dom_table, P.dom_cap, a.dom_off, a.dom_len);
+            as.reserved = 0;
+            aux = (i32)act_at;         // canonical activity-side index (remapped by the layout)
+            P.act[act_at++] = as;
+            break;
+          }
+          case CRR_EV_ACTIVITY_TASK_STARTED: case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED:
+          case CRR_EV_ACTIVITY_TASK_TIMED_OUT: case CRR_EV_ACTIVITY_TASK_CANCELED:
+            ref = a.ref; break;
+          case CRR_EV_TIMER_STARTED: ref = a.ref; break;
+          case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:
+          case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
+          case CRR_EV_SIGNAL_EXTERNAL_INITIATED:
+            aux = domain_status(in, P.dom_table, P.dom_cap, a.dom_off, a.dom_len);
+            break;
+          case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED:
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED: case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
+          case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED: case CRR_EV_SIGNAL_EXTERNAL_FAILED:
+          case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:
+            ref = a.ref; break;
+          case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: aux = new_run; break;
+          default: break;
+        }
+        if (valid && keyed_type(t)) {
+          KeyRef kr;
+          kr.off = a.key_off; kr.len = a.key_len; kr.is_reset = 0; kr.dst = x;
+          P.keys[key_at++] = kr;
+        }
+        P.ref[x] = ref;
+        P.key[x] = 0;
+        P.aux[x] = aux;
+        ++ev_at;
+      } else {
+        ++cnt[0];
+        if (valid && t == CRR_EV_ACTIVITY_TASK_SCHEDULED) ++cnt[1];
+        if (valid && t == CRR_EV_WORKFLOW_EXECUTION_STARTED) {
+          ++cnt[2];
+          if (a.prev_mode == 0) cnt[3] += (u32)a.prev_n;
+        }
+        if (valid && keyed_type(t)) ++cnt[3];
+      }
+    }
+    if (r.err) break;
+  }
+  if (r.err) { record_error(P.err, bi, r.err); return; }
+  if (WRITE && ev_at > ev_first) {   // batch boundaries
+    P.etype[ev_first] |= CRR_ETYPE_BATCH_FIRST;
+    P.etype[ev_at - 1] |= CRR_ETYPE_BATCH_LAST;
+  }
+}
+
+__global__ void blob_count_kernel(crr_blob_batch in, Plan P) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs) return;
+  u32 c[kCnt];
+  walk_blob<false>(in, P, bi, c);
+  for (int k = 0; k < kCnt; ++k) P.cnt[k * P.n_blobs + bi] = c[k];
+}
+
+__global__ void blob_decode_kernel(crr_blob_batch in, Plan P) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs) return;
+  const u64 NB = P.n_blobs + 1;
+  if (P.off[0 * NB + P.n_blobs] > P.max_events || P.off[3 * NB + P.n_blobs] > 2 * P.max_events || *P.err != ~0ull)
+    return;   // the summary reports it (error, or scratch too small)
+  u32 c[kCnt];
+  walk_blob<true>(in, P, bi, c);
+}
+
+// ---- 3: exclusive prefixes over K arrays of m u32 / u64 values (reduce, scan the tile sums, apply) --------
+constexpr int kTile = 1024;
+template <class T>
+__global__ void scan_tiles_kernel(const T* in, u64 in_stride, u32 m, int K, u64* tile_sums, u32 n_tiles) {
+  __shared__ u64 part[kBlock];
+  const u32 tile = blockIdx.x, k = blockIdx.y;
+  u64 s = 0;
+  for (u32 i = threadIdx.x; i < kTile; i += kBlock) {
+    const u64 j = (u64)tile * kTile + i;
+    if (j < m) s += (u64)in[k * in_stride + j];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = kBlock / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tile_sums[(u64)k * n_tiles + tile] = part[0];
+}
+// one block per array: exclusive scan of its tile sums (serial in chunks of kBlock)
+__global__ void scan_tile_sums_kernel(u64* tile_sums, u32 n_tiles) {
+  __shared__ u64 buf[kBlock];
+  __shared__ u64 carry;
+  const u32 k = blockIdx.x;
+  u64* ts = tile_sums + (u64)k * n_tiles;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (u32 base = 0; base < n_tiles; base += kBlock) {
+    const u32 i = base + threadIdx.x;
+    const u64 v = i < n_tiles ? ts[i] : 0;
+    buf[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < kBlock; o <<= 1) {   // inclusive Hillis-Steele
+      const u64 add = (int)threadIdx.x >= o ? buf[threadIdx.x - o] : 0;
+      __syncthreads();
+      buf[threadIdx.x] += add;
+      __syncthreads();
+    }
+    const u64 c = carry;
+    if (i < n_tiles) ts[i] = c + buf[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry = c + buf[kBlock - 1];
+    __syncthreads();
+  }
+}
+// out[k][j] = exclusive prefix of in[k][0..j), j <= m (out has m + 1 entries per array)
+template <class T>
+__global__ void scan_apply_kernel(const T* in, u64 in_stride, u32 m, const u64* tile_sums, u32 n_tiles, u64* out,
+                                  u64 out_stride) {
+  __shared__ u64 buf[kTile];
+  const u32 tile = blockIdx.x, k = blockIdx.y;
+  for (u32 i = threadIdx.x; i < kTile; i += kBlock) {
+    const u64 j = (u64)tile * kTile + i;
+    buf[i] = j < m ? (u64)in[k * in_stride + j] : 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {   // serial over the tile: 1024 adds, cheap next to the walks
+    u64 s = tile_sums[(u64)k * n_tiles + tile];
+    for (int i = 0; i < kTile; ++i) {
+      const u64 v = buf[i];
+      buf[i] = s;
+      s += v;
+    }
+    const u64 j_end = (u64)tile * kTile + kTile;
+    if (j_end >= m && (u64)tile * kTile <= m) out[k * out_stride + m] = s;  // the total
+  }
+  __syncthreads();
+  for (u32 i = threadIdx.x; i < kTile; i += kBlock) {
+    const u64 j = (u64)tile * kTile + i;
+    if (j < m) out[k * out_stride + j] = buf[i];
+  }
+}
+
+template <class T>
+void multi_scan(const T* in, u64 in_stride, u32 m, int K, u64* tile_sums, u64* out, u64 out_stride, hipStream_t s) {
+  const u32 n_tiles = (m + kTile - 1) / kTile;
+  const u32 nt = n_tiles ? n_tiles : 1;
+  hipLaunchKernelGGL(scan_tiles_kernel<T>, dim3(nt, K), dim3(kBlock), 0, s, in, in_stride, m, K, tile_sums, nt);
+  hipLaunchKernelGGL(scan_tile_sums_kernel, dim3(K), dim3(kBlock), 0, s, tile_sums, nt);
+  hipLaunchKernelGGL(scan_apply_kernel<T>, dim3(nt, K), dim3(kBlock), 0, s, in, in_stride, m, tile_sums, nt, out,
+                     out_stride);
+}
+
+// ---- 5: per workflow: interning, capacities, bounds, tier, sort key --------------------------------------
+// The workflow's table region: a power of two >= 2 * its entries (events, plus key strings), from a
+// per-workflow prefix (no collisions across workflows).
+__device__ __forceinline__ u32 pow2_at_least(u32 x) {
+  u32 c = 16;
+  while (c < x) c <<= 1;
+  return c;
+}
+
+// 64-bit table entries.  Interning: (hash32 << 32) | (entry index + 1), the key id kept in a parallel
+// word.  Bounds: (map << 40 | low 40 bits of the ID or key) + 1 in the low 43 bits, flag bits above.
+constexpr u64 kInserted = 1ull << 62, kDeleteSeen = 1ull << 61;
+constexpr u64 kMask40 = (1ull << 40) - 1;
+
+__global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
+  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= in.n_wf || !plan_ok(P)) return;
+  const crr_blob_wf src = in.wf[w];
+  const u32 bb = src.blob_begin, be = src.blob_begin + src.blob_count;
+  const u64 NB = P.n_blobs + 1;
+  const u64 e0 = P.off[0 * NB + bb], e1 = P.off[0 * NB + be];
+  const u64 k0 = P.off[3 * NB + bb], k1 = P.off[3 * NB + be];
+  const u32 n = (u32)(e1 - e0);
+  const u32 nk = (u32)(k1 - k0);
+  // this workflow's scratch table: [tbase, tbase + cap) u64 words (+ cap u32 key ids after the bounds use)
+  const u64 tbase = 4 * e0 + 4 * k0 + 64ull * w;
+  u64* tab = P.table + tbase;
+  const u32 cap_i = pow2_at_least(2 * nk + 2);
+
+  // -- interning (WfFlattener::key_of: "" is key 0, new strings get 1, 2, ... in first-seen order) --
+  {
+    for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
+    u32 next = 1;
+    for (u64 j = k0; j < k1; ++j) {
+      const KeyRef kr = P.keys[j];
+      u32 id = 0;
+      if (kr.len > 0) {
+        const u32 h = fnv1a(in.bytes, kr.off, kr.len);
+        u32 slot = h & (cap_i - 1);
+        for (;;) {
+          const u64 ent = tab[slot];
+          if (ent == 0) {                       // a new string: the next id
+            id = next++;
+            tab[slot] = ((u64)h << 32) | (u64)(j - k0 + 1);
+            break;
+          }
+          if ((u32)(ent >> 32) == h) {          // same hash: compare the bytes
+            const u64 jo = k0 + (u32)ent - 1;
+            const KeyRef other = P.keys[jo];
+            if (other.len == kr.len && bytes_equal(in.bytes, kr.off, in.bytes, other.off, kr.len)) {
+              id = P.entry_id[jo];
+              break;
+            }
+          }
+          slot = (slot + 1) & (cap_i - 1);
+        }
+      }
+      P.entry_id[j] = id;
+      if (kr.is_reset == 0) P.key[kr.dst] = id;
+    }
+  }
+
+  // -- capacities, VH items, tasks (WfFlattener::add / batch_end / finish) --
+  i32 n_act = 0, n_timer = 0, n_child = 0, n_rc = 0, n_sig = 0, n_dtc = 0, n_started = 0, vh = 0, tasks = 0;
+  i32 max_prev = 0;
+  i32 empty_at = -1;
+  {
+    bool have_ver = false;
+    i64 last_ver = 0;
+    u64 x = e0;
+    for (u32 b = bb; b < be; ++b) {
+      const u64 be_ = P.off[0 * NB + b + 1];
+      if (be_ == x) {   // an empty batch
+        if (empty_at < 0) empty_at = (i32)(x - e0);
+        continue;
+      }
+      tasks += 2;
+      for (; x < be_; ++x) {
+        const u32 t = P.etype[x] & CRR_ETYPE_MASK;
+        const i64 v = P.ver[x];
+        if (!have_ver || v > last_ver) { ++vh; last_ver = v; have_ver = true; }
+        if (t < CRR_EV_TYPE_COUNT) tasks += kTasksPerEvent[t];
+        switch (t) {
+          case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
+            ++n_started;
+            const i32 pc = P.start[P.aux[x]].prev_reset_count;
+            if (pc > max_prev) max_prev = pc;
+            break;
+          }
+          case CRR_EV_DECISION_TASK_COMPLETED: ++n_dtc; break;
+          case CRR_EV_ACTIVITY_TASK_SCHEDULED: ++n_act; break;
+          case CRR_EV_TIMER_STARTED: ++n_timer; break;
+          case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: ++n_child; break;
+          case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED: ++n_rc; break;
+          case CRR_EV_SIGNAL_EXTERNAL_INITIATED: ++n_sig; break;
+          default: break;
+        }
+      }
+    }
+    if (src.blob_count == 0) empty_at = 0;
+  }
+  const i32 rp_cap = max_prev * (n_started > 1 ? n_started : 1) + n_dtc;
+
+  // -- live-set bounds (flatten.live_set_bounds): inserts +1, deletes of inserted IDs (first delete of an
+  // ID, ref < event ID) / inserted timer keys -1; the running maximum --
+  i32 bound[kMaps] = {0, 0, 0, 0, 0, 0};
+  bool compact_ok = n <= (u32)kCompactMaxEvents;
+  {
+    const u32 cap_b = pow2_at_least(2 * n + 2);
+    for (u32 i = 0; i < cap_b; ++i) tab[i] = 0;
+    auto map_of = [](u32 t, int& dir) -> int {
+      dir = 0;
+      switch (t) {
+        case CRR_EV_ACTIVITY_TASK_SCHEDULED: dir = 1; return 0;
+        case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED: case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
+        case CRR_EV_ACTIVITY_TASK_CANCELED: dir = -1; return 0;
+        case CRR_EV_TIMER_STARTED: dir = 1; return 1;
+        case CRR_EV_TIMER_FIRED: case CRR_EV_TIMER_CANCELED: dir = -1; return 1;
+        case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: dir = 1; return 2;
+        case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
+        case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
+        case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT: case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED:
+          dir = -1; return 2;
+        case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED: dir = 1; return 3;
+        case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:
+          dir = -1; return 3;
+        case CRR_EV_SIGNAL_EXTERNAL_INITIATED: dir = 1; return 4;
+        case CRR_EV_SIGNAL_EXTERNAL_FAILED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED: dir = -1; return 4;
+        default: return -1;
+      }
+    };
+    auto entry_key = [](int m, u64 v) -> u64 { return (((u64)m << 40) | (v & kMask40)) + 1; };
+    auto find = [&](u64 k, bool create) -> u64* {
+      u32 h = (u32)((k * 0x9E3779B97F4A7C15ull) >> 32) & (cap_b - 1);
+      for (;;) {
+        const u64 ent = tab[h];
+        if ((ent & ((1ull << 43) - 1)) == k) return tab + h;
+        if (ent == 0) {
+          if (!create) return nullptr;
+          tab[h] = k;
+          return tab + h;
+        }
+        h = (h + 1) & (cap_b - 1);
+      }
+    };
+    // inserts (np.isin is over every insert of the workflow, before or after the delete)
+    for (u64 x = e0; x < e1; ++x) {
+      const u32 t = P.etype[x] & CRR_ETYPE_MASK;
+      if (P.id[x] > (i64)0xFFFFFFFFll) compact_ok = false;
+      int dir;
+      const int m = map_of(t, dir);
+      if (m < 0 || dir <= 0) continue;
+      const u64 v = m == 1 ? (u64)P.key[x] : (u64)P.id[x];
+      *find(entry_key(m, v), true) |= kInserted;
+    }
+    i32 run[5] = {0, 0, 0, 0, 0};
+    for (u64 x = e0; x < e1; ++x) {
+      const u32 t = P.etype[x] & CRR_ETYPE_MASK;
+      int dir;
+      const int m = map_of(t, dir);
+      if (m < 0) continue;
+      if (dir < 0) {
+        bool valid;
+        if (m == 1) {
+          u64* ent = find(entry_key(1, (u64)P.key[x]), false);
+          valid = ent && (*ent & kInserted);
+        } else {
+          u64* ent = find(entry_key(m, (u64)P.ref[x]), true);   // created to carry the first-delete mark
+          const bool first = !(*ent & kDeleteSeen);
+          *ent |= kDeleteSeen;
+          valid = (*ent & kInserted) && P.ref[x] < P.id[x] && first;
+        }
+        if (!valid) continue;
+      }
+      run[m] += dir;
+      if (run[m] > bound[m]) bound[m] = run[m];
+    }
+    // reset points: distinct non-empty binary checksums + the most points a start event carries over
+    // (the distinct count: a DecisionTaskCompleted key not seen before in this workflow)
+    i32 rp = 0;
+    for (u64 x = e0; x < e1; ++x) {
+      if ((P.etype[x] & CRR_ETYPE_MASK) != CRR_EV_DECISION_TASK_COMPLETED || P.key[x] == 0) continue;
+      u64* ent = find(entry_key(5, (u64)P.key[x]), true);
+      if (!(*ent & kInserted)) { *ent |= kInserted; ++rp; }
+    }
+    bound[5] = rp + (max_prev > 0 ? max_prev : 0);
+  }
+  // tier_classes
+  int tier = kWide;
+  for (int k = kWide - 1; k >= 0; --k) {
+    bool fit = true;
+    for (int m = 0; m < kMaps; ++m) fit = fit && bound[m] <= kTierSlots[k][m];
+    if (k >= 2) fit = fit && compact_ok;
+    if (fit) tier = k;
+  }
+  if (tier == 1 && compact_ok) tier = 2;
+  const bool is_long = (i32)n > kLongHistory || tier == kWide;
+  bool big = false;
+  for (int m = 0; m < kMaps; ++m) big = big || bound[m] > kWaveBigCap;
+  if (is_long && !big) {
+    bool small = true;
+    for (int m = 0; m < kMaps; ++m) small = small && bound[m] <= kWaveSmallTier[m];
+    if (!small) atomicAdd(P.counters + C_SMALL_TAIL_BAD, 1u);
+  }
+  if (is_long) { if (big) atomicAdd(P.counters + C_N_BIG, 1u); }
+  else { atomicAdd(P.counters + C_N_LANE, 1u); atomicAdd(P.counters + C_TIER0 + tier, 1u); }
+  if (src.flags & CRR_WF_FLAG_NEW_RUN) atomicAdd(P.counters + C_NEW_RUN, 1u);
+
+  i32* wi = P.wf_info;
+  const u64 nw = in.n_wf;
+  wi[WI_COUNT * nw + w] = (i32)n; wi[WI_EMPTY_AT * nw + w] = empty_at;
+  wi[WI_ACT * nw + w] = n_act; wi[WI_TIMER * nw + w] = n_timer; wi[WI_CHILD * nw + w] = n_child;
+  wi[WI_RC * nw + w] = n_rc; wi[WI_SIG * nw + w] = n_sig; wi[WI_VH * nw + w] = vh; wi[WI_RP * nw + w] = rp_cap;
+  wi[WI_TASKS * nw + w] = tasks; wi[WI_STARTED * nw + w] = n_started; wi[WI_TIER * nw + w] = tier;
+  wi[WI_LONG * nw + w] = is_long; wi[WI_BIG * nw + w] = big;
+  // device order (flatten.interleave): lanes by (tier, -length, index), then the long tail by (big, -length, index)
+  const u64 cls = is_long ? (u64)big : (u64)tier;
+  const u64 len = n < 0x1FFFFFFFu ? n : 0x1FFFFFFFu;
+  P.sort_in[w] = ((u64)is_long << 63) | (cls << 60) | ((0x1FFFFFFFull - len) << 31) | (u64)w;
+  // the branch tokens' bytes (NewHistoryBranchTokenByBranchID) + the final token
+  P.arena_off[w] = 24ull + src.run_id_len + src.branch_id_len + (src.final_token_len != 0xFFFFFFFFu ? src.final_token_len : 0);
+}
+
+// ---- 7: geometry -------------------------------------------------------------------------------------------
+__global__ void positions_kernel(Plan P, u32 n_lane) {
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.n_wf) return;
+  const u32 w = (u32)(P.sort_out[p] & 0x7FFFFFFFull);
+  P.perm[p] = w;
+  P.inv[w] = p;
+  const i32* wi = P.wf_info;
+  const u64 nw = P.n_wf;
+  u64 v[kGeo];
+  v[GV_LEN] = (u64)wi[WI_COUNT * nw + w];
+  const int caps[8] = {WI_ACT, WI_TIMER, WI_CHILD, WI_RC, WI_SIG, WI_VH, WI_RP, WI_TASKS};
+  for (int t = 0; t < 8; ++t) {
+    const i32 c = wi[caps[t] * nw + w];
+    v[GV_CAP0 + t] = c > 0 ? (u64)c : 0;
+  }
+  v[GV_ACT_SIDE] = (u64)wi[WI_ACT * nw + w];
+  v[GV_START_SIDE] = (u64)wi[WI_STARTED * nw + w];
+  if (p >= n_lane) {
+    for (int k = 0; k < kGeo; ++k) P.tvals[(u64)k * nw + (p - n_lane)] = v[k];
+  }
+}
+
+// one wavefront per group: the maxima of its 64 lanes (padding lanes count 0)
+__global__ void group_max_kernel(Plan P, u32 n_lane, u32 n_groups) {
+  const u32 g = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  if (g >= n_groups) return;
+  const u32 lane = threadIdx.x & 63;
+  const u32 p = g * 64 + lane;
+  const i32* wi = P.wf_info;
+  const u64 nw = P.n_wf;
+  const int src[kGeo] = {WI_COUNT, WI_ACT, WI_TIMER, WI_CHILD, WI_RC, WI_SIG, WI_VH, WI_RP, WI_TASKS, WI_ACT, WI_STARTED};
+  for (int k = 0; k < kGeo; ++k) {
+    i32 v = 0;
+    if (p < n_lane) {
+      v = wi[src[k] * nw + P.perm[p]];
+      if (v < 0) v = 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const i32 x = __shfl_xor(v, o, 64);
+      v = x > v ? x : v;
+    }
+    if (lane == 0) P.gvals[(u64)k * n_groups + g] = (u64)v * 64;
+  }
+}
+
+__global__ void summary_kernel(Plan P, u32 n_lane, u32 n_groups, u32 n_tail, crr_ingest_summary* S) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const u64 NB = P.n_blobs + 1;
+  S->err = 0;
+  S->reserved0 = 0;
+  S->err_blob = -1;
+  const u64 e = *P.err;
+  if (e != ~0ull) {
+    S->err = -(i32)(e & 0xff);
+    S->err_blob = (i64)(e >> 8);
+  }
+  S->n_events = P.off[0 * NB + P.n_blobs];
+  const u64 n_keys = P.off[3 * NB + P.n_blobs];
+  if (S->err == 0 && (S->n_events > P.max_events || n_keys > 2 * P.max_events)) S->err = kErrScratch;
+  S->n_wf = P.n_wf;
+  if (S->err) return;   // nothing past the decode is valid
+  auto gtot = [&](int k) { return P.gpre[(u64)k * (n_groups + 1) + n_groups]; };
+  auto ttot = [&](int k) { return P.tpre[(u64)k * (n_tail + 1) + n_tail]; };
+  S->n_slots = gtot(GV_LEN) + ttot(GV_LEN);
+  for (int t = 0; t < 8; ++t) S->table_rows[t] = gtot(GV_CAP0 + t) + ttot(GV_CAP0 + t);
+  const u64 n_act = P.off[1 * NB + P.n_blobs], n_start = P.off[2 * NB + P.n_blobs];
+  const u64 as = gtot(GV_ACT_SIDE) + ttot(GV_ACT_SIDE), ss = gtot(GV_START_SIDE) + ttot(GV_START_SIDE);
+  // _interleave_side keeps the canonical array when no event references it (the 1-record placeholder)
+  S->n_act_side = n_act ? (as > 0 ? as : 1) : 1;
+  S->n_start_side = n_start ? (ss > 0 ? ss : 1) : 1;
+  const u64 n_reset = P.reset_pos[2 * P.max_events];   // the exclusive prefix's total
+  S->n_reset_keys = n_reset ? n_reset : 1;               // flatten's [0] placeholder when there are none
+  S->arena_bytes = P.arena_off[P.n_wf];
+  S->n_wf = P.n_wf;
+  S->wave_begin = n_lane;
+  // segment boundaries on group boundaries, rounded down (flatten.interleave)
+  u32 c = 0, prev = 0;
+  for (int k = 0; k < kWide; ++k) {
+    c += P.counters[C_TIER0 + k];
+    u32 b = (c == n_lane) ? n_lane : (c / 64) * 64;
+    if (k > 0 && b < prev) b = prev;
+    S->tiers[k] = b;
+    prev = b;
+  }
+  S->tiers[5] = P.n_wf - P.counters[C_N_BIG];
+  S->has_new_run = P.counters[C_NEW_RUN] ? 1u : 0u;
+  S->lds_small_tail = P.counters[C_SMALL_TAIL_BAD] == 0 ? 1u : 0u;
+}
+
+// ---- layout -----------------------------------------------------------------------------------------------
+struct Dst {
+  crr_events ev;
+  crr_activity_side* act;
+  crr_start_side* start;
+  u32* reset_keys;
+  u8* arena;
+  crr_workflow* wf;
+};
+
+// one event (or pad) slot; side records follow their events (_interleave_side)
+__device__ __forceinline__ void put_slot(const crr_blob_batch& in, const Plan& P, const Dst& D, u64 dst, u32 p,
+                                         u32 w, i64 k, bool real, u64 side_act_base, u64 side_start_base, u64 side_stride,
+                                         u32 lane) {
+  u8* et = const_cast<u8*>(D.ev.etype);
+  i64* id = const_cast<i64*>(D.ev.event_id);
+  i64* ver = const_cast<i64*>(D.ev.version);
+  i64* ts = const_cast<i64*>(D.ev.timestamp);
+  i64* task = const_cast<i64*>(D.ev.task_id);
+  i64* ref = const_cast<i64*>(D.ev.ref);
+  u32* key = const_cast<u32*>(D.ev.key);
+  i32* aux = const_cast<i32*>(D.ev.aux);
+  if (!real) {
+    et[dst] = (u8)(CRR_EV_PAD | CRR_ETYPE_BATCH_FIRST | CRR_ETYPE_BATCH_LAST);
+    id[dst] = 0; ver[dst] = 0; ts[dst] = 0; task[dst] = 0; ref[dst] = 0; key[dst] = 0; aux[dst] = 0;
+    return;
+  }
+  const u64 NB = P.n_blobs + 1;
+  const u32 bb = in.wf[w].blob_begin;
+  const u64 x = P.off[0 * NB + bb] + (u64)k;
+  const u8 e = P.etype[x];
+  const u32 t = e & CRR_ETYPE_MASK;
+  i32 a = P.aux[x];
+  if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {
+    const u64 ord = (u64)a - P.off[1 * NB + bb];
+    const u64 ni = side_act_base + ord * side_stride + lane;
+    D.act[ni] = P.act[a];
+    a = (i32)ni;
+  } else if (t == CRR_EV_WORKFLOW_EXECUTION_STARTED) {
+    const u64 ord = (u64)a - P.off[2 * NB + bb];
+    const u64 ni = side_start_base + ord * side_stride + lane;
+    D.start[ni] = P.start[a];
+    a = (i32)ni;
+  } else if (t == CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW && a >= 0 && (u32)a < P.n_wf) {
+    a = (i32)P.inv[a];   // the new-run history's device position
+  }
+  et[dst] = e; id[dst] = P.id[x]; ver[dst] = P.ver[x]; ts[dst] = P.ts[x]; task[dst] = P.task[x];
+  ref[dst] = P.ref[x]; key[dst] = P.key[x]; aux[dst] = a;
+}
+
+__global__ void layout_groups_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u32 n_groups) {
+  const u32 g = blockIdx.x;
+  if (g >= n_groups) return;
+  const u64 glen = P.gvals[(u64)GV_LEN * n_groups + g] / 64;   // (still the maxima: prefixes live in gpre)
+  const u64 base = P.gpre[(u64)GV_LEN * (n_groups + 1) + g];
+  const u64 abase = P.gpre[(u64)GV_ACT_SIDE * (n_groups + 1) + g];
+  const u64 sbase = P.gpre[(u64)GV_START_SIDE * (n_groups + 1) + g];
+  const u32 lane = threadIdx.x & 63;
+  const u32 p = g * 64 + lane;
+  const bool have = p < n_lane;
+  const u32 w = have ? P.perm[p] : 0;
+  const i64 cnt = have ? P.wf_info[WI_COUNT * (u64)P.n_wf + w] : 0;
+  for (u64 k = threadIdx.x / 64; k < glen; k += blockDim.x / 64)
+    put_slot(in, P, D, base + k * 64 + lane, p, w, (i64)k, have && (i64)k < cnt, abase, sbase, 64, lane);
+}
+
+__global__ void layout_tail_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u32 n_groups, u32 n_tail) {
+  const u32 i = blockIdx.x;   // tail workflow
+  if (i >= n_tail) return;
+  const u32 p = n_lane + i;
+  const u32 w = P.perm[p];
+  const u64 lane_slots = P.gpre[(u64)GV_LEN * (n_groups + 1) + n_groups];
+  const u64 lane_act = P.gpre[(u64)GV_ACT_SIDE * (n_groups + 1) + n_groups];
+  const u64 lane_start = P.gpre[(u64)GV_START_SIDE * (n_groups + 1) + n_groups];
+  const u64 base = lane_slots + P.tpre[(u64)GV_LEN * (n_tail + 1) + i];
+  const u64 abase = lane_act + P.tpre[(u64)GV_ACT_SIDE * (n_tail + 1) + i];
+  const u64 sbase = lane_start + P.tpre[(u64)GV_START_SIDE * (n_tail + 1) + i];
+  const i64 cnt = P.wf_info[WI_COUNT * (u64)P.n_wf + w];
+  for (i64 k = threadIdx.x; k < cnt; k += blockDim.x) put_slot(in, P, D, base + k, p, w, k, true, abase, sbase, 1, 0);
+}
+
+// descriptors (device order) and branch tokens (canonical order)
+__global__ void layout_wf_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u32 n_groups, u32 n_tail) {
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.n_wf) return;
+  const u32 w = P.perm[p];
+  const crr_blob_wf s = in.wf[w];
+  const i32* wi = P.wf_info;
+  const u64 nw = P.n_wf;
+  crr_workflow d;
+  const bool lane_wf = p < n_lane;
+  const u32 g = p / 64, lane = p & 63, ti = p - n_lane;
+  auto pos = [&](int k) -> u64 {   // this workflow's base in geometry value k's space
+    if (lane_wf) return P.gpre[(u64)k * (n_groups + 1) + g] + lane;
+    return P.gpre[(u64)k * (n_groups + 1) + n_groups] + P.tpre[(u64)k * (n_tail + 1) + ti];
+  };
+  auto gcap = [&](int k, int wi_k) -> i32 {
+    if (lane_wf) return (i32)(P.gvals[(u64)k * n_groups + g] / 64);
+    const i32 c = wi[wi_k * nw + w];
+    return c > 0 ? c : 0;
+  };
+  d.ev_begin = (i64)pos(GV_LEN);
+  d.ev_count = wi[WI_COUNT * nw + w];
+  d.empty_batch_at = wi[WI_EMPTY_AT * nw + w];
+  d.init_version = s.init_version;
+  d.now_ns = s.now_ns;
+  const u64 ao = P.arena_off[w];
+  d.start_token_off = (u32)ao;
+  d.start_token_len = 24u + s.run_id_len + s.branch_id_len;
+  if (s.final_token_len != 0xFFFFFFFFu) {
+    d.final_token_off = (u32)(ao + d.start_token_len);
+    d.final_token_len = s.final_token_len;
+    d.rebuild_last_event_id = s.rebuild_last_event_id;
+    d.rebuild_last_event_version = s.rebuild_last_event_version;
+  } else {
+    d.final_token_off = 0;
+    d.final_token_len = 0xFFFFFFFFu;
+    d.rebuild_last_event_id = 0;
+    d.rebuild_last_event_version = 0;
+  }
+  d.act_base = (i64)pos(GV_CAP0 + 0); d.act_cap = gcap(GV_CAP0 + 0, WI_ACT);
+  d.timer_base = (i64)pos(GV_CAP0 + 1); d.timer_cap = gcap(GV_CAP0 + 1, WI_TIMER);
+  d.child_base = (i64)pos(GV_CAP0 + 2); d.child_cap = gcap(GV_CAP0 + 2, WI_CHILD);
+  d.rc_base = (i64)pos(GV_CAP0 + 3); d.rc_cap = gcap(GV_CAP0 + 3, WI_RC);
+  d.sig_base = (i64)pos(GV_CAP0 + 4); d.sig_cap = gcap(GV_CAP0 + 4, WI_SIG);
+  d.vh_base = (i64)pos(GV_CAP0 + 5); d.vh_cap = gcap(GV_CAP0 + 5, WI_VH);
+  d.rp_base = (i64)pos(GV_CAP0 + 6); d.rp_cap = gcap(GV_CAP0 + 6, WI_RP);
+  d.flags = s.flags;
+  d.task_base = (i64)pos(GV_CAP0 + 7); d.task_cap = gcap(GV_CAP0 + 7, WI_TASKS);
+  d.retention_days = s.retention_days;
+  D.wf[p] = d;
+  // branch token: 0x59 + HistoryBranch{10 TreeID, 20 BranchID, 30 Ancestors = []} (host_flatten.h branch_token)
+  u8* o = D.arena + ao;
+  u64 q = 0;
+  auto put = [&](u32 v) { o[q++] = (u8)v; };
+  auto be32 = [&](u32 v) { put(v >> 24); put(v >> 16); put(v >> 8); put(v); };
+  put(0x59);
+  put(11); put(0); put(10); be32(s.run_id_len);
+  for (u32 i = 0; i < s.run_id_len; ++i) put(in.strings[s.run_id_off + i]);
+  put(11); put(0); put(20); be32(s.branch_id_len);
+  for (u32 i = 0; i < s.branch_id_len; ++i) put(in.strings[s.branch_id_off + i]);
+  put(15); put(0); put(30); put(12); be32(0);
+  put(0);
+  if (s.final_token_len != 0xFFFFFFFFu)
+    for (u32 i = 0; i < s.final_token_len; ++i) put(in.strings[s.final_token_off + i]);
+}
+
+// the reset-point entries among the key entries (scan input), bounded by the device-side entry count
+__global__ void reset_flags_kernel(Plan P, u64 cap) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cap) return;
+  const u64 n_keys = plan_ok(P) ? P.off[3 * ((u64)P.n_blobs + 1) + P.n_blobs] : 0;
+  P.reset_flag[j] = j < n_keys ? P.keys[j].is_reset : 0u;
+}
+// start side records: prev_reset_key_off = the reset_keys index of the record's first point (for an
+// empty list, where the next point would go: host_flatten.h uses reset_keys.size())
+__global__ void fix_start_side_kernel(Plan P) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!plan_ok(P) || i >= P.off[2 * ((u64)P.n_blobs + 1) + P.n_blobs]) return;
+  crr_start_side& s = P.start[i];
+  if (s.prev_reset_count >= 0) s.prev_reset_key_off = (u32)P.reset_pos[s.prev_reset_key_off];
+}
+// reset_keys (canonical order): the interned ids of the reset-point entries, in entry order
+__global__ void layout_reset_keys_kernel(Plan P, u32* dst, u64 cap) {
+  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cap) return;
+  const u64 n_keys = P.off[3 * ((u64)P.n_blobs + 1) + P.n_blobs];
+  if (j < n_keys && P.keys[j].is_reset) dst[P.reset_pos[j]] = P.entry_id[j];
+}
+
+}  // namespace crr_ingest
+
+// ---- C ABI ----------------------------------------------------------------------------------------------------
+namespace {
+using namespace crr_ingest;
+
+struct Carved {
+  Plan P;
+  size_t bytes;
+  crr_ingest_summary* S_dev;
+};
+
+// The scratch layout for a max_events capacity; both calls carve it the same way from scratch_bytes.
+Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events) {
+  Carved c{};
+  const uintptr_t at = reinterpret_cast<uintptr_t>(scratch);
+  size_t used = 0;
+  auto take = [&](size_t bytes) -> void* {
+    void* p = reinterpret_cast<void*>(at + used);
+    used += align_up(bytes);
+    return p;
+  };
+  Plan& P = c.P;
+  P.n_blobs = n_blobs;
+  P.n_wf = n_wf;
+  P.max_events = max_events;
+  const u64 E = max_events ? max_events : 1;
+  const u64 NB = (u64)n_blobs + 1;
+  const u64 NW = n_wf ? n_wf : 1;
+  P.blob_wf = (u32*)take(4 * NB);
+  P.cnt = (u32*)take(4 * kCnt * NB);
+  P.off = (u64*)take(8 * kCnt * NB);
+  P.err = (u64*)take(8);
+  u64 max_m = 2 * E;
+  if (NB > max_m) max_m = NB;
+  if (NW + 1 > max_m) max_m = NW + 1;
+  P.tile = (u64*)take(8 * ((max_m + kTile - 1) / kTile + 1) * kGeo);
+  P.etype = (u8*)take(E);
+  P.id = (i64*)take(8 * E); P.ver = (i64*)take(8 * E); P.ts = (i64*)take(8 * E); P.task = (i64*)take(8 * E);
+  P.ref = (i64*)take(8 * E); P.key = (u32*)take(4 * E); P.aux = (i32*)take(4 * E);
+  P.act = (crr_activity_side*)take(sizeof(crr_activity_side) * E);
+  P.start = (crr_start_side*)take(sizeof(crr_start_side) * E);
+  P.keys = (KeyRef*)take(sizeof(KeyRef) * 2 * E);
+  P.entry_id = (u32*)take(4 * 2 * E);
+  P.reset_flag = (u32*)take(4 * 2 * E);
+  P.reset_pos = (u64*)take(8 * (2 * E + 1));
+  // per-workflow hash tables: a workflow of n events and k key entries uses <= 4n + 4k + 64 words
+  P.table = (u64*)take(8 * (4 * E + 4 * 2 * E + 64 * NW));
+  P.wf_info = (i32*)take(4 * kWfInfo * NW);
+  P.sort_in = (u64*)take(8 * NW);
+  P.sort_out = (u64*)take(8 * NW);
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (int)NW);
+  P.sort_tmp_bytes = tmp;
+  P.sort_tmp = take(tmp);
+  P.perm = (u32*)take(4 * NW);
+  P.inv = (u32*)take(4 * NW);
+  P.arena_off = (u64*)take(8 * (NW + 1));
+  const u64 NG = (NW + 63) / 64;
+  P.gvals = (u64*)take(8 * kGeo * NG);
+  P.tvals = (u64*)take(8 * kGeo * NW);
+  P.gpre = (u64*)take(8 * kGeo * (NG + 1));
+  P.tpre = (u64*)take(8 * kGeo * (NW + 1));
+  P.counters = (u32*)take(4 * 16);
+  c.S_dev = (crr_ingest_summary*)take(sizeof(crr_ingest_summary));
+  P.dom_table = (u32*)take(kDomainBytes);
+  P.dom_cap = 0;
+  c.bytes = used;
+  return c;
+}
+
+uint64_t max_events_of(size_t scratch_bytes, uint32_t n_blobs, uint32_t n_wf) {
+  // the largest capacity whose carve fits (the size is monotone in it)
+  uint64_t lo = 0, hi = 1;
+  while (carve(nullptr, n_blobs, n_wf, hi).bytes <= scratch_bytes && hi < (1ull << 40)) hi <<= 1;
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    if (carve(nullptr, n_blobs, n_wf, mid).bytes <= scratch_bytes) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+bool valid_batch(const crr_blob_batch* in) {
+  if (!in || !in->blob_off) return false;
+  if (in->n_wf && !in->wf) return false;
+  if (in->n_blobs && !in->bytes) return false;
+  if (reinterpret_cast<uintptr_t>(in->bytes) & 15) return false;   // the 16-byte window loads
+  if (in->n_domains != 0xFFFFFFFFu && in->n_domains && (!in->domain_off || !in->domain_len || !in->strings)) return false;
+  if (in->n_domains != 0xFFFFFFFFu && (size_t)in->n_domains * 2 * 4 > kDomainBytes) return false;
+  if ((in->n_wf || in->n_domains) && !in->strings && in->n_wf) return false;
+  if (in->n_wf >= 0x7FFFFFFFu) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t crr_ingest_scratch_bytes(uint32_t n_blobs, uint32_t n_wf, uint64_t max_events) {
+  return carve(nullptr, n_blobs, n_wf, max_events).bytes;
+}
+
+int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, crr_ingest_summary* summary,
+                    void* stream) {
+  if (!valid_batch(in) || !scratch || !summary) return -1;
+  if (in->n_wf == 0 && in->n_blobs > 0) return -1;   // blobs no workflow owns
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf);
+  if (max_events == 0) return -1;
+  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events);
+  Plan P = c.P;
+  const u32 nb = in->n_blobs, nw = in->n_wf;
+  const u64 NB = (u64)nb + 1;
+  const u64 E2 = 2 * max_events;
+  u32 dom_cap = 0;
+  if (in->n_domains != 0xFFFFFFFFu && in->n_domains) {
+    dom_cap = 16;
+    while (dom_cap < 2 * in->n_domains) dom_cap <<= 1;
+  }
+  P.dom_cap = dom_cap;
+  hipError_t e;
+  if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(P.counters, 0, 4 * 16, s)) != hipSuccess) return (int)e;
+  if (dom_cap) {
+    if ((e = hipMemsetAsync(P.dom_table, 0, 4 * (size_t)dom_cap, s)) != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(domains_build_kernel, dim3((in->n_domains + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in,
+                       P.dom_table, dom_cap);
+  }
+  // A: decode, per-workflow pass, device order, reset-key positions
+  if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
+  if (nb) hipLaunchKernelGGL(blob_count_kernel, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
+  multi_scan<u32>(P.cnt, nb, nb, kCnt, P.tile, P.off, NB, s);
+  if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
+  hipLaunchKernelGGL(reset_flags_kernel, dim3((unsigned)((E2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P, E2);
+  multi_scan<u32>(P.reset_flag, E2, (u32)E2, 1, P.tile, P.reset_pos, E2 + 1, s);
+  hipLaunchKernelGGL(fix_start_side_kernel, dim3((unsigned)((max_events + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P);
+  if (nw) hipLaunchKernelGGL(wf_pass_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
+  multi_scan<u64>(P.arena_off, nw, nw, 1, P.tile, P.arena_off, (u64)nw + 1, s);
+  if (nw) {
+    size_t tmp = P.sort_tmp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortKeys(P.sort_tmp, tmp, P.sort_in, P.sort_out, (int)nw, 0, 64, s)) != hipSuccess)
+      return (int)e;
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  // the lane / tail split sizes the geometry launches
+  u32 n_lane = 0;
+  u64 err = 0;
+  if ((e = hipMemcpyAsync(&n_lane, P.counters + C_N_LANE, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemcpyAsync(&err, P.err, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+  const bool failed = err != ~0ull || n_lane > nw;
+  const u32 n_groups = failed ? 0 : (n_lane + 63) / 64, n_tail = failed ? 0 : nw - n_lane;
+  // B: geometry and the summary (after a failed decode only the error and the counts)
+  if (nw && !failed) hipLaunchKernelGGL(positions_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, P, n_lane);
+  if (n_groups) hipLaunchKernelGGL(group_max_kernel, dim3((n_groups + 3) / 4), dim3(256), 0, s, P, n_lane, n_groups);
+  if (!failed) {
+    multi_scan<u64>(P.gvals, n_groups, n_groups, kGeo, P.tile, P.gpre, (u64)n_groups + 1, s);
+    multi_scan<u64>(P.tvals, nw, n_tail, kGeo, P.tile, P.tpre, (u64)n_tail + 1, s);
+  }
+  hipLaunchKernelGGL(summary_kernel, dim3(1), dim3(64), 0, s, P, n_lane, n_groups, n_tail, c.S_dev);
+  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+  if ((e = hipMemcpyAsync(summary, c.S_dev, sizeof(crr_ingest_summary), hipMemcpyDeviceToHost, s)) != hipSuccess)
+    return (int)e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+  return 0;
+}
+
+int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, const crr_ingest_summary* S,
+                      const crr_inputs* dst, uint32_t* perm, void* stream) {
+  if (!valid_batch(in) || !scratch || !S || !dst || S->err || S->n_wf != in->n_wf) return -1;
+  if (!dst->wf || !dst->act_side || !dst->start_side || !dst->reset_keys || !dst->arena) return -1;
+  const crr_events& ev = dst->ev;
+  if (!ev.etype || !ev.event_id || !ev.version || !ev.timestamp || !ev.task_id || !ev.ref || !ev.key || !ev.aux) return -1;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf);
+  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events);
+  Plan P = c.P;
+  const u32 nw = in->n_wf, n_lane = S->wave_begin, n_groups = (n_lane + 63) / 64, n_tail = nw - n_lane;
+  Dst D;
+  D.ev = ev;
+  D.act = const_cast<crr_activity_side*>(dst->act_side);
+  D.start = const_cast<crr_start_side*>(dst->start_side);
+  D.reset_keys = const_cast<u32*>(dst->reset_keys);
+  D.arena = const_cast<u8*>(dst->arena);
+  D.wf = const_cast<crr_workflow*>(dst->wf);
+  hipError_t e;
+  // side records not referenced by any event stay zero, like flatten's zero-filled arrays
+  if ((e = hipMemsetAsync(D.act, 0, S->n_act_side * sizeof(crr_activity_side), s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(D.start, 0, S->n_start_side * sizeof(crr_start_side), s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(D.reset_keys, 0, S->n_reset_keys * 4, s)) != hipSuccess) return (int)e;
+  if (S->n_act_side == 1 || S->n_start_side == 1) {
+    // no event references the array: it is the canonical one (the placeholder or the lone record)
+  }
+  if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups);
+  if (n_tail) hipLaunchKernelGGL(layout_tail_kernel, dim3(n_tail), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups, n_tail);
+  if (nw) hipLaunchKernelGGL(layout_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P, D, n_lane,
+                             n_groups, n_tail);
+  const u64 E2 = 2 * max_events;
+  hipLaunchKernelGGL(layout_reset_keys_kernel, dim3((unsigned)((E2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P,
+                     D.reset_keys, E2);
+  if (perm && nw && (e = hipMemcpyAsync(perm, P.perm, 4ull * nw, hipMemcpyDeviceToDevice, s)) != hipSuccess) return (int)e;
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

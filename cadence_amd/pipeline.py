@@ -154,3 +154,152 @@ class StreamingReplay:
                 rows[name] = c.host_rows[name][:int(off[t, n]) * dt.itemsize].numpy().view(dt).copy()
             out.append(CompactResult(c.host_exec.numpy().view(abi.EXEC_ROW).copy(), off, rows))
         return out
+
+
+# ---- persisted blobs -> device rows, end to end ----------------------------------------------------------------
+def split_blobs(bs, chunks: int):
+    """Split a BlobSet at workflow boundaries into `chunks` BlobSets (blob ranges and offsets rebased).
+    Continue-as-new links (new_run_wf) must stay inside a chunk: the split moves a boundary forward
+    past any workflow whose new-run history would land in the next chunk."""
+    from .blobs import BlobSet
+    n = bs.n_wf
+    bounds = [int(x) for x in np.linspace(0, n, chunks + 1)]
+    nr = bs.wf["new_run_wf"].astype(np.int64)
+    for i in range(1, chunks):
+        b = bounds[i]
+        while 0 < b < n and ((nr[:b] >= b).any()):
+            b += 1
+        bounds[i] = max(b, bounds[i - 1])
+    out = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        wf = bs.wf[a:b].copy()
+        if b == a:
+            continue
+        b0 = int(wf["blob_begin"][0])
+        b1 = int(wf["blob_begin"][-1] + wf["blob_count"][-1])
+        o0, o1 = int(bs.blob_off[b0]), int(bs.blob_off[b1])
+        wf["blob_begin"] -= b0
+        wf["new_run_wf"] = np.where(wf["new_run_wf"] >= 0, wf["new_run_wf"] - a, -1)
+        data = np.zeros(o1 - o0 + 32, np.uint8)
+        data[:o1 - o0] = bs.bytes[o0:o1]
+        out.append(BlobSet(bytes=data, blob_off=(bs.blob_off[b0:b1 + 1] - o0).astype(np.uint64), wf=wf,
+                           strings=bs.strings))
+    return out
+
+
+class BlobStreamingReplay:
+    """Persisted blobs in host memory -> replayed rows in host memory, chunked and overlapped: per chunk
+    the H2D of the blobs (pinned staging, as read from persistence), crr_ingest_plan + crr_ingest_layout
+    (decode, intern, order, interleave on the device), the replay, crr_compact_rows and the D2H of the
+    exec rows + live rows.  Uploads run ahead on their own stream; chunks alternate between two compute
+    streams so one chunk's plan (which synchronises its stream to size the layout) overlaps the previous
+    chunk's replay; downloads on a third stream."""
+
+    def __init__(self, eng: ReplayEngine, chunks):
+        from .ingest import DeviceIngest
+        torch = eng.torch
+        self.eng, self.torch = eng, torch
+        self.parts = []
+        for bs in chunks:
+            ing = DeviceIngest(eng)
+            host = {k: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).pin_memory()
+                    for k, a in ing.host_arrays(bs).items()}
+            db = ing.upload(bs, host={k: v.numpy() for k, v in host.items()})
+            S = ing.plan(db)                            # sizes the scratch and the buffers once (untimed)
+            out = ing.layout(db, S)
+            eng.compact(out)
+            n = int(S.n_wf)
+            host_rows = {name: torch.empty(out.tensors["cmp_" + name].numel(), dtype=torch.uint8).pin_memory()
+                         for name in COMPACT_TABLES}
+            self.parts.append({"bs": bs, "ing": ing, "db": db, "host": host, "out": out, "S": S, "n": n,
+                               "n_events": int(S.n_events),
+                               "host_exec": torch.empty(n * abi.EXEC_ROW.itemsize, dtype=torch.uint8).pin_memory(),
+                               "host_off": torch.empty(len(COMPACT_TABLES) * (n + 1), dtype=torch.int64).pin_memory(),
+                               "host_rows": host_rows,
+                               "host_tot": torch.empty(len(COMPACT_TABLES), dtype=torch.int64).pin_memory()})
+        torch.cuda.synchronize(eng.dev)
+        self.up = torch.cuda.Stream(eng.dev)
+        self.comp = [torch.cuda.Stream(eng.dev), torch.cuda.Stream(eng.dev)]
+        self.down = torch.cuda.Stream(eng.dev)
+
+    @property
+    def n_events(self) -> int:
+        return sum(p["n_events"] for p in self.parts)
+
+    @property
+    def h2d_bytes(self) -> int:
+        return int(sum(t.numel() for p in self.parts for t in p["host"].values()))
+
+    def run(self) -> Dict[str, float]:
+        torch, eng = self.torch, self.eng
+        torch.cuda.synchronize(eng.dev)
+        t0 = time.perf_counter()
+        ev_up, ev_tot = [], []
+        for p in self.parts:                                        # 1. every upload, in order
+            with torch.cuda.stream(self.up):
+                for k, h in p["host"].items():
+                    p["db"].tensors[k][:h.numel()].copy_(h, non_blocking=True)
+                e = torch.cuda.Event()
+                e.record(self.up)
+                ev_up.append(e)
+        for i, (p, e) in enumerate(zip(self.parts, ev_up)):        # 2. ingest + replay + compaction
+            s = self.comp[i % 2]
+            s.wait_event(e)
+            S = p["ing"].plan(p["db"], s)                          # (synchronises s: the layout's sizes)
+            out = p["out"]
+            T = out.tensors
+            with torch.cuda.stream(s):
+                for k in ("exec", "scratch"):
+                    T[k].zero_()
+                for name, *_ in abi.TABLES:
+                    T["out_" + name].zero_()
+            p["ing"].layout(p["db"], S, s, out=out)
+            eng.launch(out, s)
+            eng.compact(out, s)
+            n = p["n"]
+            with torch.cuda.stream(s):
+                p["host_tot"].copy_(T["cmp_offsets"].view(len(COMPACT_TABLES), n + 1)[:, n], non_blocking=True)
+                et = torch.cuda.Event()
+                et.record(s)
+            ev_tot.append(et)
+        d2h = 0
+        for p, et in zip(self.parts, ev_tot):                       # 3. exact-size downloads
+            et.synchronize()
+            tot = p["host_tot"].numpy().copy()
+            p["totals"] = tot
+            self.down.wait_event(et)
+            T = p["out"].tensors
+            n = p["n"]
+            with torch.cuda.stream(self.down):
+                p["host_exec"].copy_(T["exec"][:n * abi.EXEC_ROW.itemsize], non_blocking=True)
+                p["host_off"].copy_(T["cmp_offsets"], non_blocking=True)
+                d2h += n * abi.EXEC_ROW.itemsize + p["host_off"].numel() * 8
+                for t, (name, dt, *_) in enumerate(abi.TABLES):
+                    nb = int(tot[t]) * dt.itemsize
+                    if nb:
+                        p["host_rows"][name][:nb].copy_(T["cmp_" + name][:nb], non_blocking=True)
+                        d2h += nb
+        self.down.synchronize()
+        wall = time.perf_counter() - t0
+        return {"wall_s": wall, "events": self.n_events, "events_per_s": self.n_events / wall,
+                "h2d_bytes": self.h2d_bytes, "d2h_bytes": int(d2h), "chunks": len(self.parts)}
+
+    def results(self) -> List[CompactResult]:
+        out = []
+        for p in self.parts:
+            n = p["n"]
+            off = p["host_off"].numpy().reshape(len(COMPACT_TABLES), n + 1).copy()
+            rows = {}
+            for t, (name, dt, *_) in enumerate(abi.TABLES):
+                rows[name] = p["host_rows"][name][:int(off[t, n]) * dt.itemsize].numpy().view(dt).copy()
+            out.append(CompactResult(p["host_exec"].numpy().view(abi.EXEC_ROW).copy(), off, rows))
+        return out
+
+    def ev_counts(self) -> List[np.ndarray]:
+        """Per chunk, the descriptors' ev_count in device order (for dist.digest_numpy)."""
+        out = []
+        for p in self.parts:
+            n = p["n"]
+            wf = p["out"].tensors["wf"][:n * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
+            out.append(wf["ev_count"].copy())
+        return out

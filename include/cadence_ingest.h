@@ -1,0 +1,116 @@
+/*
+ * cadence_ingest.h -- device-side ingest: persisted thriftrw history blobs in HBM -> the replay engine's
+ * wave-interleaved, tiered crr_inputs, on the GPU.
+ *
+ * Replaces, for a batch of workflows whose persisted batches are already in device memory (uploaded
+ * as they were read from persistence), the host work before crr_replay:
+ *
+ *   common/persistence/serializer.go:109-119, :312-335   DeserializeBatchEvents (thriftrw blob -> events)
+ *   common/codec/version0Thriftrw.go:44-61               0x59 preamble + thrift binary (go.uber.org/thriftrw v1.29.2)
+ *   .gen/go/shared/shared.go:41935-42460                 HistoryEvent / *EventAttributes wire layout
+ *   the cgo shim's flattening and layout: events -> SoA columns, interned
+ *   ActivityID / TimerID / BinaryChecksum keys, domain-cache outcomes, slot-table capacities, the
+ *   length / expected-live-set ordering and the 64-workflow wave interleave
+ *
+ * The result is byte-identical to the host path (crr_decode_histories, cadence_amd/flatten.interleave
+ * with its default long-history threshold and tiering) on the same blobs: the same columns, side
+ * records, descriptors, tier boundaries and slot-table sizes.  Only thriftrw (and empty) blobs are
+ * decoded here; a batch holding json / unknown-encoded blobs goes through the host decoder
+ * (cadence_decode.h), and so do loaded states (CRR_WF_FLAG_RESUME), which are not blobs.
+ *
+ * Two calls, because the caller sizes the replay's buffers between them:
+ *   crr_ingest_plan   parse every blob (twice: count, then decode into a canonical scratch layout),
+ *                     intern keys, resolve domains, per-workflow capacities and live-set bounds, the
+ *                     device order (radix sort) and the group geometry; writes a crr_ingest_summary
+ *   crr_ingest_layout write the interleaved columns, side records, reset keys, branch tokens and
+ *                     descriptors into the caller's buffers (sized from the summary)
+ * Both enqueue on `stream` and return 0 on a successful launch, -1 on an invalid argument, else the
+ * hipError_t.  All pointers are device pointers unless noted.
+ */
+#ifndef CADENCE_INGEST_H_
+#define CADENCE_INGEST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "cadence_replay.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One workflow's persisted batches and host inputs (crr_wf_source of cadence_decode.h with the strings
+ * as (offset, length) into crr_blob_batch.strings).  Workflows' blob ranges are consecutive:
+ * wf[0].blob_begin == 0 and wf[w + 1].blob_begin == wf[w].blob_begin + wf[w].blob_count. */
+typedef struct crr_blob_wf {
+    uint32_t blob_begin;
+    uint32_t blob_count;
+    int64_t  init_version;          /* domainEntry.GetFailoverVersion() */
+    int64_t  now_ns;                /* injected timeSource.Now() */
+    uint32_t run_id_off, run_id_len;        /* tree ID of the branch token */
+    uint32_t branch_id_off, branch_id_len;  /* injected branch ID (state_builder.go:179-183) */
+    uint32_t final_token_off;       /* rebuild target token bytes in `strings`; len UINT32_MAX: none */
+    uint32_t final_token_len;
+    int64_t  rebuild_last_event_id;
+    int64_t  rebuild_last_event_version;
+    int32_t  new_run_wf;            /* workflow index (this batch's order) of the CAN new-run history, -1 */
+    int32_t  flags;                 /* CRR_WF_FLAG_NEW_RUN | CRR_WF_FLAG_REFRESH_TASKS */
+    int32_t  retention_days;
+    int32_t  reserved;
+} crr_blob_wf;                      /* 80 B */
+
+typedef struct crr_blob_batch {
+    const uint8_t*     bytes;       /* every blob, concatenated */
+    const uint64_t*    blob_off;    /* [n_blobs + 1] byte offsets into `bytes` */
+    uint32_t           n_blobs;
+    uint32_t           n_wf;
+    const crr_blob_wf* wf;          /* [n_wf] */
+    const uint8_t*     strings;     /* run / branch IDs, final tokens, known domain names */
+    const uint32_t*    domain_off;  /* [n_domains] known domain names in `strings` */
+    const uint32_t*    domain_len;
+    uint32_t           n_domains;   /* UINT32_MAX: every name resolves */
+    uint32_t           reserved;
+} crr_blob_batch;
+
+/* What the plan reports (a host struct, written by crr_ingest_plan once its work on `stream` is done:
+ * the plan synchronises the stream twice, to size its own launches and to read this back). */
+typedef struct crr_ingest_summary {
+    int32_t  err;                   /* CRR_DECODE_* of the failing blob with the lowest index, 0: ok */
+    int32_t  reserved0;
+    int64_t  err_blob;              /* that blob's index, -1 */
+    uint64_t n_events;              /* real events */
+    uint64_t n_slots;               /* event-column slots of the layout (lane groups padded + the tail) */
+    uint64_t n_act_side;            /* activity side-record slots */
+    uint64_t n_start_side;          /* start side-record slots */
+    uint64_t n_reset_keys;
+    uint64_t arena_bytes;           /* branch tokens (+ final tokens) */
+    uint64_t table_rows[8];         /* act, timer, child, rc, sig, vh, rp, tasks slot-table rows */
+    uint32_t n_wf;
+    uint32_t wave_begin;            /* lane workflows [0, wave_begin), long-history tail after */
+    uint32_t tiers[6];              /* large_begin, compact_begin, compact2_begin, wide_begin, hbm_begin, big_begin */
+    uint32_t has_new_run;           /* some workflow carries CRR_WF_FLAG_NEW_RUN */
+    uint32_t lds_small_tail;        /* the tail [wave_begin, big_begin) fits the small per-wave arenas */
+} crr_ingest_summary;
+
+/* Device scratch the plan keeps for the layout (opaque), for a batch of at most `max_events` events
+ * (a capacity the caller chooses: the plan reports CRR_INGEST_SCRATCH_TOO_SMALL in summary.err when the
+ * blobs hold more, and the caller plans again with more).  Both calls take the same scratch and size. */
+size_t crr_ingest_scratch_bytes(uint32_t n_blobs, uint32_t n_wf, uint64_t max_events);
+#define CRR_INGEST_SCRATCH_TOO_SMALL (-100)
+
+int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, crr_ingest_summary* summary,
+                    void* stream);
+
+/* `dst`: device buffers sized from the summary (columns n_slots entries each; the wf descriptors
+ * n_wf; act_side / start_side / reset_keys / arena their counts, arena 8-byte padded); the scalar
+ * fields of *dst (n_wf, stride, flags, wave_begin, tiers) are the caller's to set from the summary.
+ * `summary_host`: the plan's summary, as read back.  Also writes perm[n_wf] (device position ->
+ * workflow index of the blob batch) when perm != NULL.  `bytes` of the blob batch must be 16-byte
+ * aligned and readable 16 bytes past the last blob (the parser's window loads). */
+int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes,
+                      const crr_ingest_summary* summary_host, const crr_inputs* dst, uint32_t* perm, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CADENCE_INGEST_H_ */

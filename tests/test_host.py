@@ -15,7 +15,7 @@ LIB = os.path.join(ROOT, "cadence_amd", "libcadence_replay.so")
 
 
 def _declared_symbols():
-    txt = open(os.path.join(ROOT, "include", "cadence_replay.h")).read()
+    txt = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("cadence_replay.h", "cadence_ingest.h"))
     return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(crr_\w+)\s*\(", txt, re.M)))
 
 
@@ -24,7 +24,8 @@ def test_library_loads_and_exports_every_declared_symbol():
     lib = ctypes.CDLL(LIB)
     syms = _declared_symbols()
     assert {"crr_replay", "crr_checksum", "crr_set_device", "crr_abi_version", "crr_sizeof",
-            "crr_crc32_ieee", "crr_last_kernel_ms"} <= set(syms)
+            "crr_crc32_ieee", "crr_last_kernel_ms", "crr_release", "crr_ingest_plan", "crr_ingest_layout",
+            "crr_ingest_scratch_bytes"} <= set(syms)
     for s in syms:
         assert hasattr(lib, s), s
     lib.crr_abi_version.restype = ctypes.c_int

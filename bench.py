@@ -61,6 +61,11 @@ def parse():
     return a
 
 
+def progress(msg):
+    """A progress line on stderr (the JSON result stays the only stdout line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def host_cpus() -> int:
     """CPUs this process may run on: the cgroup CPU quota when one is set (the GPU box's per-GPU share),
     else the affinity mask."""
@@ -646,6 +651,7 @@ def main():
     from cadence_amd import synth_native
     from cadence_amd import dist as cdist
     line, batch2, res2, db2 = config2(ctx)
+    progress("config 2 done")
     if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
         from cadence_amd.flatten import interleave
         from cadence_amd import synth
@@ -666,7 +672,9 @@ def main():
             lambda: synth_native.mixed(50_000, shard=shard))
         del db3
         torch.cuda.empty_cache()
+        progress("config 3 done")
         pr = passive_replication(ctx, b3, r3)
+        progress("passive replication done")
         del b3, r3
         torch.cuda.empty_cache()
         n4 = args.c4_workflows * ctx.world
@@ -678,12 +686,15 @@ def main():
             lambda: synth_native.long_tail(60, shard=shard))
         del db4, b4, r4
         torch.cuda.empty_cache()
+        progress("config 4 done")
         c5 = config5(ctx, args.c5_workflows, shard)
         torch.cuda.empty_cache()
+        progress("config 5 done")
         line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr,
                            "config5_ndc": c5}
     if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
         line["pcie_inclusive"] = end_to_end(ctx, args.workflows, args.activities)
+        progress("end to end (columns) done")
         e2e = line["pcie_inclusive"]
         e2e["matches_resident_digest"] = e2e["digest"] == line["digest"] and e2e["columns_wide"]["digest"] == line["digest"]
         line["host_ingest"] = host_ingest(ctx, flat_s, flat_ev)
@@ -694,10 +705,12 @@ def main():
             ctx, c2_canon, line["digest"],
             f"config 2 persisted: {args.workflows} activity-chain workflows, one thriftrw blob per ApplyEvents batch")}
         del c2_canon
+        progress("blob -> rows config 2 done")
         c3_canon = synth_native.mixed(args.c3_workflows, shard=(cdist.NUM_SHARDS, 1, 0))
         line["blob_to_rows"]["config3_shard"] = blob_to_rows(
             ctx, c3_canon, None, f"config 3 shard persisted: {args.c3_workflows} mixed histories, one thriftrw blob per batch")
         del c3_canon
+        progress("blob -> rows config 3 done")
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ctx, res2, batch2, args.activities)
         if "pcie_inclusive" in line:

@@ -182,8 +182,21 @@ def split_blobs(bs, chunks: int):
         wf["new_run_wf"] = np.where(wf["new_run_wf"] >= 0, wf["new_run_wf"] - a, -1)
         data = np.zeros(o1 - o0 + 32, np.uint8)
         data[:o1 - o0] = bs.bytes[o0:o1]
+        # this chunk's strings only (run / branch IDs, final tokens), offsets rebased
+        spans = [(wf["run_id_off"], wf["run_id_len"]), (wf["branch_id_off"], wf["branch_id_len"])]
+        has_ft = wf["final_token_len"] != abi.NO_TOKEN
+        spans.append((np.where(has_ft, wf["final_token_off"], 0), np.where(has_ft, wf["final_token_len"], 0)))
+        lens = np.stack([ln.astype(np.int64) for _o, ln in spans], axis=1)
+        new_off = (np.cumsum(lens.reshape(-1)) - lens.reshape(-1)).reshape(lens.shape)
+        offs = np.stack([o.astype(np.int64) for o, _l in spans], axis=1).reshape(-1)
+        fl = lens.reshape(-1)
+        idx = np.repeat(offs - (np.cumsum(fl) - fl), fl) + np.arange(int(fl.sum()), dtype=np.int64)
+        strings = bs.strings[idx] if idx.size else np.zeros(1, np.uint8)
+        wf["run_id_off"] = new_off[:, 0]
+        wf["branch_id_off"] = new_off[:, 1]
+        wf["final_token_off"] = np.where(has_ft, new_off[:, 2], 0)
         out.append(BlobSet(bytes=data, blob_off=(bs.blob_off[b0:b1 + 1] - o0).astype(np.uint64), wf=wf,
-                           strings=bs.strings))
+                           strings=strings if strings.size else np.zeros(1, np.uint8)))
     return out
 
 

@@ -56,3 +56,24 @@ def test_blobs_match_the_python_writer():
         for i, pb in enumerate(py):
             nb = bs.blob(int(r["blob_begin"]) + i)
             assert nb[:9] == pb[:9]       # preamble, list header, event count
+
+
+def test_split_blobs_keeps_workflows_and_new_run_links():
+    """pipeline.split_blobs: chunks at workflow boundaries (never between a continue-as-new run and its
+    new-run history), each with only its own strings; decoding the chunks gives the whole batch."""
+    from cadence_amd.pipeline import split_blobs
+    b = synth_native.mixed(3000, can_rate=0.5)
+    bs = encode_batch(b)
+    parts = split_blobs(bs, 5)
+    assert sum(p.n_wf for p in parts) == b.n_wf
+    assert sum(p.strings.size for p in parts) == bs.strings.size
+    src, base = [], 0
+    for p in parts:
+        nr = p.wf["new_run_wf"]
+        assert ((nr < 0) | (nr < p.n_wf)).all()
+        for s in p.to_sources():
+            if s.new_run is not None:
+                s.new_run += base
+            src.append(s)
+        base += p.n_wf
+    assert_same_batch(decode_histories(src, known_domains=KNOWN_DOMAINS), b)

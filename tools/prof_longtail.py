@@ -56,7 +56,6 @@ def main():
         db = eng.upload(ib)
         eng.launch(db)
         torch.cuda.synchronize()
-        dbg = debug_cycles(eng)      # clears the instrumented build's counters (None otherwise)
         ms = []
         for _ in range(a.reps):
             eng.launch(db)
@@ -78,40 +77,44 @@ def main():
                           "ok": int((res.exec["status"] == 0).sum()), "same_as_first": same,
                           "retries_lane_wave": retries, "phase_ms": k,
                           "gen_s": gen_s}), flush=True)
-        dbg = debug_cycles(eng)
-        if dbg is not None:
-            print_cycles(dbg, a.reps)
+        if ib.wave_begin is not None:
+            wr = wave_records(eng, ib)
+            if wr is not None:
+                print(json.dumps({"threshold": th, "wave_records": wr}), flush=True)
 
 
-def debug_cycles(eng):
-    """CRR_EXP=128 builds: per-event-type shader cycles of the one-wavefront-per-workflow path."""
+def wave_records(eng, ib):
+    """tools/instrument_wave.py builds: per wavefront-path workflow, its start / end (100 MHz realtime) and
+    the core cycles of each part of the event loop; summarised over the tail (None for product builds)."""
     import ctypes
     import numpy as np
-    f = getattr(eng.lib, "crr_debug_cycles", None)
+    f = getattr(eng.lib, "crr_wave_dbg_read", None)
     if f is None:
         return None
-    buf = (ctypes.c_ulonglong * 320)()
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    if f(ctypes.addressof(buf), 320) != 320:
-        raise RuntimeError("crr_debug_cycles failed")
-    return np.frombuffer(buf, np.uint64).astype(np.float64).reshape(5, 64)
-
-
-def print_cycles(d, reps):
-    import numpy as np
-    from cadence_amd.abi import EventType
-    names = {int(e): e.name for e in EventType}
-    n = d[3]
-    tot = d[0] + d[1] + d[2]
-    print(f"wave path: {d[4][1] / reps:.0f} workflows/launch, {n.sum() / reps:.0f} events/launch, "
-          f"{d[4][0] / max(n.sum(), 1):.0f} cycles/event overall, {d[4][2] / max(d[4][1], 1):.0f} cycles/workflow tail")
-    print(f"{'type':42s} {'events':>10s} {'share':>6s} {'prolog':>7s} {'disp':>7s} {'epil':>7s} {'cyc%':>6s}")
-    for t in np.argsort(-tot):
-        if n[t] == 0:
-            continue
-        print(f"{names.get(int(t), str(t)):42s} {n[t] / reps:10.0f} {n[t] / n.sum():6.3f} {d[0][t] / n[t]:7.0f} "
-              f"{d[1][t] / n[t]:7.0f} {d[2][t] / n[t]:7.0f} {tot[t] / tot.sum() * 100:6.1f}")
-    print(flush=True)
+    buf = np.zeros(8 * 65536, np.uint64)
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    if f(buf.ctypes.data, buf.nbytes) != 0:
+        raise RuntimeError("crr_wave_dbg_read failed")
+    d = buf.reshape(65536, 8)
+    lo = ib.wave_begin
+    w = np.arange(lo, ib.n_wf)
+    r = d[w & 65535]
+    ev = (r[:, 2] & 0xFFFFFFFF).astype(np.int64)
+    ok = (ev > 0) & (r[:, 1] > r[:, 0])
+    r, ev, w = r[ok], ev[ok], w[ok]
+    t0 = int(r[:, 0].min())
+    start_us = (r[:, 0] - t0) / 100.0
+    end_us = (r[:, 1] - t0) / 100.0
+    dur_us = end_us - start_us
+    cyc = r[:, 3:7].astype(np.float64)
+    tot = cyc.sum(axis=1)
+    top = np.argsort(-end_us)[:10]
+    return {"workflows": int(ok.sum()), "events": int(ev.sum()), "span_us": float(end_us.max()),
+            "us_per_event_median": float(np.median(dur_us / ev)), "cycles_per_event_median": float(np.median(tot / ev)),
+            "start_us_max": float(start_us.max()),
+            "cycle_share": {k: float(v) for k, v in zip(("fetch", "vh", "dispatch", "epilogue"), cyc.sum(axis=0) / tot.sum())},
+            "critical": [{"events": int(ev[i]), "start_us": float(start_us[i]), "end_us": float(end_us[i]),
+                          "us_per_event": float(dur_us[i] / ev[i]), "cycles_per_event": float(tot[i] / ev[i])} for i in top]}
 
 
 if __name__ == "__main__":

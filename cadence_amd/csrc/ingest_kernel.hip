@@ -8,24 +8,29 @@
 //   cadence_amd/flatten.py                live_set_bounds, tier_classes, interleave, _interleave_side
 //
 // Pipeline (crr_ingest_plan, then crr_ingest_layout once the caller has sized its buffers):
-//   1 blob_wf_kernel       blob -> workflow map
-//   2 blob_count_kernel    lane per blob: full thrift walk, counts (events, activity / start side
-//                          records, key strings); the first failing blob's error
-//   3 multi_scan           exclusive prefixes of the counts: every blob's slice of the canonical
-//                          (stride-1, workflow-order) scratch columns
-//   4 blob_decode_kernel   lane per blob: the same walk, writing columns, side records and key-string
-//                          references; domain names resolved against a device hash set
-//   5 wf_pass_kernel       lane per workflow: interning (per-workflow open-addressed table over string
-//                          hashes, exact byte compares), capacities, VH items, tasks, live-set bounds
-//                          (valid deletes through a second table), tier class, sort key
+//   1 blob_head_kernel     lane per blob: the event count from the History list header (a full walk
+//                          only for a blob not in thriftrw's canonical shape); blob -> workflow map
+//   2 scan                 exclusive prefixes: every blob's slice of the canonical (stride-1,
+//                          workflow-order) scratch columns
+//   3 blob_decode_kernel   lane per blob, the one full thrift walk: columns, side records and key-string
+//                          references (with their hashes) at the events' own slots; domain names
+//                          resolved against a device hash set; previous reset points counted
+//   4 reset_refs_kernel    the previous reset points' strings at their canonical reset_keys positions
+//   5 wf_pass_kernel       lane per workflow: interning (per-workflow open-addressed table over the
+//                          string hashes, exact byte compares), side-record ordinals, capacities, VH
+//                          items, tasks, live-set bounds (valid deletes through a second table), tier
+//                          class, sort key
 //   6 radix sort (hipCUB)  device order = (long, tier | big, -length, index)
 //   7 geometry             per-group maxima (one wavefront per group), prefixes over groups and the
 //                          tail, tier boundaries, the summary
 //   layout                 interleaved columns + side records (block per group / tail workflow),
 //                          descriptors, branch tokens, reset keys
+// A blob whose walk finds more events than its header announced (hand-made blobs: a second events
+// list) sends the plan back to a full counting walk of every blob before decoding.
 //
-// Parsing is integer / byte work: lanes walk their own blob through a 16-byte register window (one
-// aligned dwordx4 load per 16 bytes instead of a dependent byte load each), no MFMA, no LDS staging.
+// Parsing is integer / byte work: lanes walk their own blob through a 32-byte register window (aligned
+// dwordx4 loads, one per 16 bytes of a sequential walk) and take each field header / integer with one
+// funnel-shift extraction instead of a load per byte; no MFMA, no LDS staging.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -62,39 +67,42 @@ __constant__ int8_t kTasksPerEvent[CRR_EV_TYPE_COUNT] = {
     0, 2, 1, 0, 0, 0, 0, 2, 2, 1, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 1};
 
 // ---- scratch layout ------------------------------------------------------------------------------------
-// Per blob counts (u32): events, activity side records, start side records, key strings.
-constexpr int kCnt = 4;
-struct KeyRef {     // one string to intern, in parse order: an event's key or a previous reset point
+struct KeyRef {     // a string to intern (an event's key or a previous reset point): where, and its hash
   u64 off;          // byte offset of the string in `bytes`
   u32 len;
-  u32 is_reset;     // 0: key column of event `dst`; 1: reset_keys[dst]
-  u64 dst;
+  u32 hash;         // FNV-1a 32 of its bytes
+};
+// the Points list of a start event's PrevAutoResetPoints (kept in its key slot: Started has no key)
+struct PrevRef {
+  u64 pos;          // first element's byte offset
+  u32 n;
+  u32 et;           // element type
 };
 
 struct Plan {       // pointers into the caller's scratch (carved by carve())
   u32* blob_wf;              // [n_blobs]
-  u32* cnt;                  // [kCnt][n_blobs]
-  u64* off;                  // [kCnt][n_blobs + 1] exclusive prefixes
+  u32* cnt;                  // [2][n_blobs]: events (header count), previous reset points (decode)
+  u64* off;                  // [2][n_blobs + 1] exclusive prefixes
   u64* err;                  // [1] (blob << 8) | -code, min wins
+  u32* flags;                // [1] bit 0: a header count was wrong (recount)
   u64* tile;                 // scan tiles
   // canonical scratch columns [max_events]
   u8* etype; i64* id; i64* ver; i64* ts; i64* task; i64* ref; u32* key; i32* aux;
-  crr_activity_side* act;    // [max_events]
-  crr_start_side* start;     // [max_events]
-  KeyRef* keys;              // [2 * max_events] key entries (event keys + previous reset points)
-  u32* entry_id;             // [2 * max_events] interned id of each key entry
-  u32* reset_flag;           // [2 * max_events] 1: a reset-point entry (scan input)
-  u64* reset_pos;            // [2 * max_events + 1] its reset_keys index (exclusive prefix)
-  u64* table;                // per-workflow hash tables [2 * max_events + 64 * n_wf]
+  crr_activity_side* act;    // [max_events] at the ActivityTaskScheduled event's own slot
+  crr_start_side* start;     // [max_events] at the WorkflowExecutionStarted event's own slot
+  KeyRef* keys;              // [max_events] a keyed event's string (a Started event's PrevRef)
+  KeyRef* resets;            // [max_events] previous reset points, canonical reset_keys order
+  u32* reset_ids;            // [max_events] their interned ids (= the reset_keys array)
+  u64* table;                // per-workflow hash tables [8 * max_events + 64 * n_wf]
   // per workflow (canonical order)
   i32* wf_info;              // [kWfInfo][n_wf]
   u64* sort_in; u64* sort_out;     // [n_wf]
   void* sort_tmp; size_t sort_tmp_bytes;
   u32* perm; u32* inv;       // [n_wf]
   u64* arena_off;            // [n_wf + 1]
-  u64* gvals;                // [kGeo][n_groups]   group maxima, then exclusive prefixes in place
-  u64* tvals;                // [kGeo][n_wf]       tail values, then prefixes
-  u64* gpre; u64* tpre;
+  u64* gvals;                // [kGeo][n_groups]   group maxima
+  u64* tvals;                // [kGeo][n_wf]       tail values
+  u64* gpre; u64* tpre;      // their exclusive prefixes
   u32* counters;             // [16]
   u32* dom_table; u32 dom_cap;
   u32 n_blobs, n_wf;
@@ -112,12 +120,15 @@ __host__ __device__ inline size_t align_up(size_t x) { return (x + 255) & ~(size
 constexpr size_t kDomainBytes = 64 * 1024;   // the known-domain set (<= 8192 names)
 constexpr i32 kErrScratch = -100;            // CRR_INGEST_SCRATCH_TOO_SMALL
 
-// ---- byte reader over one blob: a 16-byte aligned window in registers ----------------------------------
+// ---- byte reader over one blob: a 32-byte aligned window in registers ----------------------------------
+// The window holds bytes [wb, wb + 32); any read of up to 8 bytes starting in its first half is served
+// from registers.  A sequential walk shifts it by 16 bytes with one dwordx4 load.  `bytes` is readable
+// 32 bytes past the last blob (cadence_ingest.h).
 struct Rd {
   const u8* b;
   u64 p, end;
-  u64 wb;            // window base (aligned), ~0: none
-  uint4 w;
+  u64 wb;            // window base (16-aligned), ~0: none
+  uint4 w0, w1;
   int err;           // CRR_DECODE_* (0 ok)
 
   __device__ __forceinline__ void init(const u8* bytes, u64 begin, u64 e) {
@@ -128,39 +139,58 @@ struct Rd {
     if (end - p < n) { err = CRR_DECODE_TRUNCATED; return false; }
     return true;
   }
-  __device__ __forceinline__ u32 at(u64 q) {   // byte q (caller checked bounds)
+  // bytes q .. q+7 in memory order (little-endian u64)
+  __device__ __forceinline__ u64 peek8(u64 q) {
     const u64 a = q & ~15ull;
     if (a != wb) {
-      w = *reinterpret_cast<const uint4*>(b + a);
+      if (a == wb + 16) {
+        w0 = w1;
+      } else {
+        w0 = *reinterpret_cast<const uint4*>(b + a);
+      }
+      w1 = *reinterpret_cast<const uint4*>(b + a + 16);
       wb = a;
     }
-    const u32 o = (u32)(q & 15);
-    const u32 word = (o < 8) ? ((o < 4) ? w.x : w.y) : ((o < 12) ? w.z : w.w);
-    return (word >> ((o & 3) * 8)) & 0xff;
+    const u32 o = (u32)(q & 15), k = o >> 2, sh = (o & 3) * 8;
+    const u32 x0 = k == 0 ? w0.x : k == 1 ? w0.y : k == 2 ? w0.z : w0.w;
+    const u32 x1 = k == 0 ? w0.y : k == 1 ? w0.z : k == 2 ? w0.w : w1.x;
+    const u32 x2 = k == 0 ? w0.z : k == 1 ? w0.w : k == 2 ? w1.x : w1.y;
+    const u32 lo = sh ? (x0 >> sh) | (x1 << (32 - sh)) : x0;
+    const u32 hi = sh ? (x1 >> sh) | (x2 << (32 - sh)) : x1;
+    return ((u64)hi << 32) | lo;
   }
   __device__ __forceinline__ u32 u8_() {
     if (!need(1)) return 0;
-    return at(p++);
+    return (u32)peek8(p++) & 0xff;
   }
   __device__ __forceinline__ i32 be16() {
     if (!need(2)) return 0;
-    const u32 v = (at(p) << 8) | at(p + 1);
+    const u32 v = (u32)peek8(p);
     p += 2;
-    return (i32)(int16_t)v;
+    return (i32)(int16_t)(((v & 0xff) << 8) | ((v >> 8) & 0xff));
   }
   __device__ __forceinline__ i32 be32() {
     if (!need(4)) return 0;
-    u32 v = 0;
-    for (int i = 0; i < 4; ++i) v = (v << 8) | at(p + i);
+    const u32 v = (u32)peek8(p);
     p += 4;
-    return (i32)v;
+    return (i32)__builtin_bswap32(v);
   }
   __device__ __forceinline__ i64 be64() {
     if (!need(8)) return 0;
-    u64 v = 0;
-    for (int i = 0; i < 8; ++i) v = (v << 8) | at(p + i);
+    const u64 v = peek8(p);
     p += 8;
-    return (i64)v;
+    return (i64)__builtin_bswap64(v);
+  }
+  // a struct's next field header (type byte, then big-endian i16 id); false at the stop byte or an error
+  __device__ __forceinline__ bool field(u32& ft, i32& id) {
+    if (!need(1)) return false;
+    const u32 v = (u32)peek8(p);
+    ft = v & 0xff;
+    if (ft == T_STOP) { ++p; return false; }
+    if (!need(3)) return false;
+    id = (i32)(int16_t)(((v >> 8) & 0xff) << 8 | ((v >> 16) & 0xff));
+    p += 3;
+    return true;
   }
   // a thrift string: its (offset, length) in the blob bytes
   __device__ __forceinline__ void str(u64& off, u32& len) {
@@ -172,13 +202,59 @@ struct Rd {
     len = (u32)n;
     p += (u64)n;
   }
-  // skip one value of `type` (history_decode.cpp Reader::skip: nesting deeper than 64 is BAD_TYPE),
-  // iteratively: a stack of open containers (struct: until its stop byte; list / set / map: remaining
-  // elements and their types)
+  // FNV-1a 32 over bytes [off, off + len) through the window (the string was just walked past)
+  __device__ __forceinline__ u32 hash(u64 off, u32 len) {
+    u32 h = 2166136261u;
+    u32 i = 0;
+    while (i < len) {
+      const u64 v = peek8(off + i);
+      const u32 m = len - i < 8 ? len - i : 8;
+      for (u32 j = 0; j < m; ++j) h = (h ^ (u32)((v >> (8 * j)) & 0xff)) * 16777619u;
+      i += m;
+    }
+    return h;
+  }
+  // skip one value of `type` (history_decode.cpp Reader::skip: a value nested deeper than 64 is
+  // BAD_TYPE).  Structs, strings and scalars -- all a HistoryEvent's skipped fields but a few -- need only
+  // a count of open structs; a list / set / map goes to the general walk with its own stack.
   __device__ void skip(u32 type) {
+    u32 t = type;
+    int open = 0;   // open structs: the value about to be skipped sits at this depth
+    for (;;) {
+      if (err) return;
+      if (open > 64) { err = CRR_DECODE_BAD_TYPE; return; }
+      switch (t) {
+        case T_BOOL: case T_BYTE: if (need(1)) p += 1; break;
+        case T_I16: if (need(2)) p += 2; break;
+        case T_I32: if (need(4)) p += 4; break;
+        case T_DOUBLE: case T_I64: if (need(8)) p += 8; break;
+        case T_STRING: {
+          const i32 n = be32();
+          if (err) return;
+          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+          if (need((u64)n)) p += (u64)n;
+          break;
+        }
+        case T_STRUCT: ++open; break;
+        case T_MAP: case T_SET: case T_LIST: skip_containers(t, open); break;
+        default: err = CRR_DECODE_BAD_TYPE; return;
+      }
+      if (err) return;
+      // the innermost open struct's next field, closing finished ones
+      for (;;) {
+        if (open == 0) return;
+        i32 id;
+        if (field(t, id)) break;
+        if (err) return;
+        --open;
+      }
+    }
+  }
+  // a list / set / map at depth d0 and everything inside it
+  __device__ void skip_containers(u32 type, int d0) {
     struct Lvl { u8 kind, t1, t2, pad; i32 rem; };
     Lvl st[66];
-    int d = 0;          // depth of the value about to be skipped
+    int d = d0;     // depth of the value about to be skipped
     u32 t = type;
     for (;;) {
       if (err) return;
@@ -196,13 +272,13 @@ struct Rd {
           if (need((u64)n)) p += (u64)n;
           break;
         }
-        case T_STRUCT: st[d] = Lvl{T_STRUCT, 0, 0, 0, 0}; pushed = true; break;
+        case T_STRUCT: st[d - d0] = Lvl{T_STRUCT, 0, 0, 0, 0}; pushed = true; break;
         case T_MAP: {
           const u32 kt = u8_(), vt = u8_();
           const i32 n = be32();
           if (err) return;
           if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          st[d] = Lvl{T_MAP, (u8)kt, (u8)vt, 0, 2 * n};
+          st[d - d0] = Lvl{T_MAP, (u8)kt, (u8)vt, 0, 2 * n};
           pushed = true;
           break;
         }
@@ -211,7 +287,7 @@ struct Rd {
           const i32 n = be32();
           if (err) return;
           if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          st[d] = Lvl{T_LIST, (u8)et, (u8)et, 0, n};
+          st[d - d0] = Lvl{T_LIST, (u8)et, (u8)et, 0, n};
           pushed = true;
           break;
         }
@@ -219,17 +295,15 @@ struct Rd {
       }
       if (err) return;
       if (pushed) ++d;
-      // the next value to skip: the innermost open container's next element, popping finished ones
       for (;;) {
-        if (d == 0) return;
-        Lvl& L = st[d - 1];
+        if (d == d0) return;
+        Lvl& L = st[d - 1 - d0];
         if (L.kind == T_STRUCT) {
-          const u32 ft = u8_();
+          i32 id;
+          if (field(t, id)) break;
           if (err) return;
-          if (ft == T_STOP) { --d; continue; }
-          (void)be16();
-          t = ft;
-          break;
+          --d;
+          continue;
         }
         if (L.rem == 0) { --d; continue; }
         t = (L.kind == T_MAP && (L.rem & 1) == 0) ? L.t1 : L.t2;
@@ -281,10 +355,9 @@ __device__ __forceinline__ int attr_type_of_field(i32 id) {
 // RetryPolicy{60 ExpirationIntervalInSeconds i32}
 __device__ void read_retry_policy(Rd& r, Attr& a) {
   a.has_retry = 1;
-  for (;;) {
-    const u32 ft = r.u8_();
-    if (r.err || ft == T_STOP) return;
-    const i32 id = r.be16();
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
     if (id == 60 && r.want(ft, T_I32)) a.expiration = r.be32();
     else if (id != 60) r.skip(ft);
   }
@@ -294,10 +367,9 @@ __device__ void read_retry_policy(Rd& r, Attr& a) {
 // kept; its strings are read once the event is complete (WfFlattener::add interns them there)
 __device__ void read_reset_points(Rd& r, Attr& a) {
   a.prev_mode = -2;
-  for (;;) {
-    const u32 ft = r.u8_();
-    if (r.err || ft == T_STOP) return;
-    const i32 id = r.be16();
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
     if (id == 10 && ft == T_LIST) {
       const u32 et = r.u8_();
       const i32 n = r.be32();
@@ -309,10 +381,9 @@ __device__ void read_reset_points(Rd& r, Attr& a) {
       a.prev_et = et;
       for (i32 i = 0; i < n && !r.err; ++i) {
         if (et != T_STRUCT) { r.skip(et); continue; }
-        for (;;) {
-          const u32 t2 = r.u8_();
-          if (r.err || t2 == T_STOP) break;
-          const i32 id2 = r.be16();
+        u32 t2;
+        i32 id2;
+        while (r.field(t2, id2)) {
           if (id2 == 10 && t2 == T_STRING) { u64 o; u32 l; r.str(o, l); }
           else r.skip(t2);
         }
@@ -325,11 +396,9 @@ __device__ void read_reset_points(Rd& r, Attr& a) {
 
 // history_decode.cpp read_attributes
 __device__ void read_attributes(Rd& r, int t, Attr& a) {
-  for (;;) {
-    const u32 ft = r.u8_();
-    if (r.err || ft == T_STOP) return;
-    const i32 id = r.be16();
-    if (r.err) return;
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
     bool used = true;
     switch (t) {
       case CRR_EV_WORKFLOW_EXECUTION_STARTED:
@@ -434,11 +503,9 @@ __device__ void read_event(Rd& r, Event& e) {
   bool have_attr_at = false;
   int attr_t = -1;
   bool have_type = false;
-  for (;;) {
-    const u32 ft = r.u8_();
-    if (r.err || ft == T_STOP) break;
-    const i32 id = r.be16();
-    if (r.err) return;
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
     if (id == 10 && ft == T_I64) e.id = r.be64();
     else if (id == 20 && ft == T_I64) e.ts = r.be64();
     else if (id == 30 && ft == T_I32) { e.type = r.be32(); have_type = true; }
@@ -471,7 +538,7 @@ __device__ __forceinline__ bool keyed_type(i32 t) {
          t == CRR_EV_TIMER_CANCELED;
 }
 
-__device__ __forceinline__ u32 fnv1a(const u8* b, u64 off, u32 len) {
+__device__ __forceinline__ u32 fnv1a(const u8* b, u64 off, u32 len) {   // (known domain names)
   u32 h = 2166136261u;
   for (u32 i = 0; i < len; ++i) h = (h ^ b[off + i]) * 16777619u;
   return h;
@@ -514,10 +581,15 @@ __device__ __forceinline__ i32 domain_status(const crr_blob_batch& in, const u32
 // every blob decoded and the canonical scratch large enough: the later passes may read it
 __device__ __forceinline__ bool plan_ok(const Plan& P) {
   const u64 NB = (u64)P.n_blobs + 1;
-  return *P.err == ~0ull && P.off[0 * NB + P.n_blobs] <= P.max_events && P.off[3 * NB + P.n_blobs] <= 2 * P.max_events;
+  return *P.err == ~0ull && *P.flags == 0 && P.off[0 * NB + P.n_blobs] <= P.max_events &&
+         P.off[1 * NB + P.n_blobs] <= P.max_events;
 }
 
-// ---- 1: blob -> workflow ---------------------------------------------------------------------------------
+__device__ __forceinline__ void record_error(u64* err, u32 blob, int code) {
+  atomicMin((unsigned long long*)err, ((u64)blob << 8) | (u64)(-code));
+}
+
+// ---- 1: blob -> workflow, and each blob's event count ----------------------------------------------------
 __global__ void blob_wf_kernel(crr_blob_batch in, u32* blob_wf, u64* err) {
   const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= in.n_wf) return;
@@ -526,54 +598,91 @@ __global__ void blob_wf_kernel(crr_blob_batch in, u32* blob_wf, u64* err) {
   // the consecutive-ranges contract (cadence_ingest.h); a violation fails the plan
   const u32 expect = w == 0 ? 0u : in.wf[w - 1].blob_begin + in.wf[w - 1].blob_count;
   if (s.blob_begin != expect || (w + 1 == in.n_wf && s.blob_begin + s.blob_count != in.n_blobs))
-    atomicMin((unsigned long long*)err, ((u64)0 << 8) | (u64)(-CRR_DECODE_BAD_ARGUMENT));
+    atomicMin((unsigned long long*)err, (u64)(-CRR_DECODE_BAD_ARGUMENT));
 }
 
-__device__ __forceinline__ void record_error(u64* err, u32 blob, int code) {
-  atomicMin((unsigned long long*)err, ((u64)blob << 8) | (u64)(-code));
-}
-
-// ---- 2 / 4: the thrift walk over one blob ---------------------------------------------------------------
-// WRITE = false: counts only (events, activity side, start side, key strings); true: writes the
-// canonical columns at the blob's prefixes.
-template <bool WRITE>
-__device__ void walk_blob(const crr_blob_batch& in, const Plan& P, u32 bi, u32 cnt[kCnt]) {
-  cnt[0] = cnt[1] = cnt[2] = cnt[3] = 0;
-  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
-  if (b1 <= b0) return;   // an empty blob: an empty batch
-  Rd r;
-  r.init(in.bytes, b0, b1);
-  if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
-  u64 ev_at = 0, act_at = 0, st_at = 0, key_at = 0;
-  i32 new_run = -1;
-  if (WRITE) {
-    ev_at = P.off[0 * (P.n_blobs + 1) + bi];
-    act_at = P.off[1 * (P.n_blobs + 1) + bi];
-    st_at = P.off[2 * (P.n_blobs + 1) + bi];
-    key_at = P.off[3 * (P.n_blobs + 1) + bi];
-    new_run = in.wf[P.blob_wf[bi]].new_run_wf;
-  }
-  const u64 ev_first = ev_at;
-  Event e;
-  for (;;) {
-    const u32 ft = r.u8_();
-    if (r.err || ft == T_STOP) break;
-    const i32 id = r.be16();
-    if (r.err) break;
+// the History struct's event lists: the whole walk, counting (the shape thriftrw does not write)
+__device__ u32 count_events(Rd& r) {
+  u32 n_ev = 0;
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
     if (id != 10 || ft != T_LIST) { r.skip(ft); continue; }
     const u32 et = r.u8_();
     const i32 n = r.be32();
     if (r.err) break;
     if (n < 0) { r.err = CRR_DECODE_TRUNCATED; break; }
     if (et != T_STRUCT && n > 0) { r.err = CRR_DECODE_BAD_TYPE; break; }
-    for (i32 i = 0; i < n; ++i) {
-      read_event(r, e);
+    for (i32 i = 0; i < n && !r.err; ++i) {
+      r.skip(T_STRUCT);
+      ++n_ev;
+    }
+  }
+  return n_ev;
+}
+
+// Events per blob.  thriftrw writes History{10: list<HistoryEvent>} as its only field, so the count is
+// the list header's: 0x59, 0x0F 0x00 0x0A, 0x0C, be32 n (bounded by the bytes after it: a corrupt
+// count must not size the scratch; the decode finds the truncation).  Any other shape, or FULL (the
+// recount after a header was wrong), walks the blob.
+__global__ void blob_head_kernel(crr_blob_batch in, Plan P, int full) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs) return;
+  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
+  u32 n = 0;
+  if (b1 > b0) {
+    Rd r;
+    r.init(in.bytes, b0, b1);
+    const u64 h = r.peek8(b0);
+    const bool canonical = (h & 0xFFFFFFFFFFull) == 0x0C0A000F59ull && b1 - b0 >= 9;
+    if (canonical && !full) {
+      const i64 c = (i32)__builtin_bswap32((u32)(r.peek8(b0 + 5)));
+      const i64 room = (i64)(b1 - b0 - 9);
+      n = c < 0 ? 0u : (u32)(c < room ? c : room);
+    } else if (r.u8_() == 0x59) {
+      n = count_events(r);   // errors are the decode's to report
+    }
+  }
+  P.cnt[bi] = n;
+}
+
+// ---- 3: the decode -----------------------------------------------------------------------------------------
+// One blob, one walk: each event into its canonical slot (history_decode.cpp decode_workflow's loop,
+// host_flatten.h WfFlattener::add's per-type columns); side records and key strings at the event's own
+// slot (wf_pass numbers them within the workflow); a Started event's PrevAutoResetPoints list position
+// in its key slot, the list's length counted per blob.
+__device__ void decode_blob(const crr_blob_batch& in, const Plan& P, u32 bi) {
+  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
+  const u64 NB = (u64)P.n_blobs + 1;
+  u64 x = P.off[0 * NB + bi];
+  const u64 x_end = P.off[0 * NB + bi + 1];
+  u32 n_prev = 0;
+  if (b1 > b0) {
+    Rd r;
+    r.init(in.bytes, b0, b1);
+    if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
+    const i32 new_run = in.wf[P.blob_wf[bi]].new_run_wf;
+    const u64 x_first = x;
+    Event e;
+    u32 ft;
+    i32 fid;
+    while (r.field(ft, fid)) {
+      if (fid != 10 || ft != T_LIST) { r.skip(ft); continue; }
+      const u32 et = r.u8_();
+      const i32 n = r.be32();
       if (r.err) break;
-      const i32 t = e.type;
-      const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
-      const Attr& a = e.a;
-      if (WRITE) {
-        const u64 x = ev_at;
+      if (n < 0) { r.err = CRR_DECODE_TRUNCATED; break; }
+      if (et != T_STRUCT && n > 0) { r.err = CRR_DECODE_BAD_TYPE; break; }
+      for (i32 i = 0; i < n; ++i) {
+        read_event(r, e);
+        if (r.err) break;
+        if (x >= x_end) {   // more events than the header announced: the plan recounts
+          atomicOr(P.flags, 1u);
+          return;
+        }
+        const i32 t = e.type;
+        const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
+        const Attr& a = e.a;
         P.etype[x] = (u8)(valid ? t : CRR_EV_PAD - 1);
         P.id[x] = e.id; P.ver[x] = e.ver; P.ts[x] = e.ts; P.task[x] = e.task;
         i64 ref = 0;
@@ -589,39 +698,17 @@ __device__ void walk_blob(const crr_blob_batch& in, const Plan& P, u32 bi, u32 c
             ss.attempt = a.attempt;
             ss.expiration_ns = a.expiration_ts;
             ss.reserved = 0;
+            // prev_reset_key_off: the blob-local index of the first point until wf_pass adds the blob's
+            // prefix (for an empty list too: where the next point would go, host_flatten.h)
+            ss.prev_reset_key_off = n_prev;
+            ss.prev_reset_count = a.prev_mode == 0 ? a.prev_n : a.prev_mode;
             if (a.prev_mode == 0) {
-              ss.prev_reset_key_off = 0;   // the global reset_keys index, set below
-              ss.prev_reset_count = a.prev_n;
-            } else {
-              ss.prev_reset_key_off = 0;
-              ss.prev_reset_count = a.prev_mode;
+              PrevRef pr;
+              pr.pos = a.prev_pos; pr.n = (u32)a.prev_n; pr.et = a.prev_et;
+              *reinterpret_cast<PrevRef*>(P.keys + x) = pr;
+              n_prev += (u32)a.prev_n;
             }
-            aux = (i32)st_at;          // canonical start-side index (remapped by the layout)
-            if (a.prev_mode == 0) {
-              // the final Points list's strings, in order, as reset-key entries (key_of at add time); the
-              // record holds its first entry's index until fix_start_side_kernel makes it a reset_keys index
-              ss.prev_reset_key_off = (u32)key_at;
-              Rd r2;
-              r2.init(in.bytes, a.prev_pos, r.end);
-              for (i32 k = 0; k < a.prev_n; ++k) {
-                u64 so = 0; u32 sl = 0;
-                if (a.prev_et != T_STRUCT) {
-                  r2.skip(a.prev_et);
-                } else {
-                  for (;;) {
-                    const u32 t2 = r2.u8_();
-                    if (r2.err || t2 == T_STOP) break;
-                    const i32 id2 = r2.be16();
-                    if (id2 == 10 && t2 == T_STRING) r2.str(so, sl);   // the last BinaryChecksum wins
-                    else r2.skip(t2);
-                  }
-                }
-                KeyRef kr;
-                kr.off = so; kr.len = sl; kr.is_reset = 1; kr.dst = 0;
-                P.keys[key_at++] = kr;
-              }
-            }
-            P.start[st_at++] = ss;
+            P.start[x] = ss;
             break;
           }
           case CRR_EV_DECISION_TASK_SCHEDULED: ref = a.ref; aux = a.aux; break;
@@ -634,8 +721,7 @@ __device__ void walk_blob(const crr_blob_batch& in, const Plan& P, u32 bi, u32 c
             as.heartbeat = a.hb; as.has_retry_policy = a.has_retry; as.expiration_interval = a.expiration;
             as.domain_status = domain_status(in, P.dom_table, P.dom_cap, a.dom_off, a.dom_len);
             as.reserved = 0;
-            aux = (i32)act_at;         // canonical activity-side index (remapped by the layout)
-            P.act[act_at++] = as;
+            P.act[x] = as;
             break;
           }
           case CRR_EV_ACTIVITY_TASK_STARTED: case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED:
@@ -657,50 +743,66 @@ __device__ void walk_blob(const crr_blob_batch& in, const Plan& P, u32 bi, u32 c
           case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: aux = new_run; break;
           default: break;
         }
-        if (valid && keyed_type(t)) {
+        if (valid && keyed_type(t)) {   // "" when the attribute is absent (key 0)
           KeyRef kr;
-          kr.off = a.key_off; kr.len = a.key_len; kr.is_reset = 0; kr.dst = x;
-          P.keys[key_at++] = kr;
+          kr.off = a.key_off; kr.len = a.key_len; kr.hash = a.key_len ? r.hash(a.key_off, a.key_len) : 0u;
+          P.keys[x] = kr;
         }
         P.ref[x] = ref;
         P.key[x] = 0;
         P.aux[x] = aux;
-        ++ev_at;
-      } else {
-        ++cnt[0];
-        if (valid && t == CRR_EV_ACTIVITY_TASK_SCHEDULED) ++cnt[1];
-        if (valid && t == CRR_EV_WORKFLOW_EXECUTION_STARTED) {
-          ++cnt[2];
-          if (a.prev_mode == 0) cnt[3] += (u32)a.prev_n;
-        }
-        if (valid && keyed_type(t)) ++cnt[3];
+        ++x;
       }
+      if (r.err) break;
     }
-    if (r.err) break;
+    if (r.err) { record_error(P.err, bi, r.err); return; }
+    if (x > x_first) {   // batch boundaries
+      P.etype[x_first] |= CRR_ETYPE_BATCH_FIRST;
+      P.etype[x - 1] |= CRR_ETYPE_BATCH_LAST;
+    }
   }
-  if (r.err) { record_error(P.err, bi, r.err); return; }
-  if (WRITE && ev_at > ev_first) {   // batch boundaries
-    P.etype[ev_first] |= CRR_ETYPE_BATCH_FIRST;
-    P.etype[ev_at - 1] |= CRR_ETYPE_BATCH_LAST;
-  }
-}
-
-__global__ void blob_count_kernel(crr_blob_batch in, Plan P) {
-  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bi >= in.n_blobs) return;
-  u32 c[kCnt];
-  walk_blob<false>(in, P, bi, c);
-  for (int k = 0; k < kCnt; ++k) P.cnt[k * P.n_blobs + bi] = c[k];
+  if (x != x_end) atomicOr(P.flags, 1u);   // fewer events than the header announced: recount
+  P.cnt[1 * (u64)P.n_blobs + bi] = n_prev;
 }
 
 __global__ void blob_decode_kernel(crr_blob_batch in, Plan P) {
   const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= in.n_blobs) return;
-  const u64 NB = P.n_blobs + 1;
-  if (P.off[0 * NB + P.n_blobs] > P.max_events || P.off[3 * NB + P.n_blobs] > 2 * P.max_events || *P.err != ~0ull)
-    return;   // the summary reports it (error, or scratch too small)
-  u32 c[kCnt];
-  walk_blob<true>(in, P, bi, c);
+  const u64 NB = (u64)P.n_blobs + 1;
+  if (P.off[0 * NB + P.n_blobs] > P.max_events) return;   // the summary reports it
+  decode_blob(in, P, bi);
+}
+
+// ---- 4: previous reset points at their reset_keys positions ------------------------------------------------
+__global__ void reset_refs_kernel(crr_blob_batch in, Plan P) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs || !plan_ok(P)) return;
+  const u64 NB = (u64)P.n_blobs + 1;
+  if (P.cnt[1 * (u64)P.n_blobs + bi] == 0) return;
+  u64 k = P.off[1 * NB + bi];
+  for (u64 x = P.off[0 * NB + bi]; x < P.off[0 * NB + bi + 1]; ++x) {
+    if ((P.etype[x] & CRR_ETYPE_MASK) != CRR_EV_WORKFLOW_EXECUTION_STARTED || P.start[x].prev_reset_count <= 0) continue;
+    const PrevRef pr = *reinterpret_cast<const PrevRef*>(P.keys + x);
+    Rd r;
+    r.init(in.bytes, pr.pos, in.blob_off[bi + 1]);
+    for (u32 i = 0; i < pr.n; ++i) {   // read_reset_points: the last BinaryChecksum of each element
+      u64 so = 0;
+      u32 sl = 0;
+      if (pr.et != T_STRUCT) {
+        r.skip(pr.et);
+      } else {
+        u32 t2;
+        i32 id2;
+        while (r.field(t2, id2)) {
+          if (id2 == 10 && t2 == T_STRING) r.str(so, sl);
+          else r.skip(t2);
+        }
+      }
+      KeyRef kr;
+      kr.off = so; kr.len = sl; kr.hash = sl ? r.hash(so, sl) : 0u;
+      P.resets[k++] = kr;
+    }
+  }
 }
 
 // ---- 3: exclusive prefixes over K arrays of m u32 / u64 values (reduce, scan the tile sums, apply) --------
@@ -800,6 +902,18 @@ __device__ __forceinline__ u32 pow2_at_least(u32 x) {
 constexpr u64 kInserted = 1ull << 62, kDeleteSeen = 1ull << 61;
 constexpr u64 kMask40 = (1ull << 40) - 1;
 
+__device__ __forceinline__ bool same_bytes(const u8* b, u64 x, u64 y, u32 len) {
+  Rd rx, ry;
+  rx.init(b, x, x + len);
+  ry.init(b, y, y + len);
+  for (u32 i = 0; i < len; i += 8) {
+    const u32 m = len - i < 8 ? len - i : 8;
+    const u64 mask = m == 8 ? ~0ull : ((1ull << (8 * m)) - 1);
+    if ((rx.peek8(x + i) ^ ry.peek8(y + i)) & mask) return false;
+  }
+  return true;
+}
+
 __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= in.n_wf || !plan_ok(P)) return;
@@ -807,48 +921,38 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u32 bb = src.blob_begin, be = src.blob_begin + src.blob_count;
   const u64 NB = P.n_blobs + 1;
   const u64 e0 = P.off[0 * NB + bb], e1 = P.off[0 * NB + be];
-  const u64 k0 = P.off[3 * NB + bb], k1 = P.off[3 * NB + be];
+  const u64 r0 = P.off[1 * NB + bb], r1 = P.off[1 * NB + be];
   const u32 n = (u32)(e1 - e0);
-  const u32 nk = (u32)(k1 - k0);
-  // this workflow's scratch table: [tbase, tbase + cap) u64 words (+ cap u32 key ids after the bounds use)
-  const u64 tbase = 4 * e0 + 4 * k0 + 64ull * w;
+  const u32 nr = (u32)(r1 - r0);
+  // this workflow's scratch table: 4 * (events + reset points) + 64 u64 words from its own base
+  const u64 tbase = 4 * e0 + 4 * r0 + 64ull * w;
   u64* tab = P.table + tbase;
-  const u32 cap_i = pow2_at_least(2 * nk + 2);
+  const u32 cap_i = pow2_at_least(2 * (n + nr) + 2);
+  for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
 
-  // -- interning (WfFlattener::key_of: "" is key 0, new strings get 1, 2, ... in first-seen order) --
-  {
-    for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
-    u32 next = 1;
-    for (u64 j = k0; j < k1; ++j) {
-      const KeyRef kr = P.keys[j];
-      u32 id = 0;
-      if (kr.len > 0) {
-        const u32 h = fnv1a(in.bytes, kr.off, kr.len);
-        u32 slot = h & (cap_i - 1);
-        for (;;) {
-          const u64 ent = tab[slot];
-          if (ent == 0) {                       // a new string: the next id
-            id = next++;
-            tab[slot] = ((u64)h << 32) | (u64)(j - k0 + 1);
-            break;
-          }
-          if ((u32)(ent >> 32) == h) {          // same hash: compare the bytes
-            const u64 jo = k0 + (u32)ent - 1;
-            const KeyRef other = P.keys[jo];
-            if (other.len == kr.len && bytes_equal(in.bytes, kr.off, in.bytes, other.off, kr.len)) {
-              id = P.entry_id[jo];
-              break;
-            }
-          }
-          slot = (slot + 1) & (cap_i - 1);
-        }
+  // One pass over the events in order: interning (WfFlattener::key_of: "" is key 0, new strings get 1, 2,
+  // ... in first-seen order; a Started event's previous reset points before anything after it), the
+  // side-record ordinals, capacities, VH items, tasks (WfFlattener::add / batch_end / finish).
+  // Table entries: (hash << 32) | (entry + 1), entry = event index (keys) or n + reset index (resets).
+  u32 next_key = 1;
+  auto intern = [&](const KeyRef& kr, u32 entry) -> u32 {
+    if (kr.len == 0) return 0u;
+    u32 slot = kr.hash & (cap_i - 1);
+    for (;;) {
+      const u64 ent = tab[slot];
+      if (ent == 0) {
+        tab[slot] = ((u64)kr.hash << 32) | (u64)(entry + 1);
+        return next_key++;
       }
-      P.entry_id[j] = id;
-      if (kr.is_reset == 0) P.key[kr.dst] = id;
+      if ((u32)(ent >> 32) == kr.hash) {
+        const u32 o = (u32)ent - 1;
+        const KeyRef other = o < n ? P.keys[e0 + o] : P.resets[r0 + (o - n)];
+        if (other.len == kr.len && same_bytes(in.bytes, kr.off, other.off, kr.len))
+          return o < n ? P.key[e0 + o] : P.reset_ids[r0 + (o - n)];
+      }
+      slot = (slot + 1) & (cap_i - 1);
     }
-  }
-
-  // -- capacities, VH items, tasks (WfFlattener::add / batch_end / finish) --
+  };
   i32 n_act = 0, n_timer = 0, n_child = 0, n_rc = 0, n_sig = 0, n_dtc = 0, n_started = 0, vh = 0, tasks = 0;
   i32 max_prev = 0;
   i32 empty_at = -1;
@@ -857,27 +961,37 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
     i64 last_ver = 0;
     u64 x = e0;
     for (u32 b = bb; b < be; ++b) {
-      const u64 be_ = P.off[0 * NB + b + 1];
-      if (be_ == x) {   // an empty batch
+      const u64 bx1 = P.off[0 * NB + b + 1];
+      if (bx1 == x) {   // an empty batch
         if (empty_at < 0) empty_at = (i32)(x - e0);
         continue;
       }
       tasks += 2;
-      for (; x < be_; ++x) {
+      const u64 rb = P.off[1 * NB + b];
+      for (; x < bx1; ++x) {
         const u32 t = P.etype[x] & CRR_ETYPE_MASK;
         const i64 v = P.ver[x];
         if (!have_ver || v > last_ver) { ++vh; last_ver = v; have_ver = true; }
         if (t < CRR_EV_TYPE_COUNT) tasks += kTasksPerEvent[t];
         switch (t) {
           case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
-            ++n_started;
-            const i32 pc = P.start[P.aux[x]].prev_reset_count;
+            crr_start_side& ss = P.start[x];
+            const i32 pc = ss.prev_reset_count;
+            if (pc >= 0) {
+              const u64 g = rb + ss.prev_reset_key_off;   // the blob-local index made global
+              ss.prev_reset_key_off = (u32)g;
+              for (i32 k = 0; k < pc; ++k) P.reset_ids[g + k] = intern(P.resets[g + k], n + (u32)(g + k - r0));
+            }
             if (pc > max_prev) max_prev = pc;
+            P.aux[x] = n_started++;
             break;
           }
-          case CRR_EV_DECISION_TASK_COMPLETED: ++n_dtc; break;
-          case CRR_EV_ACTIVITY_TASK_SCHEDULED: ++n_act; break;
-          case CRR_EV_TIMER_STARTED: ++n_timer; break;
+          case CRR_EV_DECISION_TASK_COMPLETED: ++n_dtc; P.key[x] = intern(P.keys[x], (u32)(x - e0)); break;
+          case CRR_EV_ACTIVITY_TASK_SCHEDULED: P.key[x] = intern(P.keys[x], (u32)(x - e0)); P.aux[x] = n_act++; break;
+          case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED: case CRR_EV_TIMER_FIRED: case CRR_EV_TIMER_CANCELED:
+            P.key[x] = intern(P.keys[x], (u32)(x - e0));
+            break;
+          case CRR_EV_TIMER_STARTED: ++n_timer; P.key[x] = intern(P.keys[x], (u32)(x - e0)); break;
           case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: ++n_child; break;
           case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED: ++n_rc; break;
           case CRR_EV_SIGNAL_EXTERNAL_INITIATED: ++n_sig; break;
@@ -894,7 +1008,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   i32 bound[kMaps] = {0, 0, 0, 0, 0, 0};
   bool compact_ok = n <= (u32)kCompactMaxEvents;
   {
-    const u32 cap_b = pow2_at_least(2 * n + 2);
+    const u32 cap_b = pow2_at_least(2 * n + 2);   // <= the interning table's region
     for (u32 i = 0; i < cap_b; ++i) tab[i] = 0;
     auto map_of = [](u32 t, int& dir) -> int {
       dir = 0;
@@ -1067,21 +1181,18 @@ __global__ void summary_kernel(Plan P, u32 n_lane, u32 n_groups, u32 n_tail, crr
     S->err_blob = (i64)(e >> 8);
   }
   S->n_events = P.off[0 * NB + P.n_blobs];
-  const u64 n_keys = P.off[3 * NB + P.n_blobs];
-  if (S->err == 0 && (S->n_events > P.max_events || n_keys > 2 * P.max_events)) S->err = kErrScratch;
+  if (S->err == 0 && (S->n_events > P.max_events || P.off[1 * NB + P.n_blobs] > P.max_events)) S->err = kErrScratch;
   S->n_wf = P.n_wf;
   if (S->err) return;   // nothing past the decode is valid
   auto gtot = [&](int k) { return P.gpre[(u64)k * (n_groups + 1) + n_groups]; };
   auto ttot = [&](int k) { return P.tpre[(u64)k * (n_tail + 1) + n_tail]; };
   S->n_slots = gtot(GV_LEN) + ttot(GV_LEN);
   for (int t = 0; t < 8; ++t) S->table_rows[t] = gtot(GV_CAP0 + t) + ttot(GV_CAP0 + t);
-  const u64 n_act = P.off[1 * NB + P.n_blobs], n_start = P.off[2 * NB + P.n_blobs];
-  const u64 as = gtot(GV_ACT_SIDE) + ttot(GV_ACT_SIDE), ss = gtot(GV_START_SIDE) + ttot(GV_START_SIDE);
   // _interleave_side keeps the canonical array when no event references it (the 1-record placeholder)
-  S->n_act_side = n_act ? (as > 0 ? as : 1) : 1;
-  S->n_start_side = n_start ? (ss > 0 ? ss : 1) : 1;
-  const u64 n_reset = P.reset_pos[2 * P.max_events];   // the exclusive prefix's total
-  S->n_reset_keys = n_reset ? n_reset : 1;               // flatten's [0] placeholder when there are none
+  const u64 as = gtot(GV_ACT_SIDE) + ttot(GV_ACT_SIDE), ss = gtot(GV_START_SIDE) + ttot(GV_START_SIDE);
+  S->n_act_side = as > 0 ? as : 1;
+  S->n_start_side = ss > 0 ? ss : 1;
+  S->n_reset_keys = P.off[1 * NB + P.n_blobs];   // (0: the caller's buffer holds flatten's [0] placeholder)
   S->arena_bytes = P.arena_off[P.n_wf];
   S->n_wf = P.n_wf;
   S->wave_begin = n_lane;
@@ -1127,20 +1238,17 @@ __device__ __forceinline__ void put_slot(const crr_blob_batch& in, const Plan& P
     return;
   }
   const u64 NB = P.n_blobs + 1;
-  const u32 bb = in.wf[w].blob_begin;
-  const u64 x = P.off[0 * NB + bb] + (u64)k;
+  const u64 x = P.off[0 * NB + in.wf[w].blob_begin] + (u64)k;
   const u8 e = P.etype[x];
   const u32 t = e & CRR_ETYPE_MASK;
   i32 a = P.aux[x];
-  if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {
-    const u64 ord = (u64)a - P.off[1 * NB + bb];
-    const u64 ni = side_act_base + ord * side_stride + lane;
-    D.act[ni] = P.act[a];
+  if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {   // aux: the record's ordinal in the workflow (wf_pass)
+    const u64 ni = side_act_base + (u64)a * side_stride + lane;
+    D.act[ni] = P.act[x];
     a = (i32)ni;
   } else if (t == CRR_EV_WORKFLOW_EXECUTION_STARTED) {
-    const u64 ord = (u64)a - P.off[2 * NB + bb];
-    const u64 ni = side_start_base + ord * side_stride + lane;
-    D.start[ni] = P.start[a];
+    const u64 ni = side_start_base + (u64)a * side_stride + lane;
+    D.start[ni] = P.start[x];
     a = (i32)ni;
   } else if (t == CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW && a >= 0 && (u32)a < P.n_wf) {
     a = (i32)P.inv[a];   // the new-run history's device position
@@ -1246,29 +1354,6 @@ __global__ void layout_wf_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u
     for (u32 i = 0; i < s.final_token_len; ++i) put(in.strings[s.final_token_off + i]);
 }
 
-// the reset-point entries among the key entries (scan input), bounded by the device-side entry count
-__global__ void reset_flags_kernel(Plan P, u64 cap) {
-  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cap) return;
-  const u64 n_keys = plan_ok(P) ? P.off[3 * ((u64)P.n_blobs + 1) + P.n_blobs] : 0;
-  P.reset_flag[j] = j < n_keys ? P.keys[j].is_reset : 0u;
-}
-// start side records: prev_reset_key_off = the reset_keys index of the record's first point (for an
-// empty list, where the next point would go: host_flatten.h uses reset_keys.size())
-__global__ void fix_start_side_kernel(Plan P) {
-  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (!plan_ok(P) || i >= P.off[2 * ((u64)P.n_blobs + 1) + P.n_blobs]) return;
-  crr_start_side& s = P.start[i];
-  if (s.prev_reset_count >= 0) s.prev_reset_key_off = (u32)P.reset_pos[s.prev_reset_key_off];
-}
-// reset_keys (canonical order): the interned ids of the reset-point entries, in entry order
-__global__ void layout_reset_keys_kernel(Plan P, u32* dst, u64 cap) {
-  const u64 j = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= cap) return;
-  const u64 n_keys = P.off[3 * ((u64)P.n_blobs + 1) + P.n_blobs];
-  if (j < n_keys && P.keys[j].is_reset) dst[P.reset_pos[j]] = P.entry_id[j];
-}
-
 }  // namespace crr_ingest
 
 // ---- C ABI ----------------------------------------------------------------------------------------------------
@@ -1281,8 +1366,14 @@ struct Carved {
   crr_ingest_summary* S_dev;
 };
 
+size_t sort_tmp_bytes(uint32_t n_wf) {   // hipCUB's radix-sort scratch for n_wf keys
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (int)(n_wf ? n_wf : 1));
+  return tmp;
+}
+
 // The scratch layout for a max_events capacity; both calls carve it the same way from scratch_bytes.
-Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events) {
+Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events, size_t sort_tmp) {
   Carved c{};
   const uintptr_t at = reinterpret_cast<uintptr_t>(scratch);
   size_t used = 0;
@@ -1299,31 +1390,27 @@ Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events
   const u64 NB = (u64)n_blobs + 1;
   const u64 NW = n_wf ? n_wf : 1;
   P.blob_wf = (u32*)take(4 * NB);
-  P.cnt = (u32*)take(4 * kCnt * NB);
-  P.off = (u64*)take(8 * kCnt * NB);
+  P.cnt = (u32*)take(4 * 2 * NB);
+  P.off = (u64*)take(8 * 2 * NB);
   P.err = (u64*)take(8);
-  u64 max_m = 2 * E;
-  if (NB > max_m) max_m = NB;
-  if (NW + 1 > max_m) max_m = NW + 1;
+  P.flags = (u32*)take(4);
+  u64 max_m = NB > NW + 1 ? NB : NW + 1;
   P.tile = (u64*)take(8 * ((max_m + kTile - 1) / kTile + 1) * kGeo);
   P.etype = (u8*)take(E);
   P.id = (i64*)take(8 * E); P.ver = (i64*)take(8 * E); P.ts = (i64*)take(8 * E); P.task = (i64*)take(8 * E);
   P.ref = (i64*)take(8 * E); P.key = (u32*)take(4 * E); P.aux = (i32*)take(4 * E);
   P.act = (crr_activity_side*)take(sizeof(crr_activity_side) * E);
   P.start = (crr_start_side*)take(sizeof(crr_start_side) * E);
-  P.keys = (KeyRef*)take(sizeof(KeyRef) * 2 * E);
-  P.entry_id = (u32*)take(4 * 2 * E);
-  P.reset_flag = (u32*)take(4 * 2 * E);
-  P.reset_pos = (u64*)take(8 * (2 * E + 1));
-  // per-workflow hash tables: a workflow of n events and k key entries uses <= 4n + 4k + 64 words
-  P.table = (u64*)take(8 * (4 * E + 4 * 2 * E + 64 * NW));
+  P.keys = (KeyRef*)take(sizeof(KeyRef) * E);
+  P.resets = (KeyRef*)take(sizeof(KeyRef) * E);
+  P.reset_ids = (u32*)take(4 * E);
+  // per-workflow hash tables: a workflow of n events and r reset points uses <= 4n + 4r + 64 words
+  P.table = (u64*)take(8 * (8 * E + 64 * NW));
   P.wf_info = (i32*)take(4 * kWfInfo * NW);
   P.sort_in = (u64*)take(8 * NW);
   P.sort_out = (u64*)take(8 * NW);
-  size_t tmp = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, (const u64*)nullptr, (u64*)nullptr, (int)NW);
-  P.sort_tmp_bytes = tmp;
-  P.sort_tmp = take(tmp);
+  P.sort_tmp_bytes = sort_tmp;
+  P.sort_tmp = take(sort_tmp);
   P.perm = (u32*)take(4 * NW);
   P.inv = (u32*)take(4 * NW);
   P.arena_off = (u64*)take(8 * (NW + 1));
@@ -1340,13 +1427,13 @@ Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events
   return c;
 }
 
-uint64_t max_events_of(size_t scratch_bytes, uint32_t n_blobs, uint32_t n_wf) {
+uint64_t max_events_of(size_t scratch_bytes, uint32_t n_blobs, uint32_t n_wf, size_t sort_tmp) {
   // the largest capacity whose carve fits (the size is monotone in it)
   uint64_t lo = 0, hi = 1;
-  while (carve(nullptr, n_blobs, n_wf, hi).bytes <= scratch_bytes && hi < (1ull << 40)) hi <<= 1;
+  while (carve(nullptr, n_blobs, n_wf, hi, sort_tmp).bytes <= scratch_bytes && hi < (1ull << 40)) hi <<= 1;
   while (lo + 1 < hi) {
     const uint64_t mid = (lo + hi) / 2;
-    if (carve(nullptr, n_blobs, n_wf, mid).bytes <= scratch_bytes) lo = mid; else hi = mid;
+    if (carve(nullptr, n_blobs, n_wf, mid, sort_tmp).bytes <= scratch_bytes) lo = mid; else hi = mid;
   }
   return lo;
 }
@@ -1368,7 +1455,7 @@ bool valid_batch(const crr_blob_batch* in) {
 extern "C" {
 
 size_t crr_ingest_scratch_bytes(uint32_t n_blobs, uint32_t n_wf, uint64_t max_events) {
-  return carve(nullptr, n_blobs, n_wf, max_events).bytes;
+  return carve(nullptr, n_blobs, n_wf, max_events, sort_tmp_bytes(n_wf)).bytes;
 }
 
 int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, crr_ingest_summary* summary,
@@ -1376,13 +1463,13 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   if (!valid_batch(in) || !scratch || !summary) return -1;
   if (in->n_wf == 0 && in->n_blobs > 0) return -1;   // blobs no workflow owns
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf);
+  const size_t stmp = sort_tmp_bytes(in->n_wf);
+  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf, stmp);
   if (max_events == 0) return -1;
-  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events);
+  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events, stmp);
   Plan P = c.P;
   const u32 nb = in->n_blobs, nw = in->n_wf;
   const u64 NB = (u64)nb + 1;
-  const u64 E2 = 2 * max_events;
   u32 dom_cap = 0;
   if (in->n_domains != 0xFFFFFFFFu && in->n_domains) {
     dom_cap = 16;
@@ -1391,21 +1478,32 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   P.dom_cap = dom_cap;
   hipError_t e;
   if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(P.counters, 0, 4 * 16, s)) != hipSuccess) return (int)e;
   if (dom_cap) {
     if ((e = hipMemsetAsync(P.dom_table, 0, 4 * (size_t)dom_cap, s)) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(domains_build_kernel, dim3((in->n_domains + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in,
                        P.dom_table, dom_cap);
   }
-  // A: decode, per-workflow pass, device order, reset-key positions
-  if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
-  if (nb) hipLaunchKernelGGL(blob_count_kernel, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
-  multi_scan<u32>(P.cnt, nb, nb, kCnt, P.tile, P.off, NB, s);
-  if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
-  hipLaunchKernelGGL(reset_flags_kernel, dim3((unsigned)((E2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P, E2);
-  multi_scan<u32>(P.reset_flag, E2, (u32)E2, 1, P.tile, P.reset_pos, E2 + 1, s);
-  hipLaunchKernelGGL(fix_start_side_kernel, dim3((unsigned)((max_events + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P);
-  if (nw) hipLaunchKernelGGL(wf_pass_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P);
+  const unsigned gb = (nb + kBlock - 1) / kBlock, gw = (nw + kBlock - 1) / kBlock;
+  // A: event counts, the decode, reset points, the per-workflow pass, the device order
+  if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
+  for (int full = 0; full < 2; ++full) {
+    if (nb) hipLaunchKernelGGL(blob_head_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P, full);
+    multi_scan<u32>(P.cnt, nb, nb, 1, P.tile, P.off, NB, s);
+    if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
+    if (full) break;
+    // a header count that was wrong (hand-made blobs): count by walking every blob, then decode again
+    u32 flags = 0;
+    if ((e = hipMemcpyAsync(&flags, P.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
+    if (!flags) break;
+    if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
+  }
+  multi_scan<u32>(P.cnt + nb, nb, nb, 1, P.tile, P.off + NB, NB, s);   // previous reset points per blob
+  if (nb) hipLaunchKernelGGL(reset_refs_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
+  if (nw) hipLaunchKernelGGL(wf_pass_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P);
   multi_scan<u64>(P.arena_off, nw, nw, 1, P.tile, P.arena_off, (u64)nw + 1, s);
   if (nw) {
     size_t tmp = P.sort_tmp_bytes;
@@ -1415,14 +1513,16 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   if ((e = hipGetLastError()) != hipSuccess) return (int)e;
   // the lane / tail split sizes the geometry launches
   u32 n_lane = 0;
-  u64 err = 0;
+  u64 err = 0, n_events = 0, n_resets = 0;
   if ((e = hipMemcpyAsync(&n_lane, P.counters + C_N_LANE, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
   if ((e = hipMemcpyAsync(&err, P.err, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemcpyAsync(&n_events, P.off + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+  if ((e = hipMemcpyAsync(&n_resets, P.off + NB + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
-  const bool failed = err != ~0ull || n_lane > nw;
+  const bool failed = err != ~0ull || n_lane > nw || n_events > max_events || n_resets > max_events;
   const u32 n_groups = failed ? 0 : (n_lane + 63) / 64, n_tail = failed ? 0 : nw - n_lane;
   // B: geometry and the summary (after a failed decode only the error and the counts)
-  if (nw && !failed) hipLaunchKernelGGL(positions_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, P, n_lane);
+  if (nw && !failed) hipLaunchKernelGGL(positions_kernel, dim3(gw), dim3(kBlock), 0, s, P, n_lane);
   if (n_groups) hipLaunchKernelGGL(group_max_kernel, dim3((n_groups + 3) / 4), dim3(256), 0, s, P, n_lane, n_groups);
   if (!failed) {
     multi_scan<u64>(P.gvals, n_groups, n_groups, kGeo, P.tile, P.gpre, (u64)n_groups + 1, s);
@@ -1443,8 +1543,9 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
   const crr_events& ev = dst->ev;
   if (!ev.etype || !ev.event_id || !ev.version || !ev.timestamp || !ev.task_id || !ev.ref || !ev.key || !ev.aux) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf);
-  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events);
+  const size_t stmp = sort_tmp_bytes(in->n_wf);
+  const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf, stmp);
+  Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events, stmp);
   Plan P = c.P;
   const u32 nw = in->n_wf, n_lane = S->wave_begin, n_groups = (n_lane + 63) / 64, n_tail = nw - n_lane;
   Dst D;
@@ -1455,20 +1556,18 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
   D.arena = const_cast<u8*>(dst->arena);
   D.wf = const_cast<crr_workflow*>(dst->wf);
   hipError_t e;
-  // side records not referenced by any event stay zero, like flatten's zero-filled arrays
+  // side records no event references stay zero, like flatten's zero-filled arrays
   if ((e = hipMemsetAsync(D.act, 0, S->n_act_side * sizeof(crr_activity_side), s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(D.start, 0, S->n_start_side * sizeof(crr_start_side), s)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(D.reset_keys, 0, S->n_reset_keys * 4, s)) != hipSuccess) return (int)e;
-  if (S->n_act_side == 1 || S->n_start_side == 1) {
-    // no event references the array: it is the canonical one (the placeholder or the lone record)
-  }
   if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups);
   if (n_tail) hipLaunchKernelGGL(layout_tail_kernel, dim3(n_tail), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups, n_tail);
   if (nw) hipLaunchKernelGGL(layout_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P, D, n_lane,
                              n_groups, n_tail);
-  const u64 E2 = 2 * max_events;
-  hipLaunchKernelGGL(layout_reset_keys_kernel, dim3((unsigned)((E2 + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, P,
-                     D.reset_keys, E2);
+  // reset_keys: the interned previous reset points in canonical order ([0] when there are none)
+  if ((e = hipMemsetAsync(D.reset_keys, 0, 4, s)) != hipSuccess) return (int)e;
+  if (S->n_reset_keys &&
+      (e = hipMemcpyAsync(D.reset_keys, P.reset_ids, 4 * S->n_reset_keys, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return (int)e;
   if (perm && nw && (e = hipMemcpyAsync(perm, P.perm, 4ull * nw, hipMemcpyDeviceToDevice, s)) != hipSuccess) return (int)e;
   return (int)hipGetLastError();
 }

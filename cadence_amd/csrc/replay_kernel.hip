@@ -1162,8 +1162,12 @@ struct CTier {
   static constexpr int LANES = LANES_;
 };
 // activity flag word: row bits (LIVE, MAPPED, CANCEL_REQUESTED, HAS_RETRY) + LF_STARTED / LF_HB_VIS,
-// TimerTaskStatus << 8, the cached candidate's timer type << 12
+// TimerTaskStatus << 8, the cached candidate's timer type << 12, the scheduled event's offset in its
+// batch << 16 (ScheduledEventBatchID = its ID - that offset)
 constexpr int CF_CAND_SHIFT = 12;
+constexpr int CF_BATCH_SHIFT = 16;       // activity: 10 bits; request-cancel / signal: bits 18.. (10 bits)
+constexpr int CHILD_BATCH_SHIFT = 1;     // child: bits 1-7, 127 = "walk back to the batch's first event"
+constexpr u32 kChildBatchNone = 127u;
 // step fields: 10 bits each
 constexpr u32 kStepBits = 10, kStepMask = (1u << kStepBits) - 1u;
 constexpr i32 kMaxCompactSteps = (1 << kStepBits) - 1;  // step kStepMask encodes "none"
@@ -1265,14 +1269,14 @@ struct CompactTables {
   // slots finds the entry an operation addresses and the first free slot, then the operation's writes.
   __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 bfid,
                                         const crr_activity_side& as) {
-    return map_op_unified(L, G, op, ev, s, as);
+    return map_op_unified(L, G, op, ev, s, bfid, as);
   }
   // One code path for every map operation, so a divergent wavefront (lanes with different event types)
   // runs one slot scan and one write-back per step instead of one per map and operation: each lane
   // picks its map's flag and lookup words (LDS addresses), lookup value and slot count, and the
   // operations differ only in the words they write.  Same results as act_op / timer_op / child_op /
   // init_op (the per-map forms, CRR_COMPACT_UNIFIED=0).
-  __device__ __forceinline__ int map_op_unified(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s,
+  __device__ __forceinline__ int map_op_unified(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 bfid,
                                                 const crr_activity_side& as) {
     const bool is_act = op <= MOP_ACT_CANCEL;
     const bool is_timer = op == MOP_TIMER_START || op == MOP_TIMER_DELETE;
@@ -1341,14 +1345,21 @@ struct CompactTables {
       } else if (grow && j >= cap) {
         rc = CRR_ERR_CAPACITY;
       } else {
-        u32 nf = CRR_ROW_LIVE | ((u32)s << 8) | (is_child ? (kStepMask << (8 + kStepBits)) : 0u);
+        // the event's offset in its batch (IDs are consecutive: insert_ok), so the rows' batch IDs need no
+        // walk back over the columns at the end
+        const u64 bdelta = (u64)ev.id - (u64)bfid;
+        const u32 bd = bdelta < (u64)kStepMask ? (u32)bdelta : kStepMask;
+        u32 nf = CRR_ROW_LIVE | ((u32)s << 8) |
+                 (is_child ? (kStepMask << (8 + kStepBits)) | ((bd < kChildBatchNone ? bd : kChildBatchNone) << CHILD_BATCH_SHIFT)
+                           : (bd << (8 + kStepBits)));
         if (is_act) {
           if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
           // not started: ScheduleToClose and ScheduleToStart
           i64 ct = add_seconds(ev.ts, as.schedule_to_close);
           i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
           cand_min(ct, cy, add_seconds(ev.ts, as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
-          nf = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u) | ((u32)cy << CF_CAND_SHIFT);
+          nf = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u) | ((u32)cy << CF_CAND_SHIFT) |
+               (bd << CF_BATCH_SHIFT);
           M->a_key[j][t] = ev.key;
           M->a_src[j][t] = (u32)s | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
           M->a_cand[j][t] = ct;
@@ -1361,14 +1372,19 @@ struct CompactTables {
       }
     } else if (op == MOP_ACT_START) {  // :2254-2276
       rc = CRR_ERR_MISSING_ACTIVITY_INFO;
-      if (hit >= 0) rc = act_started(hit, ev, s);
+      // the rows keep only steps: a StartedID must be id0 + its step too (else the general path)
+      if (hit >= 0) rc = ev.id != id_at((u32)s) ? CRR_INTERNAL_RETRY : act_started(hit, ev, s);
     } else if (op == MOP_CHILD_START) {  // :3485-3507
       rc = CRR_ERR_MISSING_CHILD_INFO;
-      if (hit >= 0) {
+      if (hit >= 0 && ev.id != id_at((u32)s)) {
+        rc = CRR_INTERNAL_RETRY;
+      } else if (hit >= 0) {
         const u32 f = fl[hit * LANES];
         fl[hit * LANES] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
         rc = CRR_OK;
       }
+    } else if (hit >= 0 && ev.id != id_at((u32)s)) {  // MOP_ACT_CANCEL: CancelRequestID = id0 + step
+      rc = CRR_INTERNAL_RETRY;
     } else if (hit >= 0) {  // MOP_ACT_CANCEL (:2444-2467)
       M->a_fl[hit][t] |= CRR_ROW_CANCEL_REQUESTED;
       const u32 w = M->a_src[hit][t];
@@ -1518,6 +1534,10 @@ struct CompactTables {
     sort_slots<R_SLOTS>(M->r_fl, L.n_rc, [&](int j) { return (M->r_fl[j][t] >> 8) & kStepMask; }, [&](int, int) {});
     sort_slots<S_SLOTS>(M->s_fl, L.n_sig, [&](int j) { return (M->s_fl[j][t] >> 8) & kStepMask; }, [&](int, int) {});
 
+    // Row fields come from the arena and the step arithmetic of consecutive IDs (an entry's event ID is
+    // id0 + its step, checked when it was inserted / started / cancel-requested); the version of an event
+    // from the version history (one item: every event's; else the item covering its ID).  Only the
+    // activities' timestamps and side records are read back from the columns.
     for (i32 i = 0; i < L.n_act; ++i) {  // ReplicateActivityTask{Scheduled,Started,CancelRequested} images
       const u32 f = M->a_fl[i][t];
       const u32 w = M->a_src[i][t];
@@ -1527,12 +1547,12 @@ struct CompactTables {
       const crr_activity_side as = in->act_side[in->ev.aux[ix(ss)]];
       crr_activity_row r;
       r.schedule_id = id_at((u32)ss);
-      r.version = ev_ver(max(ss, max(started ? st : -1, cancel ? sc : -1)));  // last of Scheduled / Started / CancelRequested
-      r.scheduled_batch_id = batch_first_id(ss);
+      r.version = ver_of(L, G, max(ss, max(started ? st : -1, cancel ? sc : -1)));  // last of Scheduled / Started / CancelRequested
+      r.scheduled_batch_id = r.schedule_id - (i64)((f >> CF_BATCH_SHIFT) & kStepMask);
       r.scheduled_time = ev_ts(ss);
-      r.started_id = started ? ev_id(st) : CRR_EMPTY_EVENT_ID;
+      r.started_id = started ? id_at((u32)st) : CRR_EMPTY_EVENT_ID;
       r.started_time = started ? ev_ts(st) : CRR_ZERO_TIME;
-      r.cancel_request_id = cancel ? ev_id(sc) : CRR_EMPTY_EVENT_ID;
+      r.cancel_request_id = cancel ? id_at((u32)sc) : CRR_EMPTY_EVENT_ID;
       r.last_hb_timeout_vis_s = (f & LF_HB_VIS) ? unix_seconds(add_seconds(r.started_time, as.heartbeat)) : 0;
       r.sched_src = ss;
       r.started_src = started ? st : -1;
@@ -1550,7 +1570,7 @@ struct CompactTables {
       const i32 src = (i32)((f >> 8) & kStepMask);
       crr_timer_row r;
       r.started_id = id_at((u32)src);
-      r.version = ev_ver(src);
+      r.version = ver_of(L, G, src);
       r.expiry_time = M->t_exp[i][t];
       r.task_status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
       r.key = M->t_key[i][t];
@@ -1561,12 +1581,13 @@ struct CompactTables {
     for (i32 i = 0; i < L.n_child; ++i) {
       const u32 f = M->c_fl[i][t];
       const i32 src = (i32)((f >> 8) & kStepMask), sst = (i32)((f >> (8 + kStepBits)) & kStepMask);
+      const u32 bd = (f >> CHILD_BATCH_SHIFT) & kChildBatchNone;
       const bool started = sst != (i32)kStepMask;
       crr_child_row r;
       r.initiated_id = id_at((u32)src);
-      r.version = ev_ver(src);
-      r.initiated_batch_id = batch_first_id(src);
-      r.started_id = started ? ev_id(sst) : CRR_EMPTY_EVENT_ID;
+      r.version = ver_of(L, G, src);
+      r.initiated_batch_id = bd != kChildBatchNone ? r.initiated_id - (i64)bd : batch_first_id(src);
+      r.started_id = started ? id_at((u32)sst) : CRR_EMPTY_EVENT_ID;
       r.src = src;
       r.started_src = started ? sst : -1;
       r.flags = CRR_ROW_LIVE;
@@ -1574,25 +1595,38 @@ struct CompactTables {
       *G.child(i) = r;
     }
     for (i32 i = 0; i < L.n_rc; ++i) {
-      const i32 src = (i32)((M->r_fl[i][t] >> 8) & kStepMask);
+      const u32 f = M->r_fl[i][t];
+      const i32 src = (i32)((f >> 8) & kStepMask);
       crr_initiated_row r;
       r.initiated_id = id_at((u32)src);
-      r.version = ev_ver(src);
-      r.initiated_batch_id = batch_first_id(src);
+      r.version = ver_of(L, G, src);
+      r.initiated_batch_id = r.initiated_id - (i64)((f >> (8 + kStepBits)) & kStepMask);
       r.src = src;
       r.flags = CRR_ROW_LIVE;
       *G.rc(i) = r;
     }
     for (i32 i = 0; i < L.n_sig; ++i) {
-      const i32 src = (i32)((M->s_fl[i][t] >> 8) & kStepMask);
+      const u32 f = M->s_fl[i][t];
+      const i32 src = (i32)((f >> 8) & kStepMask);
       crr_initiated_row r;
       r.initiated_id = id_at((u32)src);
-      r.version = ev_ver(src);
-      r.initiated_batch_id = batch_first_id(src);
+      r.version = ver_of(L, G, src);
+      r.initiated_batch_id = r.initiated_id - (i64)((f >> (8 + kStepBits)) & kStepMask);
       r.src = src;
       r.flags = CRR_ROW_LIVE;
       *G.sig(i) = r;
     }
+  }
+  // the version of the event at `step`: the version history's item covering its ID (all written back to
+  // the workflow's own HBM rows before finalize; one item -- a single-version history -- needs no read)
+  __device__ __forceinline__ i64 ver_of(const Lane& L, const Geo& G, i32 step) const {
+    if (L.vh_n <= 1) return L.vh_last_ver;
+    const i64 id = id_at((u32)step);
+    for (i32 j = 0; j + 1 < L.vh_n; ++j) {
+      const crr_vh_item it = *G.vh(j);
+      if (it.event_id >= id) return it.version;
+    }
+    return L.vh_last_ver;
   }
   __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return id_at((M->t_fl[i][t] >> 8) & kStepMask); }
   __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return id_at(M->a_src[i][t] & kStepMask); }

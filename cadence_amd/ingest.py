@@ -169,7 +169,7 @@ class DeviceIngest:
     @staticmethod
     def input_shapes(S: CIngestSummary):
         return {"ev_slots": int(S.n_slots), "act_side": int(S.n_act_side), "start_side": int(S.n_start_side),
-                "reset_keys": int(S.n_reset_keys), "arena": int(S.arena_bytes)}
+                "reset_keys": max(int(S.n_reset_keys), 1), "arena": int(S.arena_bytes)}
 
     def allocate(self, S: CIngestSummary, emit_tasks: bool = False) -> DeviceBatch:
         """Device input / output buffers for a plan's summary, and the C structs over them."""
@@ -185,7 +185,7 @@ class DeviceIngest:
         ci.ev = ev
         for field, nb in (("act_side", int(S.n_act_side) * abi.ACTIVITY_SIDE.itemsize),
                           ("start_side", int(S.n_start_side) * abi.START_SIDE.itemsize),
-                          ("reset_keys", int(S.n_reset_keys) * 4),
+                          ("reset_keys", max(int(S.n_reset_keys), 1) * 4),
                           ("arena", int(S.arena_bytes) + 16),
                           ("wf", max(n, 1) * abi.WORKFLOW.itemsize)):
             T[field] = torch.zeros(max(nb, 1) + 16, dtype=torch.uint8, device=dev)

@@ -82,7 +82,7 @@ typedef struct crr_ingest_summary {
     uint64_t n_slots;               /* event-column slots of the layout (lane groups padded + the tail) */
     uint64_t n_act_side;            /* activity side-record slots */
     uint64_t n_start_side;          /* start side-record slots */
-    uint64_t n_reset_keys;
+    uint64_t n_reset_keys;          /* previous reset points (0: allocate one entry, left 0 -- flatten's placeholder) */
     uint64_t arena_bytes;           /* branch tokens (+ final tokens) */
     uint64_t table_rows[8];         /* act, timer, child, rc, sig, vh, rp, tasks slot-table rows */
     uint32_t n_wf;

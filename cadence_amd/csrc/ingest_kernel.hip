@@ -47,6 +47,7 @@ using i32 = int32_t;
 using u32 = uint32_t;
 using u64 = uint64_t;
 using u8 = uint8_t;
+typedef u32 v4u __attribute__((ext_vector_type(4)));
 
 enum : u32 { T_STOP = 0, T_BOOL = 2, T_BYTE = 3, T_DOUBLE = 4, T_I16 = 6, T_I32 = 8, T_I64 = 10, T_STRING = 11,
              T_STRUCT = 12, T_MAP = 13, T_SET = 14, T_LIST = 15 };
@@ -124,11 +125,23 @@ constexpr i32 kErrScratch = -100;            // CRR_INGEST_SCRATCH_TOO_SMALL
 // The window holds bytes [wb, wb + 32); any read of up to 8 bytes starting in its first half is served
 // from registers.  A sequential walk shifts it by 16 bytes with one dwordx4 load.  `bytes` is readable
 // 32 bytes past the last blob (cadence_ingest.h).
-struct Rd {
+struct Cursor { u64 p; int err; };   // where a walk ended, and how
+// the general container walk (defined after Rd): a list / set / map whose header has been read
+__device__ __attribute__((noinline)) Cursor skip_nested(const u8* b, u64 p, u64 end, u32 kind, u32 kt, u32 vt,
+                                                        i32 n, int d0);
+
+// The reader, in two builds: RdT<true> walks any value; RdT<false> (the decode's fast pass) has no call
+// in it -- a container holding structs or containers stops the walk with kDeferGeneral, and the blob is
+// decoded again by the general build (blob_decode_general_kernel).  A call would put the whole walk
+// state (reader, event) in scratch memory.
+constexpr int kDeferGeneral = -90;
+constexpr u32 kDeferMark = 0xFFFFFFFFu;   // cnt[1][blob] of a deferred blob, until the general pass
+template <bool G>
+struct RdT {
   const u8* b;
   u64 p, end;
   u64 wb;            // window base (16-aligned), ~0: none
-  uint4 w0, w1;
+  v4u w0, w1;     // native vectors: HIP's uint4 struct is copied by memcpy, which keeps the reader in scratch
   int err;           // CRR_DECODE_* (0 ok)
 
   __device__ __forceinline__ void init(const u8* bytes, u64 begin, u64 e) {
@@ -146,17 +159,19 @@ struct Rd {
       if (a == wb + 16) {
         w0 = w1;
       } else {
-        w0 = *reinterpret_cast<const uint4*>(b + a);
+        w0 = *reinterpret_cast<const v4u*>(b + a);
       }
-      w1 = *reinterpret_cast<const uint4*>(b + a + 16);
+      w1 = *reinterpret_cast<const v4u*>(b + a + 16);
       wb = a;
     }
-    const u32 o = (u32)(q & 15), k = o >> 2, sh = (o & 3) * 8;
-    const u32 x0 = k == 0 ? w0.x : k == 1 ? w0.y : k == 2 ? w0.z : w0.w;
-    const u32 x1 = k == 0 ? w0.y : k == 1 ? w0.z : k == 2 ? w0.w : w1.x;
-    const u32 x2 = k == 0 ? w0.z : k == 1 ? w0.w : k == 2 ? w1.x : w1.y;
-    const u32 lo = sh ? (x0 >> sh) | (x1 << (32 - sh)) : x0;
-    const u32 hi = sh ? (x1 >> sh) | (x2 << (32 - sh)) : x1;
+    // dwords k, k+1, k+2 of the window (k = o / 4) by two bit-selects, then the byte shift: no dynamic
+    // index into the window (the compiler would spill it to scratch to index it)
+    const u32 o = (u32)(q & 15);
+    const bool h8 = (o & 8) != 0, h4 = (o & 4) != 0;
+    const u32 a0 = h8 ? w0.z : w0.x, a1 = h8 ? w0.w : w0.y, a2 = h8 ? w1.x : w0.z, a3 = h8 ? w1.y : w0.w;
+    const u32 x0 = h4 ? a1 : a0, x1 = h4 ? a2 : a1, x2 = h4 ? a3 : a2;
+    const u32 lo = __builtin_amdgcn_alignbyte(x1, x0, o & 3);
+    const u32 hi = __builtin_amdgcn_alignbyte(x2, x1, o & 3);
     return ((u64)hi << 32) | lo;
   }
   __device__ __forceinline__ u32 u8_() {
@@ -215,30 +230,19 @@ struct Rd {
     return h;
   }
   // skip one value of `type` (history_decode.cpp Reader::skip: a value nested deeper than 64 is
-  // BAD_TYPE).  Structs, strings and scalars -- all a HistoryEvent's skipped fields but a few -- need only
-  // a count of open structs; a list / set / map goes to the general walk with its own stack.
-  __device__ void skip(u32 type) {
+  // BAD_TYPE).  Inline: scalars, strings, structs (a count of open structs) and lists / sets / maps of
+  // scalars or strings -- every skipped field of the events Cadence writes; a container holding structs
+  // or containers goes out of line to skip_nested (whose level stack lives in scratch).  Nothing here
+  // may take the reader's address: the walk state stays in registers.
+  __device__ __forceinline__ void skip(u32 type) {
     u32 t = type;
     int open = 0;   // open structs: the value about to be skipped sits at this depth
     for (;;) {
       if (err) return;
       if (open > 64) { err = CRR_DECODE_BAD_TYPE; return; }
-      switch (t) {
-        case T_BOOL: case T_BYTE: if (need(1)) p += 1; break;
-        case T_I16: if (need(2)) p += 2; break;
-        case T_I32: if (need(4)) p += 4; break;
-        case T_DOUBLE: case T_I64: if (need(8)) p += 8; break;
-        case T_STRING: {
-          const i32 n = be32();
-          if (err) return;
-          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          if (need((u64)n)) p += (u64)n;
-          break;
-        }
-        case T_STRUCT: ++open; break;
-        case T_MAP: case T_SET: case T_LIST: skip_containers(t, open); break;
-        default: err = CRR_DECODE_BAD_TYPE; return;
-      }
+      if (t == T_STRUCT) ++open;
+      else if (t == T_MAP || t == T_SET || t == T_LIST) skip_container(t, open);
+      else skip_leaf(t);
       if (err) return;
       // the innermost open struct's next field, closing finished ones
       for (;;) {
@@ -250,68 +254,47 @@ struct Rd {
       }
     }
   }
-  // a list / set / map at depth d0 and everything inside it
-  __device__ void skip_containers(u32 type, int d0) {
-    struct Lvl { u8 kind, t1, t2, pad; i32 rem; };
-    Lvl st[66];
-    int d = d0;     // depth of the value about to be skipped
-    u32 t = type;
-    for (;;) {
-      if (err) return;
-      if (d > 64) { err = CRR_DECODE_BAD_TYPE; return; }
-      bool pushed = false;
-      switch (t) {
-        case T_BOOL: case T_BYTE: if (need(1)) p += 1; break;
-        case T_I16: if (need(2)) p += 2; break;
-        case T_I32: if (need(4)) p += 4; break;
-        case T_DOUBLE: case T_I64: if (need(8)) p += 8; break;
-        case T_STRING: {
-          const i32 n = be32();
-          if (err) return;
-          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          if (need((u64)n)) p += (u64)n;
-          break;
-        }
-        case T_STRUCT: st[d - d0] = Lvl{T_STRUCT, 0, 0, 0, 0}; pushed = true; break;
-        case T_MAP: {
-          const u32 kt = u8_(), vt = u8_();
-          const i32 n = be32();
-          if (err) return;
-          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          st[d - d0] = Lvl{T_MAP, (u8)kt, (u8)vt, 0, 2 * n};
-          pushed = true;
-          break;
-        }
-        case T_SET: case T_LIST: {
-          const u32 et = u8_();
-          const i32 n = be32();
-          if (err) return;
-          if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
-          st[d - d0] = Lvl{T_LIST, (u8)et, (u8)et, 0, n};
-          pushed = true;
-          break;
-        }
-        default: err = CRR_DECODE_BAD_TYPE; return;
-      }
-      if (err) return;
-      if (pushed) ++d;
-      for (;;) {
-        if (d == d0) return;
-        Lvl& L = st[d - 1 - d0];
-        if (L.kind == T_STRUCT) {
-          i32 id;
-          if (field(t, id)) break;
-          if (err) return;
-          --d;
-          continue;
-        }
-        if (L.rem == 0) { --d; continue; }
-        t = (L.kind == T_MAP && (L.rem & 1) == 0) ? L.t1 : L.t2;
-        if (L.kind != T_MAP) t = L.t1;
-        --L.rem;
+  __device__ __forceinline__ static bool leaf(u32 t) {
+    return t == T_BOOL || t == T_BYTE || t == T_I16 || t == T_I32 || t == T_I64 || t == T_DOUBLE || t == T_STRING;
+  }
+  __device__ __forceinline__ void skip_leaf(u32 t) {
+    switch (t) {
+      case T_BOOL: case T_BYTE: if (need(1)) p += 1; break;
+      case T_I16: if (need(2)) p += 2; break;
+      case T_I32: if (need(4)) p += 4; break;
+      case T_DOUBLE: case T_I64: if (need(8)) p += 8; break;
+      case T_STRING: {
+        const i32 n = be32();
+        if (err) return;
+        if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+        if (need((u64)n)) p += (u64)n;
         break;
       }
+      default: err = CRR_DECODE_BAD_TYPE;
     }
+  }
+  // a list / set / map value at depth d0: its header, then its elements at depth d0 + 1 (a map's keys
+  // and values alternate)
+  __device__ __forceinline__ void skip_container(u32 t, int d0) {
+    const u32 kt = u8_();
+    const u32 vt = t == T_MAP ? u8_() : kt;
+    const i32 n = be32();
+    if (err) return;
+    if (n < 0) { err = CRR_DECODE_TRUNCATED; return; }
+    if (n == 0) return;
+    if (!leaf(kt) || !leaf(vt)) {
+      if constexpr (G) {
+        const Cursor c = skip_nested(b, p, end, t == T_MAP ? T_MAP : T_LIST, kt, vt, n, d0);
+        p = c.p;
+        err = c.err;
+      } else {
+        err = kDeferGeneral;
+      }
+      return;
+    }
+    if (d0 + 1 > 64) { err = CRR_DECODE_BAD_TYPE; return; }
+    const u64 m = t == T_MAP ? 2 * (u64)n : (u64)n;
+    for (u64 i = 0; i < m && !err; ++i) skip_leaf((i & 1) ? vt : kt);
   }
   __device__ __forceinline__ bool want(u32 got, u32 expect) {   // Reader::want
     if (got == expect) return true;
@@ -319,6 +302,64 @@ struct Rd {
     return false;
   }
 };
+using Rd = RdT<true>;
+
+// Rd::skip's general container walk: the value (a list / set / map whose header was just read, at depth
+// d0) and everything inside it, levels on a stack (history_decode.cpp Reader::skip).  Out of line so its
+// stack lives in this function's own scratch frame, not in every walk's registers.
+__device__ __attribute__((noinline)) Cursor skip_nested(const u8* b, u64 p, u64 end, u32 kind, u32 kt, u32 vt,
+                                                        i32 n, int d0) {
+  struct Lvl { u8 kind, t1, t2, pad; i32 rem; };
+  Lvl st[66];
+  Rd r;
+  r.init(b, p, end);
+  st[0] = Lvl{(u8)kind, (u8)kt, (u8)vt, 0, kind == T_MAP ? 2 * n : n};
+  int d = d0 + 1;   // depth of the next value
+  u32 t = 0;
+  for (;;) {
+    // the next value: the innermost open level's next field / element, closing finished levels
+    for (;;) {
+      if (d == d0) return Cursor{r.p, r.err};
+      Lvl& L = st[d - 1 - d0];
+      if (L.kind == T_STRUCT) {
+        i32 id;
+        if (r.field(t, id)) break;
+        if (r.err) return Cursor{r.p, r.err};
+        --d;
+        continue;
+      }
+      if (L.rem == 0) { --d; continue; }
+      t = (L.kind == T_MAP && (L.rem & 1) == 0) ? L.t1 : L.t2;
+      if (L.kind != T_MAP) t = L.t1;
+      --L.rem;
+      break;
+    }
+    if (d > 64) { r.err = CRR_DECODE_BAD_TYPE; return Cursor{r.p, r.err}; }
+    switch (t) {
+      case T_STRUCT: st[d - d0] = Lvl{T_STRUCT, 0, 0, 0, 0}; ++d; break;
+      case T_MAP: {
+        const u32 k1 = r.u8_(), v1 = r.u8_();
+        const i32 m = r.be32();
+        if (r.err) return Cursor{r.p, r.err};
+        if (m < 0) return Cursor{r.p, CRR_DECODE_TRUNCATED};
+        st[d - d0] = Lvl{T_MAP, (u8)k1, (u8)v1, 0, 2 * m};
+        ++d;
+        break;
+      }
+      case T_SET: case T_LIST: {
+        const u32 et = r.u8_();
+        const i32 m = r.be32();
+        if (r.err) return Cursor{r.p, r.err};
+        if (m < 0) return Cursor{r.p, CRR_DECODE_TRUNCATED};
+        st[d - d0] = Lvl{T_LIST, (u8)et, (u8)et, 0, m};
+        ++d;
+        break;
+      }
+      default: r.skip_leaf(t);
+    }
+    if (r.err) return Cursor{r.p, r.err};
+  }
+}
 
 // The fields of one event ApplyEvents reads (host_flatten.h Attr / Event), strings as blob references.
 struct Attr {
@@ -352,39 +393,45 @@ __device__ __forceinline__ int attr_type_of_field(i32 id) {
   return (id - 40) / 10;
 }
 
-// RetryPolicy{60 ExpirationIntervalInSeconds i32}
-__device__ void read_retry_policy(Rd& r, Attr& a) {
+// RetryPolicy{60 ExpirationIntervalInSeconds i32} (Reader::want: a wrong-typed field 60 is skipped)
+template <bool G>
+__device__ __forceinline__ void read_retry_policy(RdT<G>& r, Attr& a) {
   a.has_retry = 1;
   u32 ft;
   i32 id;
   while (r.field(ft, id)) {
-    if (id == 60 && r.want(ft, T_I32)) a.expiration = r.be32();
-    else if (id != 60) r.skip(ft);
+    if (id == 60 && ft == T_I32) a.expiration = r.be32();
+    else r.skip(ft);
   }
 }
 
 // ResetPoints{10 Points list<ResetPointInfo{10 BinaryChecksum}>}: only the final list's position is
-// kept; its strings are read once the event is complete (WfFlattener::add interns them there)
-__device__ void read_reset_points(Rd& r, Attr& a) {
-  a.prev_mode = -2;
+// kept; its strings are read once the event is complete (WfFlattener::add interns them there).  Out of
+// reader of its own, result by value.
+struct PrevPoints { u64 p; u64 pos; i32 err, mode, n; u32 et; };
+template <bool G>
+__device__ __forceinline__ PrevPoints read_reset_points(const u8* b, u64 p, u64 end) {
+  RdT<G> r;
+  r.init(b, p, end);
+  PrevPoints o{0, 0, 0, -2, 0, 0};
   u32 ft;
   i32 id;
   while (r.field(ft, id)) {
     if (id == 10 && ft == T_LIST) {
       const u32 et = r.u8_();
       const i32 n = r.be32();
-      if (r.err) return;
-      if (n < 0) { r.err = CRR_DECODE_TRUNCATED; return; }
-      a.prev_mode = 0;
-      a.prev_pos = r.p;
-      a.prev_n = n;
-      a.prev_et = et;
+      if (r.err) break;
+      if (n < 0) { r.err = CRR_DECODE_TRUNCATED; break; }
+      o.mode = 0;
+      o.pos = r.p;
+      o.n = n;
+      o.et = et;
       for (i32 i = 0; i < n && !r.err; ++i) {
         if (et != T_STRUCT) { r.skip(et); continue; }
         u32 t2;
         i32 id2;
         while (r.field(t2, id2)) {
-          if (id2 == 10 && t2 == T_STRING) { u64 o; u32 l; r.str(o, l); }
+          if (id2 == 10 && t2 == T_STRING) { u64 so; u32 sl; r.str(so, sl); }
           else r.skip(t2);
         }
       }
@@ -392,10 +439,14 @@ __device__ void read_reset_points(Rd& r, Attr& a) {
       r.skip(ft);
     }
   }
+  o.p = r.p;
+  o.err = r.err;
+  return o;
 }
 
 // history_decode.cpp read_attributes
-__device__ void read_attributes(Rd& r, int t, Attr& a) {
+template <bool G>
+__device__ __forceinline__ void read_attributes(RdT<G>& r, int t, Attr& a) {
   u32 ft;
   i32 id;
   while (r.field(ft, id)) {
@@ -409,7 +460,12 @@ __device__ void read_attributes(Rd& r, int t, Attr& a) {
         else if (id == 80 && ft == T_I32) a.attempt = r.be32();
         else if (id == 90 && ft == T_I64) a.expiration_ts = r.be64();
         else if (id == 110 && ft == T_I32) a.backoff = r.be32();
-        else if (id == 130 && ft == T_STRUCT) read_reset_points(r, a);
+        else if (id == 130 && ft == T_STRUCT) {
+          const PrevPoints q = read_reset_points<G>(r.b, r.p, r.end);
+          r.p = q.p;
+          r.err = q.err;
+          a.prev_mode = q.mode; a.prev_pos = q.pos; a.prev_n = q.n; a.prev_et = q.et;
+        }
         else used = false;
         break;
       case CRR_EV_DECISION_TASK_SCHEDULED:
@@ -494,41 +550,45 @@ __device__ void read_attributes(Rd& r, int t, Attr& a) {
   }
 }
 
-// history_decode.cpp read_event: an attribute struct that arrives before the type is re-read after it
-__device__ void read_event(Rd& r, Event& e) {
+// history_decode.cpp read_event: an attribute struct that arrives before the type is re-read after it.
+// One read_attributes site and one skip site (each is a large inline body).
+template <bool G>
+__device__ __forceinline__ void read_event(RdT<G>& r, Event& e) {
   e.id = e.ts = e.ver = e.task = 0;
   e.type = 0;
   attr_init(e.a);
-  u64 attr_at = 0;
-  bool have_attr_at = false;
-  int attr_t = -1;
-  bool have_type = false;
+  u64 attr_at = 0, resume = 0;
+  int attr_t = -1;     // the last attribute struct seen before the type: its type (and attr_at its bytes)
+  bool have_type = false, last = false;
   u32 ft;
   i32 id;
-  while (r.field(ft, id)) {
-    if (id == 10 && ft == T_I64) e.id = r.be64();
-    else if (id == 20 && ft == T_I64) e.ts = r.be64();
-    else if (id == 30 && ft == T_I32) { e.type = r.be32(); have_type = true; }
-    else if (id == 35 && ft == T_I64) e.ver = r.be64();
-    else if (id == 36 && ft == T_I64) e.task = r.be64();
-    else if (ft == T_STRUCT && attr_type_of_field(id) >= 0) {
-      const int at = attr_type_of_field(id);
-      if (have_type && at == e.type) {
-        read_attributes(r, at, e.a);
+  for (;;) {
+    int at = -1;
+    if (!r.field(ft, id)) {
+      if (r.err || attr_t < 0 || attr_t != e.type) return;
+      resume = r.p;               // re-read the early attributes, then leave the reader at the stop byte
+      r.p = attr_at;
+      at = attr_t;
+      last = true;
+    } else if (id == 10 && ft == T_I64) { e.id = r.be64(); continue; }
+    else if (id == 20 && ft == T_I64) { e.ts = r.be64(); continue; }
+    else if (id == 30 && ft == T_I32) { e.type = r.be32(); have_type = true; continue; }
+    else if (id == 35 && ft == T_I64) { e.ver = r.be64(); continue; }
+    else if (id == 36 && ft == T_I64) { e.task = r.be64(); continue; }
+    else {
+      const int ty = ft == T_STRUCT ? attr_type_of_field(id) : -1;
+      if (ty >= 0 && have_type && ty == e.type) {
+        at = ty;
       } else {
-        if (!have_type) { attr_at = r.p; have_attr_at = true; attr_t = at; }
+        if (ty >= 0 && !have_type) { attr_at = r.p; attr_t = ty; }
         r.skip(ft);
+        if (r.err) return;
+        continue;
       }
-    } else {
-      r.skip(ft);
     }
-  }
-  if (r.err) return;
-  if (have_attr_at && attr_t == e.type) {
-    Rd r2;
-    r2.init(r.b, attr_at, r.end);
-    read_attributes(r2, attr_t, e.a);
-    if (r2.err) r.err = r2.err;
+    read_attributes(r, at, e.a);
+    if (r.err) return;
+    if (last) { r.p = resume; return; }
   }
 }
 
@@ -568,6 +628,23 @@ __device__ __forceinline__ i32 domain_status(const crr_blob_batch& in, const u32
   if (in.n_domains == 0xFFFFFFFFu) return CRR_DOMAIN_RESOLVED;
   if (cap == 0) return CRR_DOMAIN_UNKNOWN;
   u32 h = fnv1a(in.bytes, off, len) & (cap - 1);
+  for (u32 probe = 0; probe < cap; ++probe) {
+    const u32 e = table[h];
+    if (e == 0) return CRR_DOMAIN_UNKNOWN;
+    const u32 d = e - 1;
+    if (in.domain_len[d] == len && bytes_equal(in.bytes, off, in.strings, in.domain_off[d], len)) return CRR_DOMAIN_RESOLVED;
+    h = (h + 1) & (cap - 1);
+  }
+  return CRR_DOMAIN_UNKNOWN;
+}
+
+// the same, the name's FNV-1a already computed (through the reader's window)
+__device__ __forceinline__ i32 domain_status_h(const crr_blob_batch& in, const u32* table, u32 cap, u64 off, u32 len,
+                                               u32 hash) {
+  if (len == 0) return CRR_DOMAIN_NOT_SET;
+  if (in.n_domains == 0xFFFFFFFFu) return CRR_DOMAIN_RESOLVED;
+  if (cap == 0) return CRR_DOMAIN_UNKNOWN;
+  u32 h = hash & (cap - 1);
   for (u32 probe = 0; probe < cap; ++probe) {
     const u32 e = table[h];
     if (e == 0) return CRR_DOMAIN_UNKNOWN;
@@ -651,14 +728,15 @@ __global__ void blob_head_kernel(crr_blob_batch in, Plan P, int full) {
 // host_flatten.h WfFlattener::add's per-type columns); side records and key strings at the event's own
 // slot (wf_pass numbers them within the workflow); a Started event's PrevAutoResetPoints list position
 // in its key slot, the list's length counted per blob.
-__device__ void decode_blob(const crr_blob_batch& in, const Plan& P, u32 bi) {
+template <bool G>
+__device__ __forceinline__ void decode_blob(const crr_blob_batch& in, const Plan& P, u32 bi) {
   const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
   const u64 NB = (u64)P.n_blobs + 1;
   u64 x = P.off[0 * NB + bi];
   const u64 x_end = P.off[0 * NB + bi + 1];
   u32 n_prev = 0;
   if (b1 > b0) {
-    Rd r;
+    RdT<G> r;
     r.init(in.bytes, b0, b1);
     if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
     const i32 new_run = in.wf[P.blob_wf[bi]].new_run_wf;
@@ -755,6 +833,10 @@ __device__ void decode_blob(const crr_blob_batch& in, const Plan& P, u32 bi) {
       }
       if (r.err) break;
     }
+    if (r.err == kDeferGeneral) {   // the general pass decodes this blob again, from its start
+      P.cnt[1 * (u64)P.n_blobs + bi] = kDeferMark;
+      return;
+    }
     if (r.err) { record_error(P.err, bi, r.err); return; }
     if (x > x_first) {   // batch boundaries
       P.etype[x_first] |= CRR_ETYPE_BATCH_FIRST;
@@ -765,12 +847,269 @@ __device__ void decode_blob(const crr_blob_batch& in, const Plan& P, u32 bi) {
   P.cnt[1 * (u64)P.n_blobs + bi] = n_prev;
 }
 
-__global__ void blob_decode_kernel(crr_blob_batch in, Plan P) {
+
+// ---- 3a: the fast pass -------------------------------------------------------------------------------------
+// thriftrw's own shape -- every struct's fields in increasing id order, an event's type before its
+// attributes, no more events than the header announced -- with each value stored to its column / side
+// record as it is read (defaults first, at the type), so the walk keeps only the reader and a few counters
+// in registers.  Anything else (and a container of structs) defers the blob to the general pass, which
+// is decode_blob<true>: the same results for these blobs, by construction the same walk.
+enum : u32 { S_ID = 1, S_TS = 2, S_VER = 4, S_TASK = 8, S_REF = 16, S_AUX = 32 };
+
+__device__ __forceinline__ bool domain_aux_type(i32 t) {
+  return t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED || t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ||
+         t == CRR_EV_SIGNAL_EXTERNAL_INITIATED;
+}
+
+// the attribute fields read_attributes takes, stored where decode_blob puts them
+__device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_blob_batch& in, const Plan& P, u64 x,
+                                                u32& seen, u32& n_prev) {
+  u32 ft;
+  i32 id;
+  i32 last = -0x10000;
+  while (r.field(ft, id)) {
+    if (id <= last) { r.err = kDeferGeneral; return; }
+    last = id;
+    bool used = true;
+    switch (t) {
+      case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
+        crr_start_side* ss = P.start + x;
+        if (id == 12 && ft == T_STRING) {
+          u64 o; u32 l;
+          r.str(o, l);
+          if (!r.err) ss->parent_domain_status = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u);
+        }
+        else if (id == 40 && ft == T_I32) ss->workflow_timeout = r.be32();
+        else if (id == 50 && ft == T_I32) ss->decision_start_to_close = r.be32();
+        else if (id == 55 && ft == T_I32) ss->initiator = r.be32();
+        else if (id == 80 && ft == T_I32) ss->attempt = r.be32();
+        else if (id == 90 && ft == T_I64) ss->expiration_ns = r.be64();
+        else if (id == 110 && ft == T_I32) ss->first_decision_backoff = r.be32();
+        else if (id == 130 && ft == T_STRUCT) {
+          const PrevPoints q = read_reset_points<false>(r.b, r.p, r.end);
+          r.p = q.p;
+          r.err = q.err;
+          if (!r.err) {
+            ss->prev_reset_count = q.mode == 0 ? q.n : q.mode;
+            if (q.mode == 0) {
+              PrevRef pr;
+              pr.pos = q.pos; pr.n = (u32)q.n; pr.et = q.et;
+              *reinterpret_cast<PrevRef*>(P.keys + x) = pr;
+              n_prev += (u32)q.n;
+            }
+          }
+        }
+        else used = false;
+        break;
+      }
+      case CRR_EV_DECISION_TASK_SCHEDULED:
+        if (id == 20 && ft == T_I32) { P.aux[x] = r.be32(); seen |= S_AUX; }
+        else if (id == 30 && ft == T_I64) { P.ref[x] = r.be64(); seen |= S_REF; }
+        else used = false;
+        break;
+      case CRR_EV_DECISION_TASK_TIMED_OUT:
+        if (id == 30 && ft == T_I32) { P.aux[x] = r.be32(); seen |= S_AUX; } else used = false;
+        break;
+      case CRR_EV_ACTIVITY_TASK_SCHEDULED: {
+        crr_activity_side* as = P.act + x;
+        if (id == 10 && ft == T_STRING) {
+          u64 o; u32 l;
+          r.str(o, l);
+          if (!r.err) { KeyRef kr; kr.off = o; kr.len = l; kr.hash = l ? r.hash(o, l) : 0u; P.keys[x] = kr; }
+        }
+        else if (id == 25 && ft == T_STRING) {
+          u64 o; u32 l;
+          r.str(o, l);
+          if (!r.err) as->domain_status = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u);
+        }
+        else if (id == 45 && ft == T_I32) as->schedule_to_close = r.be32();
+        else if (id == 50 && ft == T_I32) as->schedule_to_start = r.be32();
+        else if (id == 55 && ft == T_I32) as->start_to_close = r.be32();
+        else if (id == 60 && ft == T_I32) as->heartbeat = r.be32();
+        else if (id == 110 && ft == T_STRUCT) {   // RetryPolicy{60 ExpirationIntervalInSeconds}
+          as->has_retry_policy = 1;
+          u32 f2;
+          i32 id2;
+          while (r.field(f2, id2)) {
+            if (id2 == 60 && f2 == T_I32) as->expiration_interval = r.be32();
+            else r.skip(f2);
+          }
+        }
+        else used = false;
+        break;
+      }
+      case CRR_EV_DECISION_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED: case CRR_EV_TIMER_FIRED:
+      case CRR_EV_TIMER_CANCELED: case CRR_EV_TIMER_STARTED: {
+        const i32 key_id = t == CRR_EV_DECISION_TASK_COMPLETED ? 50 : 10;
+        const i32 ref_id = t == CRR_EV_DECISION_TASK_COMPLETED ? 30 : t == CRR_EV_TIMER_STARTED ? 20 : -1;
+        if (id == key_id && ft == T_STRING) {
+          u64 o; u32 l;
+          r.str(o, l);
+          if (!r.err) { KeyRef kr; kr.off = o; kr.len = l; kr.hash = l ? r.hash(o, l) : 0u; P.keys[x] = kr; }
+        }
+        else if (id == ref_id && ft == T_I64) { P.ref[x] = r.be64(); seen |= S_REF; }
+        else used = false;
+        break;
+      }
+      case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:
+      case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
+      case CRR_EV_SIGNAL_EXTERNAL_INITIATED: {
+        const i32 dom_id = t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED ? 10 : 20;
+        if (id == dom_id && ft == T_STRING) {
+          u64 o; u32 l;
+          r.str(o, l);
+          if (!r.err) { P.aux[x] = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u); seen |= S_AUX; }
+        }
+        else used = false;
+        break;
+      }
+      default: {
+        // the types whose only field is the i64 reference (read_attributes' remaining cases)
+        i32 ref_id = -1;
+        switch (t) {
+          case CRR_EV_DECISION_TASK_STARTED: case CRR_EV_ACTIVITY_TASK_STARTED: case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
+          case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:
+            ref_id = 10; break;
+          case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED: ref_id = 20; break;
+          case CRR_EV_ACTIVITY_TASK_FAILED: case CRR_EV_ACTIVITY_TASK_CANCELED: ref_id = 30; break;
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED: ref_id = 40; break;
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
+          case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT: case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED:
+          case CRR_EV_SIGNAL_EXTERNAL_FAILED:
+            ref_id = 50; break;
+          case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED: ref_id = 60; break;
+          default: break;
+        }
+        if (id == ref_id && ft == T_I64) { P.ref[x] = r.be64(); seen |= S_REF; } else used = false;
+      }
+    }
+    if (r.err) return;
+    if (!used) r.skip(ft);
+    if (r.err) return;
+  }
+}
+
+// one event into slot x (decode_blob's loop body for a canonical event)
+__device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& in, const Plan& P, u64 x, i32 new_run,
+                                           u32& n_prev) {
+  u32 seen = 0;
+  i32 t = -1;
+  bool have_type = false;
+  i32 last = -0x10000;
+  u32 ft;
+  i32 id;
+  while (r.field(ft, id)) {
+    if (id <= last) { r.err = kDeferGeneral; return; }
+    last = id;
+    if (id == 10 && ft == T_I64) { P.id[x] = r.be64(); seen |= S_ID; }
+    else if (id == 20 && ft == T_I64) { P.ts[x] = r.be64(); seen |= S_TS; }
+    else if (id == 30 && ft == T_I32) {
+      t = r.be32();
+      have_type = true;
+      if (r.err) return;
+      // the defaults of the records this type fills (attr_init's values)
+      if (t == CRR_EV_WORKFLOW_EXECUTION_STARTED) {
+        crr_start_side ss;
+        ss.decision_start_to_close = 0; ss.workflow_timeout = 0; ss.first_decision_backoff = 0;
+        ss.initiator = CRR_INITIATOR_NIL; ss.parent_domain_status = CRR_DOMAIN_NOT_SET;
+        ss.prev_reset_key_off = n_prev;   // blob-local until wf_pass adds the blob's prefix
+        ss.prev_reset_count = -1; ss.attempt = 0; ss.expiration_ns = 0; ss.reserved = 0;
+        P.start[x] = ss;
+      } else if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {
+        crr_activity_side as;
+        as.schedule_to_start = 0; as.schedule_to_close = 0; as.start_to_close = 0; as.heartbeat = 0;
+        as.has_retry_policy = 0; as.expiration_interval = 0; as.domain_status = CRR_DOMAIN_NOT_SET; as.reserved = 0;
+        P.act[x] = as;
+      }
+      if (t >= 0 && t < CRR_EV_TYPE_COUNT && keyed_type(t)) {
+        KeyRef kr;
+        kr.off = 0; kr.len = 0; kr.hash = 0;
+        P.keys[x] = kr;
+      }
+    }
+    else if (id == 35 && ft == T_I64) { P.ver[x] = r.be64(); seen |= S_VER; }
+    else if (id == 36 && ft == T_I64) { P.task[x] = r.be64(); seen |= S_TASK; }
+    else {
+      const int at = ft == T_STRUCT ? attr_type_of_field(id) : -1;
+      if (at >= 0 && !have_type) { r.err = kDeferGeneral; return; }   // attributes before the type
+      if (at >= 0 && at == t) fast_attributes(r, t, in, P, x, seen, n_prev);
+      else r.skip(ft);
+    }
+    if (r.err) return;
+  }
+  if (r.err) return;
+  if (!have_type) { r.err = kDeferGeneral; return; }   // the type's zero default: the general pass
+  const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
+  P.etype[x] = (u8)(valid ? t : CRR_EV_PAD - 1);
+  if (!(seen & S_ID)) P.id[x] = 0;
+  if (!(seen & S_TS)) P.ts[x] = 0;
+  if (!(seen & S_VER)) P.ver[x] = 0;
+  if (!(seen & S_TASK)) P.task[x] = 0;
+  if (!(seen & S_REF)) P.ref[x] = 0;
+  if (valid && t == CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW) P.aux[x] = new_run;
+  else if (!(seen & S_AUX)) P.aux[x] = 0;   // (CRR_DOMAIN_NOT_SET for a domain-aux type: also 0)
+  P.key[x] = 0;
+}
+
+__device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const Plan& P, u32 bi) {
+  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
+  const u64 NB = (u64)P.n_blobs + 1;
+  u64 x = P.off[0 * NB + bi];
+  const u64 x_end = P.off[0 * NB + bi + 1];
+  u32 n_prev = 0;
+  if (b1 > b0) {
+    RdT<false> r;
+    r.init(in.bytes, b0, b1);
+    if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
+    const i32 new_run = in.wf[P.blob_wf[bi]].new_run_wf;
+    const u64 x_first = x;
+    u32 ft;
+    i32 fid;
+    while (r.field(ft, fid)) {
+      if (fid != 10 || ft != T_LIST) { r.skip(ft); continue; }
+      const u32 et = r.u8_();
+      const i32 n = r.be32();
+      if (r.err) break;
+      if (n < 0) { r.err = CRR_DECODE_TRUNCATED; break; }
+      if (et != T_STRUCT && n > 0) { r.err = CRR_DECODE_BAD_TYPE; break; }
+      for (i32 i = 0; i < n; ++i) {
+        if (x >= x_end) { r.err = kDeferGeneral; break; }   // more events than announced
+        fast_event(r, in, P, x, new_run, n_prev);
+        if (r.err) break;
+        ++x;
+      }
+      if (r.err) break;
+    }
+    if (r.err == kDeferGeneral) {
+      P.cnt[1 * (u64)P.n_blobs + bi] = kDeferMark;
+      return;
+    }
+    if (r.err) { record_error(P.err, bi, r.err); return; }
+    if (x > x_first) {   // batch boundaries
+      P.etype[x_first] |= CRR_ETYPE_BATCH_FIRST;
+      P.etype[x - 1] |= CRR_ETYPE_BATCH_LAST;
+    }
+  }
+  if (x != x_end) atomicOr(P.flags, 1u);   // fewer events than the header announced: recount
+  P.cnt[1 * (u64)P.n_blobs + bi] = n_prev;
+}
+
+__global__ __launch_bounds__(kBlock) void blob_decode_kernel(crr_blob_batch in, Plan P) {
   const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= in.n_blobs) return;
   const u64 NB = (u64)P.n_blobs + 1;
   if (P.off[0 * NB + P.n_blobs] > P.max_events) return;   // the summary reports it
-  decode_blob(in, P, bi);
+  decode_blob_fast(in, P, bi);
+}
+
+// the blobs the fast pass deferred (a container of structs / containers), with the general reader
+__global__ __launch_bounds__(kBlock) void blob_decode_general_kernel(crr_blob_batch in, Plan P) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs) return;
+  const u64 NB = (u64)P.n_blobs + 1;
+  if (P.off[0 * NB + P.n_blobs] > P.max_events || *P.flags) return;   // reported / recounted
+  if (P.cnt[1 * (u64)P.n_blobs + bi] != kDeferMark) return;
+  decode_blob<true>(in, P, bi);
 }
 
 // ---- 4: previous reset points at their reset_keys positions ------------------------------------------------
@@ -1492,6 +1831,7 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
     if (nb) hipLaunchKernelGGL(blob_head_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P, full);
     multi_scan<u32>(P.cnt, nb, nb, 1, P.tile, P.off, NB, s);
     if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
+    if (nb) hipLaunchKernelGGL(blob_decode_general_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
     if (full) break;
     // a header count that was wrong (hand-made blobs): count by walking every blob, then decode again
     u32 flags = 0;

@@ -118,3 +118,19 @@ def test_device_ingest_empty_and_tiny(eng):
     _canon, want = _host_path(bs)
     ing, out = _ingest(eng, bs)
     _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rate", [0.05, 0.5])
+def test_device_ingest_reshaped_blobs(eng, rate):
+    """Blobs in shapes thriftrw never writes (tests/thrift_tree.py: fields reversed / shuffled, the type
+    after the attributes, duplicate types, lists of structs and maps of lists, leaf containers) go through
+    the fast pass's deferral to the general pass and still match the host decoder byte for byte."""
+    from thrift_tree import reshape_blobset
+    hs = synth_mixed.mixed_histories(400, 29, multi_version=True, invalid_rate=0.2, can_rate=0.3)
+    b = flatten(hs, known_domains=set(KNOWN_DOMAINS))
+    for src in (encode_batch(b), encode_batch(synth_native.mixed(1500, multi_version=True, unknown_domain_rate=0.2))):
+        bs = reshape_blobset(src, seed=11, rate=rate)
+        _canon, want = _host_path(bs)
+        ing, out = _ingest(eng, bs)
+        _assert_same_inputs(ing.to_host_batch(out), want)

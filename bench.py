@@ -521,6 +521,11 @@ def blob_to_rows(ctx, canon, resident_digest, name, chunks=8):
            "note": "median of 3 passes; blobs in pinned host buffers as read from persistence; every stage timed"}
     if resident_digest is not None:
         fig["matches_resident_digest"] = fig["digest"] == [int(x) for x in resident_digest]
+    # the bound: the uploads alone over PCIe (pinned host -> HBM, the same bytes, no compute)
+    peak = sr.h2d_peak()
+    fig["roofline"] = {"bound": "pcie", "achieved": fig["h2d_GBs"], "peak": peak, "unit": "GB/s",
+                       "frac": fig["h2d_GBs"] / peak if peak else None,
+                       "note": "peak = this pipeline's own H2D copies alone, measured in the same run"}
     # the same work with the blobs already resident in HBM: device-side stages only
     torch, eng = ctx.torch, ctx.eng
     torch.cuda.synchronize()
@@ -606,6 +611,33 @@ def host_ingest(ctx, flatten_s, flatten_events):
     return {"decode": dec, "interleave_config2": {"events_per_s": flatten_events / flatten_s, "seconds": flatten_s}}
 
 
+def cpu_blob_path(ctx, threads, k):
+    """The CPU doing what blob_to_rows does: persisted thriftrw blobs -> the native host decoder
+    (crr_decode_histories, `threads` workers) -> the oracle's replay (`threads` workers), on a sample of
+    config-2 workflows; both stages timed, the rate of the two in sequence reported."""
+    from oracle import oracle
+    from cadence_amd import synth
+    from cadence_amd.blobs import KNOWN_DOMAINS, encode_batch
+    from cadence_amd.decode import decode_histories, time_native_decode
+    n = min(ctx.args.cpu_sample, 50_000)
+    canon = synth.activity_chain(n, k, synth.SEED_C2, with_keys=True, wf_ids=np.arange(n))
+    src = encode_batch(canon).to_sources()
+    dec = time_native_decode(src, KNOWN_DOMAINS, n_threads=threads, min_seconds=ctx.args.cpu_seconds / 2)
+    batch = decode_histories(src, known_domains=KNOWN_DOMAINS, n_threads=threads)
+    passes, dt = 0, 0.0
+    while passes == 0 or dt < ctx.args.cpu_seconds / 2:
+        t0 = time.perf_counter()
+        oracle.replay(batch, threads)
+        dt += time.perf_counter() - t0
+        passes += 1
+    rep = batch.n_events * passes / dt
+    both = 1.0 / (1.0 / dec["events_per_s"] + 1.0 / rep)
+    return {"value": both, "unit": "events/s", "cores": threads, "kind": "port",
+            "decode_events_per_s": dec["events_per_s"], "replay_events_per_s": rep,
+            "sample": f"{n} config-2 workflows ({batch.n_events} events) as thriftrw blobs: native decoder "
+                      f"({dec['reps']} passes) then the oracle's replay ({passes} passes), {threads} threads each"}
+
+
 def cpu_baseline(ctx, gpu_res, gpu_batch, k):
     """The oracle (C++ restatement of the Go stateBuilder, per-workflow hash maps, std::thread workers)
     on this process's host CPUs: a bounded sample of config 2 (bit-compared with the GPU rows) and
@@ -636,6 +668,7 @@ def cpu_baseline(ctx, gpu_res, gpu_batch, k):
            "wall_s": dt, "cpu_seconds_approx": dt * threads}
     if n == gpu_batch.n_wf:
         out["gpu_parity_bit_exact"] = not diff_results(gpu_batch, gpu_res, sample, res)
+    out["blob_path"] = cpu_blob_path(ctx, threads, k)
     c1 = synth.activity_chain(10_000, 3, synth.SEED_C1, with_keys=True)
     p1, d1, _ = timed(c1)
     out["config1"] = {"events_per_s": c1.n_events * p1 / d1, "workflows_per_s": c1.n_wf * p1 / d1,
@@ -717,6 +750,9 @@ def main():
             line["pcie_inclusive"]["vs_cpu_baseline"] = line["pcie_inclusive"]["events_per_s"] / line["cpu_baseline"]["value"]
         for k, fig in line.get("blob_to_rows", {}).items():
             fig["vs_cpu_baseline"] = fig["events_per_s"] / line["cpu_baseline"]["value"]
+            fig["vs_cpu_blob_path"] = fig["events_per_s"] / line["cpu_baseline"]["blob_path"]["value"]
+            fig["device_resident"]["vs_cpu_baseline"] = (fig["device_resident"]["events_per_s"]
+                                                         / line["cpu_baseline"]["value"])
     if ctx.rank == 0:
         print(json.dumps(line), flush=True)
     if ctx.world > 1:

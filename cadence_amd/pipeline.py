@@ -247,7 +247,7 @@ class BlobStreamingReplay:
         torch, eng = self.torch, self.eng
         torch.cuda.synchronize(eng.dev)
         t0 = time.perf_counter()
-        ev_up, ev_tot = [], []
+        ev_up = []
         for p in self.parts:                                        # 1. every upload, in order
             with torch.cuda.stream(self.up):
                 for k, h in p["host"].items():
@@ -255,9 +255,31 @@ class BlobStreamingReplay:
                 e = torch.cuda.Event()
                 e.record(self.up)
                 ev_up.append(e)
+        d2h = [0]
+
+        def download(p, et):                                        # 3. exact-size downloads (D2H runs
+            et.synchronize()                                        #    beside the remaining uploads)
+            tot = p["host_tot"].numpy().copy()
+            p["totals"] = tot
+            self.down.wait_event(et)
+            T = p["out"].tensors
+            n = p["n"]
+            with torch.cuda.stream(self.down):
+                p["host_exec"].copy_(T["exec"][:n * abi.EXEC_ROW.itemsize], non_blocking=True)
+                p["host_off"].copy_(T["cmp_offsets"], non_blocking=True)
+                d2h[0] += n * abi.EXEC_ROW.itemsize + p["host_off"].numel() * 8
+                for t, (name, dt, *_) in enumerate(abi.TABLES):
+                    nb = int(tot[t]) * dt.itemsize
+                    if nb:
+                        p["host_rows"][name][:nb].copy_(T["cmp_" + name][:nb], non_blocking=True)
+                        d2h[0] += nb
+
+        queued = []                                                  # (part, totals event), not downloaded
         for i, (p, e) in enumerate(zip(self.parts, ev_up)):        # 2. ingest + replay + compaction
             s = self.comp[i % 2]
             s.wait_event(e)
+            if i >= 2:                          # chunk i-2 ran on s: this plan's sync would wait for it anyway
+                download(*queued.pop(0))
             S = p["ing"].plan(p["db"], s)                          # (synchronises s: the layout's sizes)
             out = p["out"]
             T = out.tensors
@@ -274,28 +296,29 @@ class BlobStreamingReplay:
                 p["host_tot"].copy_(T["cmp_offsets"].view(len(COMPACT_TABLES), n + 1)[:, n], non_blocking=True)
                 et = torch.cuda.Event()
                 et.record(s)
-            ev_tot.append(et)
-        d2h = 0
-        for p, et in zip(self.parts, ev_tot):                       # 3. exact-size downloads
-            et.synchronize()
-            tot = p["host_tot"].numpy().copy()
-            p["totals"] = tot
-            self.down.wait_event(et)
-            T = p["out"].tensors
-            n = p["n"]
-            with torch.cuda.stream(self.down):
-                p["host_exec"].copy_(T["exec"][:n * abi.EXEC_ROW.itemsize], non_blocking=True)
-                p["host_off"].copy_(T["cmp_offsets"], non_blocking=True)
-                d2h += n * abi.EXEC_ROW.itemsize + p["host_off"].numel() * 8
-                for t, (name, dt, *_) in enumerate(abi.TABLES):
-                    nb = int(tot[t]) * dt.itemsize
-                    if nb:
-                        p["host_rows"][name][:nb].copy_(T["cmp_" + name][:nb], non_blocking=True)
-                        d2h += nb
+            queued.append((p, et))
+        for item in queued:
+            download(*item)
         self.down.synchronize()
         wall = time.perf_counter() - t0
         return {"wall_s": wall, "events": self.n_events, "events_per_s": self.n_events / wall,
-                "h2d_bytes": self.h2d_bytes, "d2h_bytes": int(d2h), "chunks": len(self.parts)}
+                "h2d_bytes": self.h2d_bytes, "d2h_bytes": int(d2h[0]), "chunks": len(self.parts)}
+
+    def h2d_peak(self, reps: int = 3) -> float:
+        """The pinned host -> HBM copy rate of this pipeline's own uploads alone (one stream, no compute):
+        the PCIe ceiling the blob -> rows figure is bound by, in GB/s (best of `reps`)."""
+        torch, eng = self.torch, self.eng
+        best = 0.0
+        for _ in range(reps):
+            torch.cuda.synchronize(eng.dev)
+            t0 = time.perf_counter()
+            with torch.cuda.stream(self.up):
+                for p in self.parts:
+                    for k, h in p["host"].items():
+                        p["db"].tensors[k][:h.numel()].copy_(h, non_blocking=True)
+            self.up.synchronize()
+            best = max(best, self.h2d_bytes / (time.perf_counter() - t0) / 1e9)
+        return best
 
     def results(self) -> List[CompactResult]:
         out = []

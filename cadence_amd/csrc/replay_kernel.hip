@@ -375,16 +375,32 @@ __device__ __forceinline__ void swap_rows(R* a, R* b) {
 // ===================================================================================================
 // GlobalTables: pending maps as slot tables in the HBM output rows (any layout, unbounded).
 // ===================================================================================================
-struct Ev { u32 et; i64 id, ver, ts, task, ref; u32 key; i32 aux; };
+// One event's fields.  The transitions read them through accessors: the lane path holds them in
+// registers (Ev), the wavefront path reads each one out of the 64-event chunk only where a transition
+// uses it (WaveEv, below).
+struct Ev {
+  u32 et;
+  i64 id_, ver_, ts_, task_, ref_;
+  u32 key_;
+  i32 aux_;
+  __device__ __forceinline__ i64 id() const { return id_; }
+  __device__ __forceinline__ i64 ver() const { return ver_; }
+  __device__ __forceinline__ i64 ts() const { return ts_; }
+  __device__ __forceinline__ i64 task() const { return task_; }
+  __device__ __forceinline__ i64 ref() const { return ref_; }
+  __device__ __forceinline__ u32 key() const { return key_; }
+  __device__ __forceinline__ i32 aux() const { return aux_; }
+};
 
 // The rows each insert writes (mutable_state_builder.go:2142-2197, :3057-3081, :3417-3453, :2760-2779, :2883-2905)
-__device__ __forceinline__ crr_activity_row activity_row(const Ev& ev, i32 s, i64 batch_first_id,
+template <class EV>
+__device__ __forceinline__ crr_activity_row activity_row(const EV& ev, i32 s, i64 batch_first_id,
                                                          const crr_activity_side& as) {
   crr_activity_row row;
-  row.schedule_id = ev.id;
-  row.version = ev.ver;
+  row.schedule_id = ev.id();
+  row.version = ev.ver();
   row.scheduled_batch_id = batch_first_id;
-  row.scheduled_time = ev.ts;
+  row.scheduled_time = ev.ts();
   row.started_id = CRR_EMPTY_EVENT_ID;
   row.started_time = CRR_ZERO_TIME;
   row.cancel_request_id = CRR_EMPTY_EVENT_ID;
@@ -396,27 +412,29 @@ __device__ __forceinline__ crr_activity_row activity_row(const Ev& ev, i32 s, i6
   row.start_to_close = as.start_to_close;
   row.heartbeat = as.heartbeat;
   row.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
-  row.key = ev.key;
+  row.key = ev.key();
   row.flags = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u);
   row.attempt = 0;
   row.last_heartbeat_time = CRR_ZERO_TIME;
   return row;
 }
-__device__ __forceinline__ crr_timer_row timer_row(const Ev& ev, i32 s) {
+template <class EV>
+__device__ __forceinline__ crr_timer_row timer_row(const EV& ev, i32 s) {
   crr_timer_row row;
-  row.started_id = ev.id;
-  row.version = ev.ver;
-  row.expiry_time = add_seconds(ev.ts, ev.ref);
+  row.started_id = ev.id();
+  row.version = ev.ver();
+  row.expiry_time = add_seconds(ev.ts(), ev.ref());
   row.task_status = CRR_TIMER_TASK_STATUS_NONE;
-  row.key = ev.key;
+  row.key = ev.key();
   row.src = s;
   row.flags = CRR_ROW_LIVE;
   return row;
 }
-__device__ __forceinline__ crr_child_row child_row(const Ev& ev, i32 s, i64 batch_first_id) {
+template <class EV>
+__device__ __forceinline__ crr_child_row child_row(const EV& ev, i32 s, i64 batch_first_id) {
   crr_child_row row;
-  row.initiated_id = ev.id;
-  row.version = ev.ver;
+  row.initiated_id = ev.id();
+  row.version = ev.ver();
   row.initiated_batch_id = batch_first_id;
   row.started_id = CRR_EMPTY_EVENT_ID;
   row.src = s;
@@ -425,10 +443,11 @@ __device__ __forceinline__ crr_child_row child_row(const Ev& ev, i32 s, i64 batc
   row.reserved = 0;
   return row;
 }
-__device__ __forceinline__ crr_initiated_row initiated_row(const Ev& ev, i32 s, i64 batch_first_id) {
+template <class EV>
+__device__ __forceinline__ crr_initiated_row initiated_row(const EV& ev, i32 s, i64 batch_first_id) {
   crr_initiated_row row;
-  row.initiated_id = ev.id;
-  row.version = ev.ver;
+  row.initiated_id = ev.id();
+  row.version = ev.ver();
   row.initiated_batch_id = batch_first_id;
   row.src = s;
   row.flags = CRR_ROW_LIVE;
@@ -1304,7 +1323,7 @@ struct CompactTables {
     const u32 sh = (by_step && !is_act) ? 8u : 0u;
     const u32 msk = by_step ? kStepMask : 0xFFFFFFFFu;
     // inserts of children / request-cancels / signals look nothing up (kStepMask matches no entry)
-    const u32 want = by_step ? (insert ? kStepMask : step_of(ev.ref)) : ev.key;
+    const u32 want = by_step ? (insert ? kStepMask : step_of(ev.ref())) : ev.key();
     constexpr int kMax = A_SLOTS > T_SLOTS ? A_SLOTS : T_SLOTS;
     static_assert(kMax >= C_SLOTS && kMax >= R_SLOTS && kMax >= S_SLOTS, "activity or timer map is the largest");
     i32 hit = -1, fr = -1;
@@ -1340,14 +1359,14 @@ struct CompactTables {
       // Geo (and the output pointers in it) in scratch memory
       const i32 ca = G.act_cap, ct = G.timer_cap, cc = G.child_cap, cr = G.rc_cap, cs = G.sig_cap;
       const i32 cap = is_act ? ca : is_timer ? ct : is_child ? cc : is_rc ? cr : cs;
-      if (!insert_ok(ev.id, s) || j < 0) {
+      if (!insert_ok(ev.id(), s) || j < 0) {
         rc = CRR_INTERNAL_RETRY;
       } else if (grow && j >= cap) {
         rc = CRR_ERR_CAPACITY;
       } else {
         // the event's offset in its batch (IDs are consecutive: insert_ok), so the rows' batch IDs need no
         // walk back over the columns at the end
-        const u64 bdelta = (u64)ev.id - (u64)bfid;
+        const u64 bdelta = (u64)ev.id() - (u64)bfid;
         const u32 bd = bdelta < (u64)kStepMask ? (u32)bdelta : kStepMask;
         u32 nf = CRR_ROW_LIVE | ((u32)s << 8) |
                  (is_child ? (kStepMask << (8 + kStepBits)) | ((bd < kChildBatchNone ? bd : kChildBatchNone) << CHILD_BATCH_SHIFT)
@@ -1355,17 +1374,17 @@ struct CompactTables {
         if (is_act) {
           if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
           // not started: ScheduleToClose and ScheduleToStart
-          i64 ct = add_seconds(ev.ts, as.schedule_to_close);
+          i64 ct = add_seconds(ev.ts(), as.schedule_to_close);
           i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-          cand_min(ct, cy, add_seconds(ev.ts, as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+          cand_min(ct, cy, add_seconds(ev.ts(), as.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
           nf = CRR_ROW_LIVE | CRR_ROW_MAPPED | (as.has_retry_policy ? CRR_ROW_HAS_RETRY : 0u) | ((u32)cy << CF_CAND_SHIFT) |
                (bd << CF_BATCH_SHIFT);
-          M->a_key[j][t] = ev.key;
+          M->a_key[j][t] = ev.key();
           M->a_src[j][t] = (u32)s | (kStepMask << kStepBits) | (kStepMask << (2 * kStepBits));
           M->a_cand[j][t] = ct;
         } else if (is_timer) {
-          M->t_exp[j][t] = add_seconds(ev.ts, ev.ref);
-          M->t_key[j][t] = ev.key;
+          M->t_exp[j][t] = add_seconds(ev.ts(), ev.ref());
+          M->t_key[j][t] = ev.key();
         }
         fl[j * LANES] = nf;
         d = grow ? 1 : 0;
@@ -1373,17 +1392,17 @@ struct CompactTables {
     } else if (op == MOP_ACT_START) {  // :2254-2276
       rc = CRR_ERR_MISSING_ACTIVITY_INFO;
       // the rows keep only steps: a StartedID must be id0 + its step too (else the general path)
-      if (hit >= 0) rc = ev.id != id_at((u32)s) ? CRR_INTERNAL_RETRY : act_started(hit, ev, s);
+      if (hit >= 0) rc = ev.id() != id_at((u32)s) ? CRR_INTERNAL_RETRY : act_started(hit, ev, s);
     } else if (op == MOP_CHILD_START) {  // :3485-3507
       rc = CRR_ERR_MISSING_CHILD_INFO;
-      if (hit >= 0 && ev.id != id_at((u32)s)) {
+      if (hit >= 0 && ev.id() != id_at((u32)s)) {
         rc = CRR_INTERNAL_RETRY;
       } else if (hit >= 0) {
         const u32 f = fl[hit * LANES];
         fl[hit * LANES] = (f & ~(kStepMask << (8 + kStepBits))) | ((u32)s << (8 + kStepBits));
         rc = CRR_OK;
       }
-    } else if (hit >= 0 && ev.id != id_at((u32)s)) {  // MOP_ACT_CANCEL: CancelRequestID = id0 + step
+    } else if (hit >= 0 && ev.id() != id_at((u32)s)) {  // MOP_ACT_CANCEL: CancelRequestID = id0 + step
       rc = CRR_INTERNAL_RETRY;
     } else if (hit >= 0) {  // MOP_ACT_CANCEL (:2444-2467)
       M->a_fl[hit][t] |= CRR_ROW_CANCEL_REQUESTED;
@@ -1408,8 +1427,8 @@ struct CompactTables {
     const crr_activity_side sa = in->act_side[in->ev.aux[six]];
     i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
     i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-    cand_min(ct, cy, add_seconds(ev.ts, sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
-    if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts, sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
+    cand_min(ct, cy, add_seconds(ev.ts(), sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+    if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts(), sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
     M->a_cand[hit][t] = ct;
     M->a_fl[hit][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
     M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
@@ -2163,13 +2182,13 @@ struct LaneSource {
     Ev e;
     const i64 i = ix(step);
     e.et = et;
-    e.id = E.event_id[i];
-    e.ver = E.version[i];
-    e.ts = need::has(ts_mask, et) ? E.timestamp[i] : 0;
-    e.ref = need::has(need::kRef, et) ? E.ref[i] : 0;
-    e.key = need::has(need::kKey, et) ? E.key[i] : 0u;
-    e.aux = need::has(need::kAux, et) ? E.aux[i] : 0;
-    e.task = 0;
+    e.id_ = E.event_id[i];
+    e.ver_ = E.version[i];
+    e.ts_ = need::has(ts_mask, et) ? E.timestamp[i] : 0;
+    e.ref_ = need::has(need::kRef, et) ? E.ref[i] : 0;
+    e.key_ = need::has(need::kKey, et) ? E.key[i] : 0u;
+    e.aux_ = need::has(need::kAux, et) ? E.aux[i] : 0;
+    e.task_ = 0;
     return e;
   }
   // step 0: every column with both type bytes, no load waiting on another (one round trip)
@@ -2178,13 +2197,13 @@ struct LaneSource {
       const i64 i = ix(0);
       nx.et = E.etype[i];
       if (n > 1) et_nx = E.etype[ix(1)];
-      nx.id = E.event_id[i];
-      nx.ver = E.version[i];
-      nx.ts = E.timestamp[i];
-      nx.ref = E.ref[i];
-      nx.key = E.key[i];
-      nx.aux = E.aux[i];
-      nx.task = 0;
+      nx.id_ = E.event_id[i];
+      nx.ver_ = E.version[i];
+      nx.ts_ = E.timestamp[i];
+      nx.ref_ = E.ref[i];
+      nx.key_ = E.key[i];
+      nx.aux_ = E.aux[i];
+      nx.task_ = 0;
     }
   }
   __device__ __forceinline__ Ev next(i32 s) {
@@ -2200,16 +2219,23 @@ struct LaneSource {
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[ix(step)]; }
 };
 
-// One wavefront per workflow runs the state machine on wave-uniform values.  With the event fields read
-// out of the chunk by readlane (scalar registers), all of that state is scalar: ~265 SALU instructions and
-// a stream of scalar copies / spills per event, and a CU's one scalar issue slot per cycle is shared by
-// every wavefront on it -- the long tail was bound by it.  Broadcast into VGPRs instead (the type stays
-// scalar for the dispatch), the same work issues on the vector units: config 4 24.7 -> 17.1 ms.
+// One wavefront per workflow runs the state machine on wave-uniform values.  The workflow's events
+// stream through in 64-event chunks, one event per lane (one coalesced load per column, the next chunk
+// one chunk ahead).  Per chunk the version-history prologue of all 64 events runs lane-parallel
+// (replay_body); the transitions then walk the chunk one event at a time and read each field out of
+// its lane only where they use it (WaveEv): a MarkerRecorded reads nothing, a DecisionTaskCompleted
+// two fields, instead of every event broadcasting all seven.
+//   CRR_WAVE_FIELDS 0: __shfl (LDS crossbar) into VGPRs; 1: v_readlane into SGPRs; 2: v_readlane then a
+//   VGPR copy.  Config 4 (alternating A/B on one box): 13.4 / 13.9 / 13.9 ms, against 15.7 ms for the
+//   per-event prologue with every field broadcast.
+#ifndef CRR_WAVE_FIELDS
+#define CRR_WAVE_FIELDS 0
+#endif
 struct WaveSource {
   const crr_events& E;
   i64 begin, st;
   i32 n, lane;
-  Ev cur, nxt;
+  Ev cur, nxt;  // per lane: event c * 64 + lane of the current / next chunk
   __device__ __forceinline__ WaveSource(const crr_events& e, i64 b, i64 stride, i32 count)
       : E(e), begin(b), st(stride), n(count) {
     lane = (i32)(threadIdx.x & 63);
@@ -2218,37 +2244,52 @@ struct WaveSource {
     Ev e;
     const i32 s = c * 64 + lane;
     const i64 ix = begin + (i64)(s < n ? s : 0) * st;
-    e.et = E.etype[ix]; e.id = E.event_id[ix]; e.ver = E.version[ix]; e.ts = E.timestamp[ix];
-    e.task = E.task_id[ix]; e.ref = E.ref[ix]; e.key = E.key[ix]; e.aux = E.aux[ix];
+    e.et = E.etype[ix]; e.id_ = E.event_id[ix]; e.ver_ = E.version[ix]; e.ts_ = E.timestamp[ix];
+    e.task_ = 0; e.ref_ = E.ref[ix]; e.key_ = E.key[ix]; e.aux_ = E.aux[ix];
     return e;
   }
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[begin + (i64)step * st]; }
-  __device__ __forceinline__ static i64 rl64(i64 v, i32 l) {
-    const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
-    const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
-    return (i64)(((u64)hi << 32) | lo);
-  }
   __device__ __forceinline__ void start() {
     if (n > 0) cur = load_chunk(0);
     if (n > 64) nxt = load_chunk(1);
   }
-  __device__ __forceinline__ Ev next(i32 s) {
-    const i32 l = s & 63;
-    if (l == 0 && s > 0) {
-      cur = nxt;
-      const i32 c = (s >> 6) + 1;
-      if (c * 64 < n) nxt = load_chunk(c);
-    }
-    Ev e;
-    e.et = __builtin_amdgcn_readlane(cur.et, l);
-    // event fields broadcast into VGPRs (the state they update then lives in VGPRs: VALU work instead
-    // of scalar moves and SGPR spills); the type stays scalar for the dispatch
-    e.id = __shfl((long long)cur.id, l, 64); e.ver = __shfl((long long)cur.ver, l, 64);
-    e.ts = __shfl((long long)cur.ts, l, 64); e.task = __shfl((long long)cur.task, l, 64);
-    e.ref = __shfl((long long)cur.ref, l, 64);
-    e.key = (u32)__shfl((int)cur.key, l, 64); e.aux = __shfl((int)cur.aux, l, 64);
-    return e;
+  // chunk c (>= 1) becomes the current one
+  __device__ __forceinline__ void advance(i32 c) {
+    cur = nxt;
+    if ((c + 1) * 64 < n) nxt = load_chunk(c + 1);
   }
+};
+// lane l's value of a per-lane register, wave-uniform (CRR_WAVE_FIELDS above)
+__device__ __forceinline__ u32 lane_u32(u32 v, i32 l) {
+#if CRR_WAVE_FIELDS == 0
+  return (u32)__shfl((int)v, l, 64);
+#else
+  const u32 r = __builtin_amdgcn_readlane(v, l);
+#if CRR_WAVE_FIELDS == 2
+  u32 o;
+  asm("v_mov_b32 %0, %1" : "=v"(o) : "s"(r));
+  return o;
+#else
+  return r;
+#endif
+#endif
+}
+__device__ __forceinline__ i64 lane_i64(i64 v, i32 l) {
+  const u32 lo = lane_u32((u32)(u64)v, l), hi = lane_u32((u32)((u64)v >> 32), l);
+  return (i64)(((u64)hi << 32) | lo);
+}
+// event l of the current chunk, each field read out of lane l where a transition uses it
+struct WaveEv {
+  const Ev& C;
+  i32 l;
+  u32 et;
+  __device__ __forceinline__ i64 id() const { return lane_i64(C.id_, l); }
+  __device__ __forceinline__ i64 ver() const { return lane_i64(C.ver_, l); }
+  __device__ __forceinline__ i64 ts() const { return lane_i64(C.ts_, l); }
+  __device__ __forceinline__ i64 task() const { return 0; }
+  __device__ __forceinline__ i64 ref() const { return lane_i64(C.ref_, l); }
+  __device__ __forceinline__ u32 key() const { return lane_u32(C.key_, l); }
+  __device__ __forceinline__ i32 aux() const { return (i32)lane_u32((u32)C.aux_, l); }
 };
 
 // ---------------------------------------------------------------------------------------------------
@@ -2353,23 +2394,23 @@ __device__ __forceinline__ void close_tasks(Lane& L, const Geo& G, const TaskSin
 
 // A map operation through the policy's per-operation methods (a policy may fuse them instead:
 // P::kFusedMapOps, P::map_op)
-template <class P>
-__device__ __forceinline__ int map_op_by_method(P& T, Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s,
+template <class P, class EV>
+__device__ __forceinline__ int map_op_by_method(P& T, Lane& L, const Geo& G, u32 op, const EV& ev, i32 s,
                                                 i64 batch_first_id, const crr_activity_side& as) {
   switch (op) {
     case MOP_ACT_INSERT: return T.act_insert(L, G, activity_row(ev, s, batch_first_id, as));
-    case MOP_ACT_START: return T.act_start(L, G, ev.ref, ev.id, ev.ver, s, ev.ts);
-    case MOP_ACT_DELETE: T.act_delete(L, G, ev.ref); return CRR_OK;
-    case MOP_ACT_CANCEL: T.act_cancel(L, G, ev.key, ev.id, ev.ver, s); return CRR_OK;
+    case MOP_ACT_START: return T.act_start(L, G, ev.ref(), ev.id(), ev.ver(), s, ev.ts());
+    case MOP_ACT_DELETE: T.act_delete(L, G, ev.ref()); return CRR_OK;
+    case MOP_ACT_CANCEL: T.act_cancel(L, G, ev.key(), ev.id(), ev.ver(), s); return CRR_OK;
     case MOP_TIMER_START: return T.timer_start(L, G, timer_row(ev, s));
-    case MOP_TIMER_DELETE: T.timer_delete(L, G, ev.key); return CRR_OK;
+    case MOP_TIMER_DELETE: T.timer_delete(L, G, ev.key()); return CRR_OK;
     case MOP_CHILD_INSERT: return T.child_insert(L, G, child_row(ev, s, batch_first_id));
-    case MOP_CHILD_START: return T.child_start(L, G, ev.ref, ev.id, s);
-    case MOP_CHILD_DELETE: T.child_delete(L, G, ev.ref); return CRR_OK;
+    case MOP_CHILD_START: return T.child_start(L, G, ev.ref(), ev.id(), s);
+    case MOP_CHILD_DELETE: T.child_delete(L, G, ev.ref()); return CRR_OK;
     case MOP_RC_INSERT: return T.init_insert(L, G, true, initiated_row(ev, s, batch_first_id));
-    case MOP_RC_DELETE: T.init_delete(L, G, true, ev.ref); return CRR_OK;
+    case MOP_RC_DELETE: T.init_delete(L, G, true, ev.ref()); return CRR_OK;
     case MOP_SIG_INSERT: return T.init_insert(L, G, false, initiated_row(ev, s, batch_first_id));
-    case MOP_SIG_DELETE: T.init_delete(L, G, false, ev.ref); return CRR_OK;
+    case MOP_SIG_DELETE: T.init_delete(L, G, false, ev.ref()); return CRR_OK;
     default: return CRR_OK;
   }
 }
@@ -2380,8 +2421,8 @@ struct FusedMapOps<P, decltype((void)P::kFusedMapOps)> { static constexpr bool v
 
 // The map operation an event's transition performs, then what the transition does after it (its task,
 // a late domain check).
-template <class P>
-__device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, const u32 op, const Ev& ev, const i32 s,
+template <class P, class EV>
+__device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, const u32 op, const EV& ev, const i32 s,
                                                 const i64 batch_first_id, const crr_activity_side& as, const TaskSink& K) {
   if (op == MOP_NONE) return CRR_OK;
   int rc;
@@ -2389,32 +2430,32 @@ __device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, con
   else rc = map_op_by_method(T, L, G, op, ev, s, batch_first_id, as);
   if (rc) return rc;
   if (op == MOP_ACT_INSERT) {
-    K.add(L, G, CRR_TASK_ACTIVITY, 0, ev.ver, 0, ev.id, 0, s);  // GenerateActivityTransferTasks
+    K.add(L, G, CRR_TASK_ACTIVITY, 0, ev.ver(), 0, ev.id(), 0, s);  // GenerateActivityTransferTasks
   } else if (op == MOP_CHILD_INSERT) {
-    K.add(L, G, CRR_TASK_START_CHILD, 0, ev.ver, 0, ev.id, 0, s);  // GenerateChildWorkflowTasks
+    K.add(L, G, CRR_TASK_START_CHILD, 0, ev.ver(), 0, ev.id(), 0, s);  // GenerateChildWorkflowTasks
   } else if (op == MOP_RC_INSERT || op == MOP_SIG_INSERT) {
     // Generate{RequestCancel,Signal}ExternalTasks -> getTargetDomainID (task_generator.go:556-559, :604-607)
-    if (ev.aux == CRR_DOMAIN_UNKNOWN) return CRR_ERR_DOMAIN_NOT_FOUND;
-    K.add(L, G, op == MOP_RC_INSERT ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0, ev.ver, 0, ev.id, 0, s);
+    if (ev.aux() == CRR_DOMAIN_UNKNOWN) return CRR_ERR_DOMAIN_NOT_FOUND;
+    K.add(L, G, op == MOP_RC_INSERT ? CRR_TASK_CANCEL_EXECUTION : CRR_TASK_SIGNAL_EXECUTION, 0, ev.ver(), 0, ev.id(), 0, s);
   }
   return CRR_OK;
 }
 
 // One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
 // code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
-template <class P>
+template <class P, class EV>
 __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outputs& out, Lane& L, const Geo& G, P& T,
-                                           const Ev& ev, const i32 s, const i32 t, const i64 batch_first_id,
+                                           const EV& ev, const i32 s, const i32 t, const i64 batch_first_id,
                                            const i64 now_ns, const TaskSink& K, const i32 retention_days) {
-  const i64 id = ev.id;
-  const i64 ver = ev.ver;
+  const i64 id = ev.id();
+  const i64 ver = ev.ver();
   u32 op = MOP_NONE;
   crr_activity_side as{};
 #define FAIL(code, step) return (code)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) return rc_; } while (0)
     switch (t) {
       case CRR_EV_WORKFLOW_EXECUTION_STARTED: {  // :132-183 -> mutable_state_builder.go:1751-1829
-        const crr_start_side ss = in.start_side[ev.aux];
+        const crr_start_side ss = in.start_side[ev.aux()];
         if (ss.parent_domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         L.decision_start_to_close = ss.decision_start_to_close;
         L.start_src = s;
@@ -2441,7 +2482,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         // GenerateRecordWorkflowStartedTasks / GenerateWorkflowStartTasks (task_generator.go:143-166, :301-313)
         K.add(L, G, CRR_TASK_RECORD_WORKFLOW_STARTED, 0, ver, 0, 0, 0, s);
         if (K.on) {
-          i64 vis = add_seconds(ev.ts, (i64)ss.workflow_timeout + (i64)ss.first_decision_backoff);
+          i64 vis = add_seconds(ev.ts(), (i64)ss.workflow_timeout + (i64)ss.first_decision_backoff);
           if (ss.attempt > 0 && L.expiration_ns != 0 && vis > L.expiration_ns) vis = L.expiration_ns;
           K.add(L, G, CRR_TASK_WORKFLOW_TIMEOUT, 0, ver, vis, 0, 0, s);
         }
@@ -2451,35 +2492,35 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
               ss.initiator != CRR_INITIATOR_CRON)
             FAIL(CRR_ERR_BAD_INITIATOR, s);
           K.add(L, G, CRR_TASK_WORKFLOW_BACKOFF, ss.initiator == CRR_INITIATOR_RETRY_POLICY ? CRR_BACKOFF_RETRY : CRR_BACKOFF_CRON,
-                ver, add_seconds(ev.ts, ss.first_decision_backoff), 0, 0, s);
+                ver, add_seconds(ev.ts(), ss.first_decision_backoff), 0, 0, s);
         }
         L.token_src = 1;  // SetHistoryTree(runID) (:367-376)
         break;
       }
       case CRR_EV_DECISION_TASK_SCHEDULED: {  // :185-208 -> decision_task_manager.go:129-166
         if (L.state != CRR_STATE_ZOMBIE) CHECK(update_state(L, CRR_STATE_RUNNING, CRR_CLOSE_NONE));
-        update_decision(L, ver, id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, ev.aux, ev.ref, 0, ev.ts, ev.ts);
+        update_decision(L, ver, id, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, ev.aux(), ev.ref(), 0, ev.ts(), ev.ts());
         K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, s);  // GenerateDecisionScheduleTasks
         break;
       }
       case CRR_EV_DECISION_TASK_STARTED: {  // :210-228 -> decision_task_manager.go:199-242
-        if (ev.ref != L.decision_schedule_id) FAIL(CRR_ERR_DECISION_NOT_FOUND, s);
-        update_decision(L, ver, ev.ref, id, s, L.decision_timeout, 0, ev.ts, L.decision_scheduled_ts,
+        if (ev.ref() != L.decision_schedule_id) FAIL(CRR_ERR_DECISION_NOT_FOUND, s);
+        update_decision(L, ver, ev.ref(), id, s, L.decision_timeout, 0, ev.ts(), L.decision_scheduled_ts,
                         L.decision_orig_scheduled_ts);
         // GenerateDecisionStartTasks (task_generator.go:352-388)
         K.add(L, G, CRR_TASK_DECISION_TIMEOUT, CRR_TIMEOUT_START_TO_CLOSE, L.decision_version,
-              add_seconds(ev.ts, L.decision_timeout), L.decision_schedule_id, (i32)L.decision_attempt, s);
+              add_seconds(ev.ts(), L.decision_timeout), L.decision_schedule_id, (i32)L.decision_attempt, s);
         break;
       }
       case CRR_EV_DECISION_TASK_COMPLETED: {  // :230-235 -> decision_task_manager.go:244-249, :827-838
         update_decision(L, CRR_EMPTY_VERSION, CRR_EMPTY_EVENT_ID, CRR_EMPTY_EVENT_ID, CRR_SRC_EMPTY_UUID, 0, 0, 0, 0,
                         L.decision_orig_scheduled_ts);  // DeleteDecision
-        L.last_processed_event = ev.ref;
-        if (ev.key != 0 && !T.rp_has(L, G, ev.key)) {  // addBinaryCheckSumIfNotExists (:1911-1974)
+        L.last_processed_event = ev.ref();
+        if (ev.key() != 0 && !T.rp_has(L, G, ev.key())) {  // addBinaryCheckSumIfNotExists (:1911-1974)
           crr_reset_point_row rp;
           rp.src = s;
           rp.prev_index = -1;
-          rp.key = ev.key;
+          rp.key = ev.key();
           const bool resettable = L.n_child == 0 && L.n_rc == 0 && L.n_sig == 0;  // CheckResettable (:1977-1994)
           rp.flags = CRR_ROW_LIVE | (resettable ? CRR_ROW_RESETTABLE : 0u);
           CHECK(T.rp_push(L, G, rp));
@@ -2493,7 +2534,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
           K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, L.start_src);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
-        as = in.act_side[ev.aux];
+        as = in.act_side[ev.aux()];
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         op = MOP_ACT_INSERT;  // then GenerateActivityTransferTasks (below)
         break;
@@ -2518,7 +2559,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         op = MOP_TIMER_DELETE;
         break;
       case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:  // :366-381 -> :3417-3453
-        if (ev.aux == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
+        if (ev.aux() == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         op = MOP_CHILD_INSERT;  // then GenerateChildWorkflowTasks (below)
         break;
       case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED:  // :390-395 -> :3485-3507
@@ -2564,11 +2605,11 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
                                                                 : CRR_CLOSE_TERMINATED;
         CHECK(update_state(L, CRR_STATE_COMPLETED, cs));
         L.completion_event_batch_id = batch_first_id;
-        close_tasks(L, G, K, ver, ev.ts, s, retention_days);
+        close_tasks(L, G, K, ver, ev.ts(), s, retention_days);
         break;
       }
       case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW: {  // :587-627 -> :3366-3382
-        const i32 nr = ev.aux;
+        const i32 nr = ev.aux();
         if (nr >= 0) {
           if ((u32)nr >= in.n_wf) FAIL(CRR_ERR_NEW_RUN_MISSING, s);
           const int nst = out.exec[nr].status;  // written by the phase-0 launches
@@ -2576,7 +2617,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
         }
         CHECK(update_state(L, CRR_STATE_COMPLETED, CRR_CLOSE_CONTINUED_AS_NEW));
         L.completion_event_batch_id = batch_first_id;
-        close_tasks(L, G, K, ver, ev.ts, s, retention_days);
+        close_tasks(L, G, K, ver, ev.ts(), s, retention_days);
         break;
       }
       case CRR_EV_REQUEST_CANCEL_ACTIVITY_TASK_FAILED:  // :339-340
@@ -2651,13 +2692,13 @@ __device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr
   // DecisionTaskScheduled: UpdateWorkflowStateCloseStatus(Running, None) unless Zombie (:185-208)
   if (is_ds) rc = L.state == CRR_STATE_COMPLETED ? (int)CRR_ERR_INVALID_STATE_TRANSITION
                 : (u32)L.state > (u32)CRR_STATE_VOID ? (int)CRR_ERR_UNKNOWN_WORKFLOW_STATE : (int)CRR_OK;
-  if (is_dt && ev.ref != L.decision_schedule_id) rc = CRR_ERR_DECISION_NOT_FOUND;  // :210-228
+  if (is_dt && ev.ref() != L.decision_schedule_id) rc = CRR_ERR_DECISION_NOT_FOUND;  // :210-228
   crr_activity_side as{};
   if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {  // :283-295
-    as = in.act_side[ev.aux];
+    as = in.act_side[ev.aux()];
     if (as.domain_status == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
   }
-  if (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED && ev.aux == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
+  if (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED && ev.aux() == CRR_DOMAIN_UNKNOWN) rc = CRR_ERR_DOMAIN_NOT_FOUND;
   if (rc) return rc;
   // the workflow state of DecisionTaskScheduled
   const bool run = is_ds && L.state != CRR_STATE_ZOMBIE;
@@ -2670,25 +2711,25 @@ __device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr
   const bool tr = is_df && a1 != 0;  // the transient decision is scheduled
   const bool dec = is_ds || is_dt || is_dc || is_df;
   if (dec) {
-    const i64 nv = (is_ds || is_dt) ? ev.ver : tr ? L.current_version : (i64)CRR_EMPTY_VERSION;
-    const i64 nsched = is_ds ? ev.id : is_dt ? ev.ref : tr ? L.next_event_id : (i64)CRR_EMPTY_EVENT_ID;
-    const i64 nstarted = is_dt ? ev.id : (i64)CRR_EMPTY_EVENT_ID;
+    const i64 nv = (is_ds || is_dt) ? ev.ver() : tr ? L.current_version : (i64)CRR_EMPTY_VERSION;
+    const i64 nsched = is_ds ? ev.id() : is_dt ? ev.ref() : tr ? L.next_event_id : (i64)CRR_EMPTY_EVENT_ID;
+    const i64 nstarted = is_dt ? ev.id() : (i64)CRR_EMPTY_EVENT_ID;
     const i32 nreq = is_dt ? s : (i32)CRR_SRC_EMPTY_UUID;
-    const i32 nto = is_ds ? ev.aux : is_dt ? L.decision_timeout : tr ? L.decision_start_to_close : 0;
-    const i64 natt = is_ds ? ev.ref : is_df ? a1 : 0;
-    const i64 nsts = is_dt ? ev.ts : 0;
-    const i64 nscts = is_ds ? ev.ts : is_dt ? L.decision_scheduled_ts : is_df ? now_ns : 0;
-    const i64 nots = is_ds ? ev.ts : (is_dt || is_dc) ? L.decision_orig_scheduled_ts : 0;
+    const i32 nto = is_ds ? ev.aux() : is_dt ? L.decision_timeout : tr ? L.decision_start_to_close : 0;
+    const i64 natt = is_ds ? ev.ref() : is_df ? a1 : 0;
+    const i64 nsts = is_dt ? ev.ts() : 0;
+    const i64 nscts = is_ds ? ev.ts() : is_dt ? L.decision_scheduled_ts : is_df ? now_ns : 0;
+    const i64 nots = is_ds ? ev.ts() : (is_dt || is_dc) ? L.decision_orig_scheduled_ts : 0;
     update_decision(L, nv, nsched, nstarted, nreq, nto, natt, nsts, nscts, nots);
   }
-  L.last_processed_event = is_dc ? ev.ref : L.last_processed_event;
+  L.last_processed_event = is_dc ? ev.ref() : L.last_processed_event;
   L.signal_count = (i32)((u32)L.signal_count + (t == CRR_EV_WORKFLOW_EXECUTION_SIGNALED ? 1u : 0u));  // :497-502
   L.flags |= t == CRR_EV_WORKFLOW_EXECUTION_CANCEL_REQUESTED ? (u32)CRR_EXEC_CANCEL_REQUESTED : 0u;  // :504-509
-  if (is_dc && ev.key != 0 && !T.rp_has(L, G, ev.key)) {  // addBinaryCheckSumIfNotExists (:1911-1974)
+  if (is_dc && ev.key() != 0 && !T.rp_has(L, G, ev.key())) {  // addBinaryCheckSumIfNotExists (:1911-1974)
     crr_reset_point_row rp;
     rp.src = s;
     rp.prev_index = -1;
-    rp.key = ev.key;
+    rp.key = ev.key();
     const bool resettable = L.n_child == 0 && L.n_rc == 0 && L.n_sig == 0;  // CheckResettable (:1977-1994)
     rp.flags = CRR_ROW_LIVE | (resettable ? CRR_ROW_RESETTABLE : 0u);
     rc = T.rp_push(L, G, rp);
@@ -2785,13 +2826,89 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   }
 
   src.start();
+  if constexpr (std::is_same<SRC, WaveSource>::value) {
+    // Wavefront per workflow, a 64-event chunk at a time (lane l: event c0 + l).  The prologue of
+    // :98-129 for every event of the chunk runs lane-parallel: each lane checks its (ID, version)
+    // against its predecessor's (lane 0 against the state carried in), the version-history items it
+    // closes are written at once, and the first lane whose check fails bounds the walk.  The walk
+    // then runs the dispatch and the batch epilogue one event at a time.  The prologue does not read
+    // the workflow state except through `completed` (UpdateCurrentVersion), which the walk applies
+    // per event, and the VH_EMPTY check (only the first event of a history with no items can meet it:
+    // lane 0 of the first chunk, against the loaded state).
+    const i32 lane = src.lane;
+    const u64 below = lane == 0 ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
+    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {
+      if (c0) src.advance(c0 >> 6);
+      const Ev& C = src.cur;
+      const i32 cnt = n_ev - c0 < 64 ? n_ev - c0 : 64;
+      const bool valid = lane < cnt;
+      i64 pid = __shfl_up((long long)C.id_, 1, 64), pver = __shfl_up((long long)C.ver_, 1, 64);
+      if (lane == 0) { pid = L.vh_last_id; pver = L.vh_last_ver; }
+      const bool first = lane == 0 && L.vh_n == 0;
+      const bool grow = !first && C.ver_ > pver;
+      const u64 gm = __builtin_amdgcn_ballot_w64(valid && (first || grow));
+      const i32 nb = L.vh_n + __builtin_popcountll(gm & below);  // items before this event's
+      // :98-100 empty batch; UpdateCurrentVersion's VH_EMPTY (mutable_state_builder.go:495-533)
+      const i32 rc0 = c0 + lane == empty_at ? (i32)CRR_ERR_EMPTY_HISTORY
+                      : (first && L.state == CRR_STATE_COMPLETED) ? (i32)CRR_ERR_VH_EMPTY : 0;
+      // :123-128 AddOrUpdateItem(NewVersionHistoryItem(event.ID, event.Version)) (versionHistory.go:32-46, :193-226)
+      const i32 vh_rc = (C.id_ < 0 || (C.ver_ < 0 && C.ver_ != CRR_EMPTY_VERSION)) ? (i32)CRR_ERR_VH_INVALID_ITEM
+                        : first ? (G.vh_cap < 1 ? (i32)CRR_ERR_CAPACITY : 0)
+                        : C.ver_ < pver ? (i32)CRR_ERR_VH_LOWER_VERSION
+                        : C.id_ <= pid ? (i32)CRR_ERR_VH_EVENT_ID_NOT_INCREASING
+                        : (grow && nb >= G.vh_cap) ? (i32)CRR_ERR_CAPACITY : 0;
+      const i32 prc = !valid ? 0 : rc0 ? rc0 : vh_rc;
+      const u64 em = __builtin_amdgcn_ballot_w64(prc != 0);
+      const i32 lim = em ? (i32)__builtin_ctzll(em) : cnt;  // events before the first failing prologue
+      if (valid && grow && lane < lim) {  // the item this event's version change closes
+        crr_vh_item* it = G.vh(nb - 1);
+        it->event_id = pid;
+        it->version = pver;
+      }
+      const i32 vh_n0 = L.vh_n;
+      // the version-history state after event k of the chunk (k >= 0)
+#define WAVE_VH_AFTER(k)                                                                          \
+      do {                                                                                        \
+        L.vh_n = vh_n0 + __builtin_popcountll(gm & (~0ull >> (63 - (k))));                        \
+        L.vh_last_id = lane_i64(C.id_, (k));                                                      \
+        L.vh_last_ver = lane_i64(C.ver_, (k));                                                    \
+      } while (0)
+      for (i32 j = 0; j < lim; ++j) {
+        const i32 s = c0 + j;
+        const WaveEv ev{C, j, (u32)__builtin_amdgcn_readlane(C.et, j)};
+        const u32 et = ev.et;
+        if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = ev.id();  // firstEvent := history[0] (:101)
+        // :112 UpdateCurrentVersion: a closed workflow keeps its version history's last version
+        L.current_version = L.state == CRR_STATE_COMPLETED ? lane_i64(pver, j) : ev.ver();
+        last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
+        const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base, (i32)(et & CRR_ETYPE_MASK), batch_first_id,
+                                   now_ns, K, retention_days);
+        if (rc) {
+          WAVE_VH_AFTER(j);
+          FAIL(rc, s);
+        }
+        if (et & CRR_ETYPE_BATCH_LAST) {
+          T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
+          L.last_first_event_id = batch_first_id;  // :642-643
+          L.next_event_id = ev.id() + 1;
+        }
+      }
+      if (lim > 0) WAVE_VH_AFTER(lim - 1);
+      if (lim < cnt) {  // event c0 + lim fails its prologue; a version-history error follows UpdateCurrentVersion
+        if (__builtin_amdgcn_readlane((u32)rc0, lim) == 0)
+          L.current_version = L.state == CRR_STATE_COMPLETED ? lane_i64(pver, lim) : lane_i64(C.ver_, lim);
+        FAIL((i32)__builtin_amdgcn_readlane((u32)prc, lim), c0 + lim);
+      }
+#undef WAVE_VH_AFTER
+    }
+  } else
   for (i32 s = 0; s < n_ev; ++s) {
     // one loop exit for the whole prologue: the checks become a select chain (no divergent branch
     // per check), and on success vh_last = (id, ver) in every case (new item, same version, first).
     const Ev ev = src.next(s);
     const u32 et = ev.et;
-    const i64 id = ev.id;
-    const i64 ver = ev.ver;
+    const i64 id = ev.id();
+    const i64 ver = ev.ver();
     const i32 t = et & CRR_ETYPE_MASK;
     if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = id;  // firstEvent := history[0] (:101)
     {
@@ -2828,7 +2945,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       int rc;
       const i32 tu = uniform32(t);
       const i32 ps = s + L.src_base;  // provenance step of the event (rows' *_src)
-      if (std::is_same<SRC, WaveSource>::value || __builtin_amdgcn_ballot_w64(t != tu) == 0)  // WaveSource: readlane, uniform
+      if (__builtin_amdgcn_ballot_w64(t != tu) == 0)
         rc = apply_event(in, out, L, G, T, ev, ps, tu, batch_first_id, now_ns,
                          K, retention_days);
       else if (LaneDispatch<P>::value)
@@ -2883,6 +3000,8 @@ done_events:
   const bool want_crc = L.status == CRR_OK;
   TokenWords TW;
   TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
+  // the wave path's items were written by the lanes of their events; the checksum reads them all
+  if constexpr (std::is_same<SRC, WaveSource>::value) wave_sync_global();
   if (L.vh_n > 0) {
     crr_vh_item* it = G.vh(L.vh_n - 1);
     it->event_id = L.vh_last_id;

@@ -2873,25 +2873,184 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         L.vh_last_id = lane_i64(C.id_, (k));                                                      \
         L.vh_last_ver = lane_i64(C.ver_, (k));                                                    \
       } while (0)
-      for (i32 j = 0; j < lim; ++j) {
+      const u32 tl = C.et & CRR_ETYPE_MASK;
+      const bool live = valid && lane < lim;
+      auto le = [](i32 k) -> u64 { return k < 0 ? 0ull : k >= 63 ? ~0ull : (2ull << k) - 1; };  // lanes <= k
+      auto last_in = [](u64 m) -> i32 { return m ? 63 - (i32)__builtin_clzll(m) : -1; };
+      // A chunk without the rare types (start, closes, continue-as-new, unknown) on a created or running
+      // workflow, with no task emission, is `fast`: its decision events, signals, cancel requests and no-op
+      // types are resolved lane-parallel, and the walk visits only the map operations, the reset points of
+      // DecisionTaskCompleted and the batch ends whose epilogue has work.  Otherwise it visits every event.
+      const bool fast = !K.on && (L.state == CRR_STATE_CREATED || L.state == CRR_STATE_RUNNING) &&
+                        __builtin_amdgcn_ballot_w64(live && ((kLaneRare >> tl) & 1)) == 0;
+      u64 vm = le(lim - 1), OPS = 0;  // lanes the walk visits; of those, the ones it applies
+      i32 stop = lim;
+      if (fast) {
+        const bool is_ds = tl == CRR_EV_DECISION_TASK_SCHEDULED, is_dt = tl == CRR_EV_DECISION_TASK_STARTED;
+        const bool is_dc = tl == CRR_EV_DECISION_TASK_COMPLETED;
+        const bool is_df = tl == CRR_EV_DECISION_TASK_TIMED_OUT || tl == CRR_EV_DECISION_TASK_FAILED;
+        const u64 DM = __builtin_amdgcn_ballot_w64(live && (is_ds || is_dt || is_dc || is_df));  // decision events
+        const u64 DA = __builtin_amdgcn_ballot_w64(live && (is_ds || is_dt || is_dc));  // set the attempt
+        const u64 BL = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_LAST));
+        constexpr u64 mw0 = mop_word(0), mw1 = mop_word(1), mw2 = mop_word(2);
+        const u32 mop = (u32)((tl < 16 ? mw0 : tl < 32 ? mw1 : mw2) >> (4 * (tl & 15))) & 15u;
+        const u64 MP = __builtin_amdgcn_ballot_w64(live && mop != MOP_NONE);       // map operations
+        const u64 RP = __builtin_amdgcn_ballot_w64(live && is_dc && C.key_ != 0);  // addBinaryCheckSumIfNotExists
+        // FailDecision's attempt (decision_task_manager.go:643-676): the last attempt-setting decision
+        // event's (Scheduled: its own; Started / Completed: 0) plus one per failure since
+        const i32 u = last_in(DA & below);
+        const i64 ubase = __shfl((long long)(is_ds ? C.ref_ : 0), u < 0 ? lane : u, 64);
+        const i64 att = (u < 0 ? L.decision_attempt : ubase) + __builtin_popcountll(DM & below & ~le(u)) + 1;
+        // NextEventID when the event is applied: the last batch end's ID + 1 (:642-643)
+        const i32 bl = last_in(BL & below);
+        const i64 nei = bl < 0 ? L.next_event_id : (i64)__shfl((long long)C.id_, bl < 0 ? lane : bl, 64) + 1;
+        // the decision's ScheduleID after each decision event, and DecisionTaskStarted's check (:210-228)
+        const i64 dsched = is_ds ? C.id_ : is_dt ? C.ref_ : (is_df && att != 0) ? nei : (i64)CRR_EMPTY_EVENT_ID;
+        const i32 pr = last_in(DM & below);
+        const i64 psched = (i64)__shfl((long long)dsched, pr < 0 ? lane : pr, 64);
+        const u64 DF = __builtin_amdgcn_ballot_w64(live && is_dt && C.ref_ != (pr < 0 ? L.decision_schedule_id : psched));
+        stop = DF ? (i32)__builtin_ctzll(DF) : lim;
+        // batch ends whose epilogue has work: a map operation in the batch (or dirty maps carried in)
+        const u64 seg = le(lane) & ~le(bl);
+        const bool carried_dirty = T.dirty_act || T.dirty_timer;
+        const u64 EB = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_LAST) &&
+                                                   ((MP & seg) != 0 || (bl < 0 && carried_dirty)));
+        OPS = MP | RP;
+        vm = (OPS | EB) & le(stop - 1);
+      }
+      const u64 BF = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_FIRST));
+      // The walk.  A visited DecisionTaskCompleted runs its whole transition: its decision update is
+      // overwritten by the chunk's (below), which covers it, and its reset point is the walk's part.
+      i32 wfail = -1;
+      int wrc = CRR_OK;
+      while (vm) {
+        const i32 j = (i32)__builtin_ctzll(vm);
+        vm &= vm - 1;
         const i32 s = c0 + j;
         const WaveEv ev{C, j, (u32)__builtin_amdgcn_readlane(C.et, j)};
         const u32 et = ev.et;
-        if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = ev.id();  // firstEvent := history[0] (:101)
-        // :112 UpdateCurrentVersion: a closed workflow keeps its version history's last version
-        L.current_version = L.state == CRR_STATE_COMPLETED ? lane_i64(pver, j) : ev.ver();
-        last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
-        const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base, (i32)(et & CRR_ETYPE_MASK), batch_first_id,
-                                   now_ns, K, retention_days);
-        if (rc) {
-          WAVE_VH_AFTER(j);
-          FAIL(rc, s);
+        i64 bfid = batch_first_id;
+        if (!fast) {
+          if (et & CRR_ETYPE_BATCH_FIRST) batch_first_id = ev.id();  // firstEvent := history[0] (:101)
+          bfid = batch_first_id;
+          // :112 UpdateCurrentVersion: a closed workflow keeps its version history's last version
+          L.current_version = L.state == CRR_STATE_COMPLETED ? lane_i64(pver, j) : ev.ver();
+          last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
+        } else {
+          const i32 bf = last_in(BF & le(j));
+          if (bf >= 0) bfid = lane_i64(C.id_, bf);
+        }
+        if (!fast || ((OPS >> j) & 1)) {
+          const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base, (i32)(et & CRR_ETYPE_MASK), bfid, now_ns,
+                                     K, retention_days);
+          if (rc) {
+            wfail = j;
+            wrc = rc;
+            break;
+          }
         }
         if (et & CRR_ETYPE_BATCH_LAST) {
           T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks
-          L.last_first_event_id = batch_first_id;  // :642-643
-          L.next_event_id = ev.id() + 1;
+          if (!fast) {
+            L.last_first_event_id = batch_first_id;  // :642-643
+            L.next_event_id = ev.id() + 1;
+          }
         }
+      }
+      if (fast) {
+        // what the events [0, end) of the chunk did besides the walk (a failing DecisionTaskCompleted has
+        // applied its decision update before its reset point failed)
+        const i32 end = wfail >= 0 ? wfail : stop;
+        const i32 dend = (wfail >= 0 && (__builtin_amdgcn_readlane(tl, wfail) == CRR_EV_DECISION_TASK_COMPLETED)) ? wfail + 1 : end;
+        const bool lv = live && lane < dend;  // masks of their own, not the walk's: short live ranges
+        const bool is_ds = tl == CRR_EV_DECISION_TASK_SCHEDULED, is_dt = tl == CRR_EV_DECISION_TASK_STARTED;
+        const bool is_dc = tl == CRR_EV_DECISION_TASK_COMPLETED;
+        const bool is_df = tl == CRR_EV_DECISION_TASK_TIMED_OUT || tl == CRR_EV_DECISION_TASK_FAILED;
+        const u64 DM = __builtin_amdgcn_ballot_w64(lv && (is_ds || is_dt || is_dc || is_df));
+        const u64 DS = __builtin_amdgcn_ballot_w64(lv && is_ds), DT = __builtin_amdgcn_ballot_w64(lv && is_dt);
+        const u64 DC = __builtin_amdgcn_ballot_w64(lv && is_dc);
+        const u64 BL = __builtin_amdgcn_ballot_w64(lv && (C.et & CRR_ETYPE_BATCH_LAST));
+        const u64 E = le(end - 1);
+        const i32 p = last_in(DM);
+        if (p >= 0) {  // the last decision event's UpdateDecision (decision_task_manager.go:697-721)
+          const i32 tp = (i32)__builtin_amdgcn_readlane(tl, p);
+          auto att_at = [&](i32 x) -> i64 {  // a failed / timed-out decision's attempt
+            const i32 v = last_in((DS | DT | DC) & le(x - 1));
+            const i64 base = v < 0 ? L.decision_attempt : ((DS >> v) & 1) ? lane_i64(C.ref_, v) : 0;
+            return base + __builtin_popcountll(DM & le(x) & ~le(v));
+          };
+          i64 nv, ns, nst = CRR_EMPTY_EVENT_ID, natt = 0, nsts = 0, nscts = 0, nots = 0;
+          i32 nreq = CRR_SRC_EMPTY_UUID, nto = 0;
+          if (tp == CRR_EV_DECISION_TASK_SCHEDULED) {  // :129-166
+            nv = lane_i64(C.ver_, p); ns = lane_i64(C.id_, p); nto = (i32)lane_u32((u32)C.aux_, p);
+            natt = lane_i64(C.ref_, p); nscts = lane_i64(C.ts_, p); nots = nscts;
+          } else if (tp == CRR_EV_DECISION_TASK_STARTED || tp == CRR_EV_DECISION_TASK_COMPLETED) {
+            // the original scheduled time: the last Scheduled (its time) or failure (0) before it
+            const i32 r = last_in((DM & ~(DT | DC)) & le(p - 1));
+            nots = r < 0 ? L.decision_orig_scheduled_ts : ((DS >> r) & 1) ? lane_i64(C.ts_, r) : 0;
+            if (tp == CRR_EV_DECISION_TASK_STARTED) {  // :199-242
+              // the timeout and scheduled time: the last decision event before it that sets them
+              const i32 q = last_in(DM & ~DT & le(p - 1));
+              if (q < 0) {
+                nto = L.decision_timeout;
+                nscts = L.decision_scheduled_ts;
+              } else if ((DS >> q) & 1) {
+                nto = (i32)lane_u32((u32)C.aux_, q);
+                nscts = lane_i64(C.ts_, q);
+              } else if ((DC >> q) & 1) {
+                nto = 0;
+                nscts = 0;
+              } else {  // failed / timed out: the transient decision's
+                nto = att_at(q) != 0 ? L.decision_start_to_close : 0;
+                nscts = now_ns;
+              }
+              nv = lane_i64(C.ver_, p); ns = lane_i64(C.ref_, p); nst = lane_i64(C.id_, p);
+              nreq = c0 + p + L.src_base; nsts = lane_i64(C.ts_, p);
+            } else {  // DeleteDecision (:244-249, :827-838)
+              nv = CRR_EMPTY_VERSION; ns = CRR_EMPTY_EVENT_ID;
+            }
+          } else {  // FailDecision + the transient decision (:643-676, :168-197)
+            natt = att_at(p);
+            const bool tr = natt != 0;
+            const i32 b = last_in(BL & le(p - 1));
+            nv = tr ? lane_i64(C.ver_, p) : (i64)CRR_EMPTY_VERSION;
+            ns = !tr ? (i64)CRR_EMPTY_EVENT_ID : b < 0 ? L.next_event_id : lane_i64(C.id_, b) + 1;
+            nto = tr ? L.decision_start_to_close : 0;
+            nscts = now_ns;
+          }
+          update_decision(L, nv, ns, nst, nreq, nto, natt, nsts, nscts, nots);
+        }
+        const i32 q = last_in(DC);
+        if (q >= 0) L.last_processed_event = lane_i64(C.ref_, q);
+        if (DS & E) {  // UpdateWorkflowStateCloseStatus(Running, None) (:185-208)
+          L.state = CRR_STATE_RUNNING;
+          L.close_status = CRR_CLOSE_NONE;
+        }
+        const u64 SG = __builtin_amdgcn_ballot_w64(lv && tl == CRR_EV_WORKFLOW_EXECUTION_SIGNALED);  // :497-502
+        const u64 CR = __builtin_amdgcn_ballot_w64(lv && tl == CRR_EV_WORKFLOW_EXECUTION_CANCEL_REQUESTED);
+        L.signal_count = (i32)((u32)L.signal_count + (u32)__builtin_popcountll(SG & E));
+        if (CR & E) L.flags |= CRR_EXEC_CANCEL_REQUESTED;  // :504-509
+        const i32 b = last_in(BL & E);
+        if (b >= 0) {  // :642-643
+          const i32 bf = last_in(BF & le(b));
+          L.last_first_event_id = bf < 0 ? batch_first_id : lane_i64(C.id_, bf);
+          L.next_event_id = lane_i64(C.id_, b) + 1;
+        }
+        const i32 f = last_in(BF & E);
+        if (f >= 0) batch_first_id = lane_i64(C.id_, f);
+        const i32 k = wfail >= 0 ? wfail : stop < lim ? stop : lim - 1;  // the last event whose prologue ran
+        if (k >= 0) {
+          L.current_version = lane_i64(C.ver_, k);
+          last_task_step = c0 + k;
+        }
+        if (wfail < 0 && stop < lim) {  // DecisionTaskStarted without its decision (:210-228)
+          wfail = stop;
+          wrc = CRR_ERR_DECISION_NOT_FOUND;
+        }
+      }
+      if (wfail >= 0) {  // the failing event's prologue has run
+        WAVE_VH_AFTER(wfail);
+        FAIL(wrc, c0 + wfail);
       }
       if (lim > 0) WAVE_VH_AFTER(lim - 1);
       if (lim < cnt) {  // event c0 + lim fails its prologue; a version-history error follows UpdateCurrentVersion

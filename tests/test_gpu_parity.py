@@ -87,6 +87,19 @@ def test_wave_per_workflow_all_event_types(engine):
     assert len(set(int(s) for s in got.exec["status"])) >= 8
 
 
+def test_wave_chunks_with_failures(engine):
+    """Histories of several 64-event chunks, one per wavefront, most ending in an injected error: the
+    chunks after the first resolve their decision events lane-parallel and walk only the map events, so
+    failures land inside such chunks (decision not found, missing activity / child, unknown domain,
+    version-history checks) as well as in the per-event chunks (rare types)."""
+    hs = synth_mixed.mixed_histories(1500, 23, mean_len=300, multi_version=True, invalid_rate=0.6, can_rate=0.3)
+    ib = interleave(flatten(hs, known_domains=KNOWN), long_threshold=0)
+    assert ib.wave_begin == 0
+    got = check(engine, ib)
+    st = collections.Counter(int(s) for s in got.exec["status"])
+    assert st[0] > 400 and len(st) >= 8, st
+
+
 def test_long_tail_continue_as_new(engine):
     """Config 4 shape: Zipf lengths, continue-as-new chains.  Unbounded random walks: live sets
     outgrow both LDS arenas, so those workflows go through the HBM-row wavefront pass."""

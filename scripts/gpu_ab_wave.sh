@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"; mkdir -p gpurun_out
 log() { echo "$(date +%T) $*" >> "$R/gpurun_out/status.log"; }
 if [ -z "${NO_TESTS:-}" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ${TESTS:-} > gpurun_out/pytest_ab.log 2>&1
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_ab.log 2>&1
   rc=$?; log "pytest rc=$rc"; tail -3 gpurun_out/pytest_ab.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error|assert" gpurun_out/pytest_ab.log | head -30; exit $rc; }
 fi
 for r in $(seq 1 ${REPS:-2}); do

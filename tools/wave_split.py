@@ -1,0 +1,44 @@
+"""Profiling aid (not product code): where the wavefront path's time goes, by removing one part at a
+time.  Builds variant libraries from patched copies of replay_kernel.hip (results are wrong by design;
+only the kernel times are read, tools/prof_longtail.py --lib):
+
+    python tools/wave_split.py noepi noside nowalk      ->  tools/variants/<name>.so
+
+  noepi   the batch epilogue (timer re-selection) skipped
+  noside  ActivityTaskScheduled's side record not loaded (a constant instead)
+  nowalk  fast chunks visit nothing (only the lane-parallel passes run)
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+PATCHES = {
+    "noepi": [("          T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks\n"
+               "          if (!fast) {",
+               "          if (0) T.epilogue(L, G, K);\n          if (!fast) {")],
+    "noside": [("        as = in.act_side[ev.aux()];\n        if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL",
+                "        as.domain_status = 1; as.has_retry_policy = 0; as.schedule_to_start = 10; "
+                "as.schedule_to_close = 20; as.start_to_close = 10; as.heartbeat = 0;\n"
+                "        if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL")],
+    "nowalk": [("        vm = (OPS | EB) & le(stop - 1);", "        vm = 0;")],
+}
+
+
+def main():
+    for name in sys.argv[1:]:
+        s = open(os.path.join(ROOT, "cadence_amd", "csrc", "replay_kernel.hip")).read()
+        for old, new in PATCHES[name]:
+            if old not in s:
+                raise SystemExit(f"{name}: patch point not found: {old[:60]!r}")
+            s = s.replace(old, new, 1)
+        d = tempfile.mkdtemp()
+        p = os.path.join(d, "replay_kernel.hip")
+        open(p, "w").write(s)
+        subprocess.run([sys.executable, os.path.join(ROOT, "tools", "build_variant.py"), name, "--src=" + p], check=True)
+
+
+if __name__ == "__main__":
+    main()

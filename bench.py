@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
+PROFILE_TRAFFIC_CONFIGS = os.path.join(ROOT, "profiles", "traffic_configs.json")
 MAX_TIMED_STEPS = 512   # crr_timing ring size (capi.hip kRing)
 
 
@@ -230,6 +231,18 @@ def config2(ctx):
 FAST_GROUP = "crr_replay phase-1 launch group (tier kernels on side streams, fork to join)"
 
 
+def config_traffic(name, n_wf, n_events):
+    """HBM bytes per launch group of a non-headline line, from its PMC passes (tools/traffic_configs.py,
+    profiles/traffic_configs.json) when they were taken on this exact workload; else None."""
+    try:
+        tr = json.load(open(PROFILE_TRAFFIC_CONFIGS)).get(name)
+    except (OSError, ValueError):
+        return None
+    if tr and tr.get("workflows") == n_wf and tr.get("events") == n_events:
+        return tr.get("hbm_bytes_per_launch")
+    return None
+
+
 def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
     """One non-headline line: generate this rank's shard, time `config_steps` replays, roofline over the
     launch group, parity of a sample against the oracle (rank 0)."""
@@ -253,7 +266,8 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
            "workflows_per_gpu": batch.n_wf, "events_per_gpu": batch.n_events, "workflows_ok": int(tot_ok),
            "workflows_per_s": tot_wf * args.config_steps / wall,
            "tiers": list(batch.tiers) if batch.tiers else None, "wave_tail": batch.n_wf - (batch.wave_begin or batch.n_wf),
-           "roofline": roofline(synth.algorithmic_bytes(batch, res), grp_ms, FAST_GROUP),
+           "roofline": roofline(synth.algorithmic_bytes(batch, res), grp_ms, FAST_GROUP,
+                                config_traffic(name, batch.n_wf, batch.n_events)),
            "setup_s": {"generate": t1 - t0, "interleave": t2 - t1}}
     if ctx.rank == 0:
         out["parity_sample"] = parity_sample(ctx, sample_fn, long_threshold)

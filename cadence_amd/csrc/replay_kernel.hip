@@ -461,6 +461,30 @@ enum : u32 {
   MOP_CHILD_INSERT, MOP_CHILD_START, MOP_CHILD_DELETE,
   MOP_RC_INSERT, MOP_RC_DELETE, MOP_SIG_INSERT, MOP_SIG_DELETE
 };
+// The map operation of each event type (0: none), 4 bits per type
+constexpr u32 mop_of(int t) {
+  return t == CRR_EV_ACTIVITY_TASK_SCHEDULED ? MOP_ACT_INSERT
+       : t == CRR_EV_ACTIVITY_TASK_STARTED ? MOP_ACT_START
+       : (t == CRR_EV_ACTIVITY_TASK_COMPLETED || t == CRR_EV_ACTIVITY_TASK_FAILED || t == CRR_EV_ACTIVITY_TASK_TIMED_OUT ||
+          t == CRR_EV_ACTIVITY_TASK_CANCELED) ? MOP_ACT_DELETE
+       : t == CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED ? MOP_ACT_CANCEL
+       : t == CRR_EV_TIMER_STARTED ? MOP_TIMER_START
+       : (t == CRR_EV_TIMER_FIRED || t == CRR_EV_TIMER_CANCELED) ? MOP_TIMER_DELETE
+       : t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED ? MOP_CHILD_INSERT
+       : t == CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED ? MOP_CHILD_START
+       : (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED || (t >= CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED &&
+          t <= CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED)) ? MOP_CHILD_DELETE
+       : t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ? MOP_RC_INSERT
+       : (t == CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED) ? MOP_RC_DELETE
+       : t == CRR_EV_SIGNAL_EXTERNAL_INITIATED ? MOP_SIG_INSERT
+       : (t == CRR_EV_SIGNAL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED) ? MOP_SIG_DELETE
+       : MOP_NONE;
+}
+constexpr u64 mop_word(int w) {
+  u64 v = 0;
+  for (int k = 0; k < 16; ++k) v |= (u64)mop_of(16 * w + k) << (4 * k);
+  return v;
+}
 
 struct GlobalTables {
   static constexpr bool kResumable = true;  // rows live in HBM: a loaded state is continued in place
@@ -1936,6 +1960,9 @@ struct WaveTables {
     return find(P_(), L.n_rp, [&](const crr_reset_point_row& r) { return r.key == key; }) >= 0;
   }
 
+#ifndef CRR_WAVE_MIN_SCALAR
+#define CRR_WAVE_MIN_SCALAR 2
+#endif
   // argmin of the per-lane candidates across the wavefront (keys are unique: (time, eventID, type)):
   // a scalar pass with readlane over the candidate lanes -- all of them when few, else only those
   // holding the minimum timestamp (found with a shuffle tree over the timestamp alone).
@@ -1965,7 +1992,7 @@ struct WaveTables {
   }
   __device__ __forceinline__ static void wave_min(BestTimer& B) {
     u64 m = __builtin_amdgcn_ballot_w64(B.have);
-    if (__builtin_popcountll(m) > 12) {
+    if (__builtin_popcountll(m) > CRR_WAVE_MIN_SCALAR) {
       // many candidates: reduce the timestamp alone (two crossbar shuffles per level), then keep only
       // the lanes holding the minimum (almost always one) for the scalar pass below
       const i64 t = wave_min_i64(B.have ? B.t : (i64)0x7fffffffffffffffLL);
@@ -2639,30 +2666,6 @@ template <class P, class = void>
 struct LaneDispatch { static constexpr bool value = true; };
 template <class P>
 struct LaneDispatch<P, decltype((void)P::kLaneDispatch)> { static constexpr bool value = P::kLaneDispatch; };
-// The map operation of each event type (0: none), 4 bits per type
-constexpr u32 mop_of(int t) {
-  return t == CRR_EV_ACTIVITY_TASK_SCHEDULED ? MOP_ACT_INSERT
-       : t == CRR_EV_ACTIVITY_TASK_STARTED ? MOP_ACT_START
-       : (t == CRR_EV_ACTIVITY_TASK_COMPLETED || t == CRR_EV_ACTIVITY_TASK_FAILED || t == CRR_EV_ACTIVITY_TASK_TIMED_OUT ||
-          t == CRR_EV_ACTIVITY_TASK_CANCELED) ? MOP_ACT_DELETE
-       : t == CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED ? MOP_ACT_CANCEL
-       : t == CRR_EV_TIMER_STARTED ? MOP_TIMER_START
-       : (t == CRR_EV_TIMER_FIRED || t == CRR_EV_TIMER_CANCELED) ? MOP_TIMER_DELETE
-       : t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED ? MOP_CHILD_INSERT
-       : t == CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED ? MOP_CHILD_START
-       : (t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED || (t >= CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED &&
-          t <= CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED)) ? MOP_CHILD_DELETE
-       : t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED ? MOP_RC_INSERT
-       : (t == CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED) ? MOP_RC_DELETE
-       : t == CRR_EV_SIGNAL_EXTERNAL_INITIATED ? MOP_SIG_INSERT
-       : (t == CRR_EV_SIGNAL_EXTERNAL_FAILED || t == CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED) ? MOP_SIG_DELETE
-       : MOP_NONE;
-}
-constexpr u64 mop_word(int w) {
-  u64 v = 0;
-  for (int k = 0; k < 16; ++k) v |= (u64)mop_of(16 * w + k) << (4 * k);
-  return v;
-}
 // types whose transition is more than a handful of field updates: the start event, the closes and
 // continue-as-new (once per run each), and anything unknown
 constexpr u64 kLaneRare = (1ull << CRR_EV_WORKFLOW_EXECUTION_STARTED) | (1ull << CRR_EV_WORKFLOW_EXECUTION_COMPLETED) |
@@ -2913,9 +2916,19 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         // batch ends whose epilogue has work: a map operation in the batch (or dirty maps carried in)
         const u64 seg = le(lane) & ~le(bl);
         const bool carried_dirty = T.dirty_act || T.dirty_timer;
+        // DecisionTaskCompleted's reset point (addBinaryCheckSumIfNotExists, :1911-1974): a binary checksum
+        // already in the list, or pushed by an earlier event of the chunk, is a no-op -- only the first
+        // event of each checksum not yet listed is walked (the list only grows inside a fast chunk)
+        u64 RPV = 0;
+        for (u64 rpm = RP; rpm;) {
+          const i32 j = (i32)__builtin_ctzll(rpm);
+          const u32 key = __builtin_amdgcn_readlane(C.key_, j);
+          rpm &= ~__builtin_amdgcn_ballot_w64(live && is_dc && C.key_ == key);
+          if (!T.rp_has(L, G, key)) RPV |= 1ull << j;
+        }
         const u64 EB = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_LAST) &&
                                                    ((MP & seg) != 0 || (bl < 0 && carried_dirty)));
-        OPS = MP | RP;
+        OPS = MP | RPV;
         vm = (OPS | EB) & le(stop - 1);
       }
       const u64 BF = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_FIRST));

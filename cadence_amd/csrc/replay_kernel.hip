@@ -1818,12 +1818,27 @@ struct WaveTables {
     return find(row, hw, [&](const auto& r) { return (r.flags & CRR_ROW_LIVE) && r.initiated_id == id; });
   }
 
+  // LdsRows: each activity's earliest timer candidate (timer_sequence.go:269-381 over its own timeouts),
+  // kept current by what changes it -- the insert, the start, the epilogue's created mark, RefreshTasks
+  // -- in the arena's ids[] (unused until finalize): the epilogue then reads one candidate per row
+  // instead of recomputing every row's.  ids[j]: the time; ids[A + j]: 1 | type << 8 | created << 16.
+  __device__ __forceinline__ void act_cand_store(i32 j, const crr_activity_row& r) {
+    if constexpr (ST::kLds) {
+      BestTimer B;
+      activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
+                          max(r.started_time, r.last_heartbeat_time), r.schedule_to_start, r.schedule_to_close,
+                          r.start_to_close, r.heartbeat, (u32)r.timer_task_status);
+      S.M->ids[j] = B.t;
+      S.M->ids[ST::A + j] = B.have ? (i64)(1u | ((u32)B.y << 8) | ((B.created ? 1u : 0u) << 16)) : 0;
+    }
+  }
   __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
     const i32 m = find_act_mapped(row.key);
     const i32 j = take(A_(), hw_act, ST::A, G.act_cap);
     if (j < 0) return -j;
     if (m >= 0 && own(m)) S.act(m).flags &= ~CRR_ROW_MAPPED;
     if (own(j)) S.act(j) = row;
+    act_cand_store(j, row);
     ++L.n_act;
     dirty_act = true;
     return CRR_OK;
@@ -1839,6 +1854,7 @@ struct WaveTables {
       r.started_src = s;
       r.started_time = ts;
       r.last_heartbeat_time = ts;
+      act_cand_store(j, r);
     }
     return CRR_OK;
   }
@@ -2021,10 +2037,15 @@ struct WaveTables {
       for (i32 j = lane; j < hw_act; j += 64) {
         const crr_activity_row& r = S.act(j);
         if (!(r.flags & CRR_ROW_LIVE)) continue;
-        activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
-                            max(r.started_time, r.last_heartbeat_time),
-                            r.schedule_to_start, r.schedule_to_close, r.start_to_close, r.heartbeat,
-                            (u32)r.timer_task_status);
+        if constexpr (ST::kLds) {
+          const i64 w = S.M->ids[ST::A + j];
+          if (w & 1) B.offer(S.M->ids[j], r.schedule_id, (i32)((w >> 8) & 0xff), j, ((w >> 16) & 1) != 0);
+        } else {
+          activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
+                              max(r.started_time, r.last_heartbeat_time),
+                              r.schedule_to_start, r.schedule_to_close, r.start_to_close, r.heartbeat,
+                              (u32)r.timer_task_status);
+        }
       }
       wave_min(B);
       i32 attempt = 0;
@@ -2033,6 +2054,7 @@ struct WaveTables {
         r.timer_task_status |= timer_mask(B.y);
         if (B.y == CRR_TIMEOUT_HEARTBEAT) r.last_hb_timeout_vis_s = unix_seconds(B.t);
         attempt = r.attempt;
+        if constexpr (ST::kLds) S.M->ids[ST::A + B.j] |= (i64)1 << 16;  // the row's earliest is now created
       }
       if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, (i32)bcast(B.j, (u32)attempt), -1);
     }
@@ -2054,7 +2076,11 @@ struct WaveTables {
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365); each lane clears the slots
   // the epilogue's candidate loop reads with the same lane, so no cross-lane ordering is needed
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
-    for (i32 j = lane; j < hw_act; j += 64) S.act(j).timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+    for (i32 j = lane; j < hw_act; j += 64) {
+      S.act(j).timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+      if constexpr (ST::kLds) S.M->ids[ST::A + j] &= ~((i64)1 << 16);
+    }
+    if constexpr (ST::kLds) wave_sync_lds();
     for (i32 j = lane; j < hw_timer; j += 64) S.timer(j).task_status = CRR_TIMER_TASK_STATUS_NONE;
     dirty_act = dirty_timer = true;
     epilogue(L, G, TaskSink{false, false});

@@ -7,6 +7,7 @@ only the kernel times are read, tools/prof_longtail.py --lib):
   noepi   the batch epilogue (timer re-selection) skipped
   noside  ActivityTaskScheduled's side record not loaded (a constant instead)
   nowalk  fast chunks visit nothing (only the lane-parallel passes run)
+  noreread  compact tiers' ActivityTaskStarted without re-reading its scheduled event (config 3)
 """
 import os
 import subprocess
@@ -24,6 +25,11 @@ PATCHES = {
                 "as.schedule_to_close = 20; as.start_to_close = 10; as.heartbeat = 0;\n"
                 "        if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL")],
     "nowalk": [("        vm = (OPS | EB) & le(stop - 1);", "        vm = 0;")],
+    # compact tiers: ActivityTaskStarted without the re-reads of its scheduled event (aux -> side record, time)
+    "noreread": [("    const crr_activity_side sa = in->act_side[in->ev.aux[six]];\n"
+                  "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",
+                  "    crr_activity_side sa{}; sa.schedule_to_close = 20; sa.start_to_close = 10; (void)six;\n"
+                  "    i64 ct = add_seconds(ev.ts(), sa.schedule_to_close);")],
 }
 
 

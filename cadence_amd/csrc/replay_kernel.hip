@@ -2958,6 +2958,10 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         vm = (OPS | EB) & le(stop - 1);
       }
       const u64 BF = __builtin_amdgcn_ballot_w64(live && (C.et & CRR_ETYPE_BATCH_FIRST));
+      constexpr u64 kBatchIdTypes = (1ull << CRR_EV_ACTIVITY_TASK_SCHEDULED) |
+                                    (1ull << CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED) |
+                                    (1ull << CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED) |
+                                    (1ull << CRR_EV_SIGNAL_EXTERNAL_INITIATED);
       // The walk.  A visited DecisionTaskCompleted runs its whole transition: its decision update is
       // overwritten by the chunk's (below), which covers it, and its reset point is the walk's part.
       i32 wfail = -1;
@@ -2975,7 +2979,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
           // :112 UpdateCurrentVersion: a closed workflow keeps its version history's last version
           L.current_version = L.state == CRR_STATE_COMPLETED ? lane_i64(pver, j) : ev.ver();
           last_task_step = s;  // :129 SetLastEventTaskID(event.TaskID): read once, after the loop
-        } else {
+        } else if (((1ull << (et & CRR_ETYPE_MASK)) & kBatchIdTypes) != 0) {
+          // only the inserts record their batch's first event ID
           const i32 bf = last_in(BF & le(j));
           if (bf >= 0) bfid = lane_i64(C.id_, bf);
         }

@@ -7,6 +7,7 @@ only the kernel times are read, tools/prof_longtail.py --lib):
   noepi   the batch epilogue (timer re-selection) skipped
   noside  ActivityTaskScheduled's side record not loaded (a constant instead)
   nowalk  fast chunks visit nothing (only the lane-parallel passes run)
+  noops   fast chunks visit their lanes but apply no map operation (visit and epilogue costs only)
   noreread  compact tiers' ActivityTaskStarted without re-reading its scheduled event (config 3)
 """
 import os
@@ -25,6 +26,8 @@ PATCHES = {
                 "as.schedule_to_close = 20; as.start_to_close = 10; as.heartbeat = 0;\n"
                 "        if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL")],
     "nowalk": [("        vm = (OPS | EB) & le(stop - 1);", "        vm = 0;")],
+    "noops": [("        if (!fast || ((OPS >> j) & 1)) {\n          const int rc = apply_event(",
+               "        if (!fast) {\n          const int rc = apply_event(")],
     # compact tiers: ActivityTaskStarted without the re-reads of its scheduled event (aux -> side record, time)
     "noreread": [("    const crr_activity_side sa = in->act_side[in->ev.aux[six]];\n"
                   "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",

@@ -7,6 +7,7 @@ only the kernel times are read, tools/prof_longtail.py --lib):
   noepi   the batch epilogue (timer re-selection) skipped
   noside  ActivityTaskScheduled's side record not loaded (a constant instead)
   nowalk  fast chunks visit nothing (only the lane-parallel passes run)
+  bare    no chunk is walked or resolved (chunk loads, the VH prologue and the chunk bookkeeping only)
   noops   fast chunks visit their lanes but apply no map operation (visit and epilogue costs only)
   noreread  compact tiers' ActivityTaskStarted without re-reading its scheduled event (config 3)
 """
@@ -28,6 +29,8 @@ PATCHES = {
     "nowalk": [("        vm = (OPS | EB) & le(stop - 1);", "        vm = 0;")],
     "noops": [("        if (!fast || ((OPS >> j) & 1)) {\n          const int rc = apply_event(",
                "        if (!fast) {\n          const int rc = apply_event(")],
+    "bare": [("      u64 vm = le(lim - 1), OPS = 0;", "      u64 vm = 0, OPS = 0;"),
+             ("      const bool fast = !K.on &&", "      const bool fast = false && !K.on &&")],
     # compact tiers: ActivityTaskStarted without the re-reads of its scheduled event (aux -> side record, time)
     "noreread": [("    const crr_activity_side sa = in->act_side[in->ev.aux[six]];\n"
                   "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",

@@ -642,15 +642,24 @@ struct GlobalTables {
   __device__ __forceinline__ void load(Lane& L, const Geo& G) {
     hw_act = L.n_act; hw_timer = L.n_timer; hw_child = L.n_child; hw_rc = L.n_rc; hw_sig = L.n_sig;
     dirty_act = dirty_timer = true;  // the loaded state's timer masks are re-examined by the first epilogue
+    // the ActivityID map (Load: the latest ScheduleID of each ActivityID wins): a 64-bit filter over the
+    // keys finds the rows whose ActivityID may repeat; only those compare against the other rows
+    u64 seen = 0, dup = 0;
+    for (i32 j = 0; j < hw_act; ++j) {
+      const u64 b = 1ull << (G.act(j)->key & 63u);
+      dup |= seen & b;
+      seen |= b;
+    }
     for (i32 j = 0; j < hw_act; ++j) {
       crr_activity_row* r = G.act(j);
       const u32 key = r->key;
       const i64 sid = r->schedule_id;
       bool mapped = true;
-      for (i32 k = 0; k < hw_act; ++k) {
-        const crr_activity_row* o = G.act(k);
-        if (k != j && o->key == key && o->schedule_id > sid) mapped = false;
-      }
+      if (dup & (1ull << (key & 63u)))
+        for (i32 k = 0; k < hw_act; ++k) {
+          const crr_activity_row* o = G.act(k);
+          if (k != j && o->key == key && o->schedule_id > sid) mapped = false;
+        }
       r->flags = (r->flags & ~CRR_ROW_MAPPED) | CRR_ROW_LIVE | (mapped ? CRR_ROW_MAPPED : 0u);
     }
     for (i32 j = 0; j < hw_timer; ++j) G.timer(j)->flags |= CRR_ROW_LIVE;
@@ -1727,6 +1736,8 @@ struct LdsRows {
   static constexpr bool kLds = true;
   static constexpr int kList = LIST;  // scratch list a workflow that outgrows the arena is handed to
   static constexpr i32 A = ARENA::A, T = ARENA::T, C = ARENA::C, R = ARENA::R, S = ARENA::S, P = ARENA::P;
+  // WaveTables::act_cand_store keeps two words per activity slot in ids[] until finalize
+  static_assert(A + T + C + R + S >= 2 * A, "ids[] too small for the activity candidate cache");
   ARENA* M;
   __device__ __forceinline__ crr_activity_row& act(i32 j) const { return M->act[j]; }
   __device__ __forceinline__ crr_timer_row& timer(i32 j) const { return M->timer[j]; }

@@ -1,0 +1,58 @@
+"""Passive-replication probe (the bench's `passive_replication` line at its size): the config-3 shard cut
+before every history's last batch, the prefix replayed once, then `--reps` steps of restore + apply the
+last batches onto the loaded rows (CRR_WF_FLAG_RESUME); kernel time of each step.  Run it under
+`rocprofv3 --kernel-trace --stats` to see which kernels the resume path spends its time in.
+
+    python tools/prof_replication.py [--wf 1250000] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--wf", type=int, default=1_250_000)
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
+    a = p.parse_args()
+    if a.lib:
+        os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
+    import numpy as np
+    import torch
+    from cadence_amd import synth_native
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.flatten import interleave
+    from cadence_amd.replication import PassiveReplication
+
+    t0 = time.time()
+    batch = interleave(synth_native.mixed(a.wf), long_threshold=256)
+    eng = ReplayEngine(0)
+    db = eng.upload(batch)
+    eng.launch(db)
+    one_shot = eng.download(db)
+    del db
+    torch.cuda.empty_cache()
+    pr = PassiveReplication(eng, batch)
+    pr.setup()
+    setup_s = time.time() - t0
+    ms = []
+    for _ in range(a.reps + 1):
+        pr.restore()
+        torch.cuda.synchronize()
+        eng.launch(pr.db_new)
+        torch.cuda.synchronize()
+        ms.append(sum(x for x in eng.last_kernel_ms()[:2] if x > 0))
+    v = pr.verify(one_shot)
+    med = float(np.median(ms[1:]))
+    print(json.dumps({"workflows": a.wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
+                      "events_per_s": pr.n_events / (med * 1e-3), "verify": v, "setup_s": setup_s}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

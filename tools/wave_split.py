@@ -9,6 +9,7 @@ only the kernel times are read, tools/prof_longtail.py --lib):
   nowalk  fast chunks visit nothing (only the lane-parallel passes run)
   bare    no chunk is walked or resolved (chunk loads, the VH prologue and the chunk bookkeeping only)
   noops   fast chunks visit their lanes but apply no map operation (visit and epilogue costs only)
+  nosort  GlobalTables::finalize without its selection sorts (passive replication, tools/prof_replication.py)
   noreread  compact tiers' ActivityTaskStarted without re-reading its scheduled event (config 3)
 """
 import os
@@ -31,6 +32,9 @@ PATCHES = {
                "        if (!fast) {\n          const int rc = apply_event(")],
     "bare": [("      u64 vm = le(lim - 1), OPS = 0;", "      u64 vm = 0, OPS = 0;"),
              ("      const bool fast = !K.on &&", "      const bool fast = false && !K.on &&")],
+    # lane path over HBM rows (resume / wide segment): finalize without the in-place selection sorts
+    "nosort": [("    for (i32 i = 0; i < n; ++i) {\n      i32 best = -1;\n      i64 bid = 0;",
+                "    for (i32 i = 0; i < 0 * n; ++i) {\n      i32 best = -1;\n      i64 bid = 0;")],
     # compact tiers: ActivityTaskStarted without the re-reads of its scheduled event (aux -> side record, time)
     "noreread": [("    const crr_activity_side sa = in->act_side[in->ev.aux[six]];\n"
                   "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",

@@ -726,6 +726,17 @@ struct GlobalTables {
   __device__ __forceinline__ bool task_writer() const { return true; }
   template <class R, class IdOf>
   __device__ __forceinline__ static void compact_sort(R* (Geo::*row)(i32) const, const Geo& G, i32 hw, i32 n, IdOf id_of) {
+    // already in place (a resumed state whose map the new events did not reorder): one pass, no sort
+    bool in_place = true;
+    i64 prev = 0;
+    for (i32 j = 0; j < hw; ++j) {
+      const R* r = (G.*row)(j);
+      const bool live = (r->flags & CRR_ROW_LIVE) != 0;
+      const i64 id = id_of(r);
+      in_place = in_place && (j < n ? live && (j == 0 || id > prev) : !live);
+      prev = id;
+    }
+    if (in_place) return;
     for (i32 i = 0; i < n; ++i) {
       i32 best = -1;
       i64 bid = 0;

@@ -362,7 +362,7 @@ crr_encoded* crr_encode_blobs(const crr_inputs* in, const uint32_t* key_off, con
     r->strings.insert(r->strings.end(), o.strings.begin(), o.strings.end());
     o = Out();
   }
-  r->bytes.resize(r->bytes.size() + 32, 0);   // the device parser's 16-byte window reads past the end
+  r->bytes.resize(r->bytes.size() + CRR_INGEST_PAD, 0);   // the device parser's window reads past the end
   if (r->strings.empty()) r->strings.push_back(0);
   return r;
 }

@@ -6,6 +6,7 @@
 #include <mutex>
 
 #include "cadence_replay.h"
+#include "stream_device.h"
 
 namespace crr {
 template <bool WAVE_TAIL, bool EMIT>
@@ -37,11 +38,72 @@ constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena eac
 
 // Launch state is kept per HIP device, not per host thread: a cgo caller's goroutines migrate between
 // OS threads, and one thread may drive several devices.  Each device's state is created on first use
-// and guarded by its mutex for the whole enqueue of a call (the fork / join events and the timing
-// events are shared by every call on that device); crr_release() destroys it.
+// and guarded by its mutex while a call enqueues (microseconds: nothing waits on the GPU under it);
+// crr_release() destroys it.  The side streams a call forks its tier segments onto are keyed by the
+// caller's stream (kSideSets sets per device), so callers on different streams do not queue each
+// other's segments; with more distinct caller streams than sets, the least recently used set is reused
+// (still correct -- a false dependency, no more).
 constexpr int kMaxDevices = 64;
 constexpr int kRing = 512;   // per-launch records of a measured region (crr_timing_begin .. _read)
 constexpr int kSide = 6;
+constexpr int kSideSets = 4;
+
+// n events created, or none (a partial failure destroys what it created)
+bool create_events(hipEvent_t* e, int n, unsigned flags) {
+  for (int i = 0; i < n; ++i) {
+    if (hipEventCreateWithFlags(&e[i], flags) != hipSuccess) {
+      for (int j = 0; j < i; ++j) { (void)hipEventDestroy(e[j]); e[j] = nullptr; }
+      e[i] = nullptr;
+      return false;
+    }
+  }
+  return true;
+}
+void destroy_events(hipEvent_t* e, int n) {
+  for (int i = 0; i < n; ++i) { if (e[i]) (void)hipEventDestroy(e[i]); e[i] = nullptr; }
+}
+
+// One caller stream's side streams and fork / join events.
+struct SideSet {
+  hipStream_t caller = nullptr;   // the stream this set serves
+  unsigned long long last_use = 0;
+  hipStream_t side[kSide] = {};
+  hipEvent_t fork = nullptr, join[kSide] = {};
+  bool ready = false;
+
+  bool create() {
+    if (ready) return true;
+    // the compact tiers carry most of a mixed batch's work and tiers 2 / 3 the longest-running
+    // wavefronts (their blocks hold the most LDS per lane, so the fewest fit a CU): their streams get
+    // the higher priority, so their workgroups are dispatched first and the short, dense segments fill
+    // the CUs around them instead of ahead of them
+    int lo_prio = 0, hi_prio = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
+    int made = 0;
+    for (; made < kSide; ++made) {
+      const int prio = ((kSegPrioMask >> made) & 1) ? hi_prio : lo_prio;
+      if (hipStreamCreateWithPriority(&side[made], hipStreamNonBlocking, prio) != hipSuccess) break;
+    }
+    bool ok = made == kSide && create_events(&fork, 1, hipEventDisableTiming);
+    if (ok && !create_events(join, kSide, hipEventDisableTiming)) {
+      destroy_events(&fork, 1);
+      ok = false;
+    }
+    if (!ok) {
+      for (int i = 0; i < made; ++i) { (void)hipStreamDestroy(side[i]); side[i] = nullptr; }
+      return false;
+    }
+    return ready = true;
+  }
+  void destroy() {
+    if (!ready) return;
+    for (auto& x : side) { if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); } x = nullptr; }
+    destroy_events(&fork, 1);
+    destroy_events(join, kSide);
+    ready = false;
+    caller = nullptr;
+  }
+};
 
 struct DeviceState {
   std::mutex mu;
@@ -56,66 +118,62 @@ struct DeviceState {
   bool ring_on = false, ring_events = false;
   // tier segments of one phase run concurrently: side streams fork from and join back into the
   // caller's stream
-  hipStream_t side[kSide] = {};
-  hipEvent_t fork = nullptr, join[kSide] = {};
-  bool sides = false;
+  SideSet sets[kSideSets];
+  unsigned long long use_clock = 0;
   // diagnostics (crr_segment_timing): when each side stream's segments of the last phase-1 group
   // finished, relative to the fork
   bool seg_on = false, seg_valid = false, seg_events = false;
   hipEvent_t seg_start = nullptr, seg_end[kSide + 1] = {};
 
   bool ensure_events() {
-    if (events) return true;
-    for (auto& e : ev)
-      if (hipEventCreate(&e) != hipSuccess) return false;
-    return events = true;
+    if (!events) events = create_events(ev, 6, hipEventDefault);
+    return events;
   }
   bool ensure_ring() {
-    if (ring_events) return true;
-    for (auto& e : ring)
-      if (hipEventCreate(&e) != hipSuccess) return false;
-    return ring_events = true;
+    if (!ring_events) ring_events = create_events(ring, 2 * kRing, hipEventDefault);
+    return ring_events;
   }
-  bool ensure_side_streams() {
-    if (sides) return true;
-    // the compact tiers carry most of a mixed batch's work and tiers 2 / 3 the longest-running
-    // wavefronts (their blocks hold the most LDS per lane, so the fewest fit a CU): their streams get
-    // the higher priority, so their workgroups are dispatched first and the short, dense segments fill
-    // the CUs around them instead of ahead of them
-    int lo_prio = 0, hi_prio = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio) != hipSuccess) lo_prio = hi_prio = 0;
-    for (int i = 0; i < kSide; ++i) {
-      const int prio = ((kSegPrioMask >> i) & 1) ? hi_prio : lo_prio;
-      if (hipStreamCreateWithPriority(&side[i], hipStreamNonBlocking, prio) != hipSuccess) return false;
+  // the side-stream set of `caller` (created on first use), or nullptr when none can be created (the
+  // call then launches every segment on the caller's stream)
+  SideSet* sides_for(hipStream_t caller) {
+    SideSet* pick = nullptr;
+    for (auto& x : sets)
+      if (x.ready && x.caller == caller) pick = &x;
+    if (!pick)
+      for (auto& x : sets)
+        if (!x.ready) { pick = &x; break; }
+    if (!pick) {  // every set serves another stream: reuse the least recently used one
+      pick = &sets[0];
+      for (auto& x : sets)
+        if (x.last_use < pick->last_use) pick = &x;
     }
-    if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) return false;
-    for (auto& e : join)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-    return sides = true;
+    if (!pick->create()) return nullptr;
+    pick->caller = caller;
+    pick->last_use = ++use_clock;
+    return pick;
   }
   bool ensure_seg_events() {
     if (seg_events) return true;
-    if (hipEventCreate(&seg_start) != hipSuccess) return false;
-    for (auto& e : seg_end)
-      if (hipEventCreate(&e) != hipSuccess) return false;
+    if (!create_events(&seg_start, 1, hipEventDefault)) return false;
+    if (!create_events(seg_end, kSide + 1, hipEventDefault)) { destroy_events(&seg_start, 1); return false; }
     return seg_events = true;
   }
   // destroys everything (the device must be current); the state can be rebuilt by a later call
   void release() {
-    auto drop_ev = [](hipEvent_t& e) { if (e) (void)hipEventDestroy(e); e = nullptr; };
-    if (sides) {
-      for (auto& x : side) { if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); } x = nullptr; }
-    }
-    for (auto& e : ev) drop_ev(e);
-    for (auto& e : ring) drop_ev(e);
-    drop_ev(fork);
-    for (auto& e : join) drop_ev(e);
-    drop_ev(seg_start);
-    for (auto& e : seg_end) drop_ev(e);
-    events = ring_events = sides = seg_events = false;
+    for (auto& x : sets) x.destroy();
+    destroy_events(ev, 6);
+    destroy_events(ring, 2 * kRing);
+    destroy_events(&seg_start, 1);
+    destroy_events(seg_end, kSide + 1);
+    events = ring_events = seg_events = false;
     valid[0] = valid[1] = valid[2] = false;
     ring_n = 0;
     ring_on = seg_on = seg_valid = false;
+  }
+  bool any() const {
+    bool s = false;
+    for (auto& x : sets) s = s || x.ready;
+    return s || events || ring_events || seg_events;
   }
 };
 DeviceState g_dev[kMaxDevices];
@@ -128,24 +186,7 @@ DeviceState* current_state() {
   return &g_dev[dev];
 }
 
-// A call on a non-NULL stream runs on that stream's device whatever this thread has selected (a cgo
-// goroutine may have moved to a thread that never called crr_set_device); the selection is restored.
-struct StreamDevice {
-  int prev = -1;
-  bool ok = true;
-  explicit StreamDevice(hipStream_t s) {
-    if (!s) return;
-    int cur = 0, dev = 0;
-    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice(s, &dev) != hipSuccess) { ok = false; return; }
-    if (dev != cur) {
-      if (hipSetDevice(dev) != hipSuccess) { ok = false; return; }
-      prev = cur;
-    }
-  }
-  ~StreamDevice() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
+using crr_internal::StreamDevice;
 
 bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!in || !out) return false;
@@ -287,16 +328,18 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         const bool run_big = tail_end < in->n_wf;
         // more than one segment: the others fork onto the side streams (each launch alone leaves
         // most of the chip idle: few wavefronts, each latency-bound) and join back before the retry
-        const bool fork = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_c3 + (int)run_wide +
+        const bool many = (int)run_small + (int)run_large + (int)run_c1 + (int)run_c2 + (int)run_c3 + (int)run_wide +
                               (int)run_big + (int)run_tail > 1;
-        if (fork && !d->ensure_side_streams()) return fail_reset(out, s, hipErrorOutOfMemory);
-        hipStream_t s_large = fork ? d->side[0] : s, s_wide = fork ? d->side[1] : s, s_big = fork ? d->side[2] : s;
-        hipStream_t s_c1 = fork ? d->side[3] : s, s_c2 = fork ? d->side[4] : s, s_tail = fork ? d->side[5] : s;
+        // no side streams to be had: every segment on the caller's stream (serial, same results)
+        SideSet* ss = many ? d->sides_for(s) : nullptr;
+        const bool fork = ss != nullptr;
+        hipStream_t s_large = fork ? ss->side[0] : s, s_wide = fork ? ss->side[1] : s, s_big = fork ? ss->side[2] : s;
+        hipStream_t s_c1 = fork ? ss->side[3] : s, s_c2 = fork ? ss->side[4] : s, s_tail = fork ? ss->side[5] : s;
         const bool seg = fork && d->seg_on && phase == 1 && d->seg_events;
         if (fork) {
           if (seg) (void)hipEventRecord(d->seg_start, s);
-          (void)hipEventRecord(d->fork, s);
-          for (hipStream_t x : d->side) (void)hipStreamWaitEvent(x, d->fork, 0);
+          (void)hipEventRecord(ss->fork, s);
+          for (hipStream_t x : ss->side) (void)hipStreamWaitEvent(x, ss->fork, 0);
         }
         if (run_big)  // the longest histories first
           hipLaunchKernelGGL(crr::replay_big_kernel, dim3(in->n_wf - tail_end), dim3(64), 0, s_big, *in, *out, phase,
@@ -326,13 +369,13 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         launch_fast(s, true, false, 0, lb, fork);
         if (fork) {
           if (seg) {
-            for (int i = 0; i < kSide; ++i) (void)hipEventRecord(d->seg_end[i], d->side[i]);
+            for (int i = 0; i < kSide; ++i) (void)hipEventRecord(d->seg_end[i], ss->side[i]);
             (void)hipEventRecord(d->seg_end[kSide], s);
             d->seg_valid = true;
           }
           for (int i = 0; i < kSide; ++i) {
-            (void)hipEventRecord(d->join[i], d->side[i]);
-            (void)hipStreamWaitEvent(s, d->join[i], 0);
+            (void)hipEventRecord(ss->join[i], ss->side[i]);
+            (void)hipStreamWaitEvent(s, ss->join[i], 0);
           }
         }
       } else {
@@ -414,7 +457,7 @@ int crr_release(void) {
   for (int i = 0; i < kMaxDevices; ++i) {
     DeviceState& d = g_dev[i];
     std::lock_guard<std::mutex> lk(d.mu);
-    if (!(d.events || d.ring_events || d.sides || d.seg_events)) continue;
+    if (!d.any()) continue;
     if (hipSetDevice(i) != hipSuccess) { rc = -1; continue; }
     d.release();
   }

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "cadence_replay.h"
+#include "stream_device.h"
 
 namespace crr {
 namespace {
@@ -158,9 +159,10 @@ int crr_compact_rows(const crr_inputs* in, const crr_outputs* out, const crr_com
   if (in->stride == 0 || ((in->flags & CRR_IN_WAVE_TAIL) && in->wave_begin > in->n_wf)) return -1;
   for (int t = 0; t < CRR_COMPACT_TABLES; ++t)
     if ((uintptr_t)dst->rows[t] & 7u) return -1;  // rows are copied as 8-byte words
-  if (in->n_wf == 0) return hipMemsetAsync(dst->offsets, 0, CRR_COMPACT_TABLES * sizeof(int64_t),
-                                           reinterpret_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -2;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  crr_internal::StreamDevice on_dev_(s);
+  if (!on_dev_.ok) return (int)hipErrorInvalidHandle;
+  if (in->n_wf == 0) return hipMemsetAsync(dst->offsets, 0, CRR_COMPACT_TABLES * sizeof(int64_t), s) == hipSuccess ? 0 : -2;
   const uint32_t n_blocks = (in->n_wf + crr::kCompactBlock - 1) / crr::kCompactBlock;
   int64_t* bsum = reinterpret_cast<int64_t*>(dst->scratch);
   hipLaunchKernelGGL(crr::compact_count_kernel, dim3(n_blocks), dim3(crr::kCompactBlock), 0, s, *in, *out, dst->offsets,

@@ -39,6 +39,7 @@
 
 #include "cadence_ingest.h"
 #include "cadence_decode.h"
+#include "stream_device.h"
 
 namespace crr_ingest {
 
@@ -1098,6 +1099,9 @@ __global__ __launch_bounds__(kBlock) void blob_decode_kernel(crr_blob_batch in, 
   const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= in.n_blobs) return;
   const u64 NB = (u64)P.n_blobs + 1;
+  // this plan's mark, never an earlier plan's: a blob whose fast decode fails or is skipped leaves no
+  // stale kDeferMark (the scratch is reused across plans) for the general pass to act on
+  P.cnt[1 * (u64)P.n_blobs + bi] = 0;
   if (P.off[0 * NB + P.n_blobs] > P.max_events) return;   // the summary reports it
   decode_blob_fast(in, P, bi);
 }
@@ -1239,7 +1243,10 @@ __device__ __forceinline__ u32 pow2_at_least(u32 x) {
 // 64-bit table entries.  Interning: (hash32 << 32) | (entry index + 1), the key id kept in a parallel
 // word.  Bounds: (map << 40 | low 40 bits of the ID or key) + 1 in the low 43 bits, flag bits above.
 constexpr u64 kInserted = 1ull << 62, kDeleteSeen = 1ull << 61;
-constexpr u64 kMask40 = (1ull << 40) - 1;
+// live-set bound table entries: the creating event's position + 1 (bits 0-32), its map (33-35), which
+// of its fields holds the value (36-37); flags above
+constexpr u64 kPosMask = (1ull << 33) - 1;
+constexpr int kMapShift = 33, kKindShift = 36;
 
 __device__ __forceinline__ bool same_bytes(const u8* b, u64 x, u64 y, u32 len) {
   Rd rx, ry;
@@ -1370,17 +1377,25 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
         default: return -1;
       }
     };
-    auto entry_key = [](int m, u64 v) -> u64 { return (((u64)m << 40) | (v & kMask40)) + 1; };
-    auto find = [&](u64 k, bool create) -> u64* {
-      u32 h = (u32)((k * 0x9E3779B97F4A7C15ull) >> 32) & (cap_b - 1);
+    // An entry names the event that created it (its position, and which of its fields holds the value:
+    // the ID, the ref or the interned key), so a lookup compares the full 64-bit value, never a truncation
+    // (two IDs that differ only in high bits stay two entries, as in flatten's exact np.isin).
+    enum : u32 { kById = 0, kByRef = 1, kByKey = 2 };
+    auto value_of = [&](u64 ent) -> u64 {
+      const u64 x = e0 + ((ent & kPosMask) - 1);
+      const u32 kind = (u32)(ent >> kKindShift) & 3u;
+      return kind == kById ? (u64)P.id[x] : kind == kByRef ? (u64)P.ref[x] : (u64)P.key[x];
+    };
+    auto find = [&](int m, u64 v, u32 kind, u64 x, bool create) -> u64* {
+      u32 h = (u32)(((v ^ ((u64)m << 59)) * 0x9E3779B97F4A7C15ull) >> 32) & (cap_b - 1);
       for (;;) {
         const u64 ent = tab[h];
-        if ((ent & ((1ull << 43) - 1)) == k) return tab + h;
         if (ent == 0) {
           if (!create) return nullptr;
-          tab[h] = k;
+          tab[h] = ((u64)kind << kKindShift) | ((u64)m << kMapShift) | ((x - e0) + 1);
           return tab + h;
         }
+        if ((int)((ent >> kMapShift) & 7u) == m && value_of(ent) == v) return tab + h;
         h = (h + 1) & (cap_b - 1);
       }
     };
@@ -1392,7 +1407,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
       const int m = map_of(t, dir);
       if (m < 0 || dir <= 0) continue;
       const u64 v = m == 1 ? (u64)P.key[x] : (u64)P.id[x];
-      *find(entry_key(m, v), true) |= kInserted;
+      *find(m, v, m == 1 ? kByKey : kById, x, true) |= kInserted;
     }
     i32 run[5] = {0, 0, 0, 0, 0};
     for (u64 x = e0; x < e1; ++x) {
@@ -1403,10 +1418,10 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
       if (dir < 0) {
         bool valid;
         if (m == 1) {
-          u64* ent = find(entry_key(1, (u64)P.key[x]), false);
+          u64* ent = find(1, (u64)P.key[x], kByKey, x, false);
           valid = ent && (*ent & kInserted);
         } else {
-          u64* ent = find(entry_key(m, (u64)P.ref[x]), true);   // created to carry the first-delete mark
+          u64* ent = find(m, (u64)P.ref[x], kByRef, x, true);   // created to carry the first-delete mark
           const bool first = !(*ent & kDeleteSeen);
           *ent |= kDeleteSeen;
           valid = (*ent & kInserted) && P.ref[x] < P.id[x] && first;
@@ -1421,7 +1436,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
     i32 rp = 0;
     for (u64 x = e0; x < e1; ++x) {
       if ((P.etype[x] & CRR_ETYPE_MASK) != CRR_EV_DECISION_TASK_COMPLETED || P.key[x] == 0) continue;
-      u64* ent = find(entry_key(5, (u64)P.key[x]), true);
+      u64* ent = find(5, (u64)P.key[x], kByKey, x, true);
       if (!(*ent & kInserted)) { *ent |= kInserted; ++rp; }
     }
     bound[5] = rp + (max_prev > 0 ? max_prev : 0);
@@ -1802,6 +1817,8 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   if (!valid_batch(in) || !scratch || !summary) return -1;
   if (in->n_wf == 0 && in->n_blobs > 0) return -1;   // blobs no workflow owns
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  crr_internal::StreamDevice on_dev_(s);
+  if (!on_dev_.ok) return (int)hipErrorInvalidHandle;
   const size_t stmp = sort_tmp_bytes(in->n_wf);
   const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf, stmp);
   if (max_events == 0) return -1;
@@ -1883,6 +1900,8 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
   const crr_events& ev = dst->ev;
   if (!ev.etype || !ev.event_id || !ev.version || !ev.timestamp || !ev.task_id || !ev.ref || !ev.key || !ev.aux) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  crr_internal::StreamDevice on_dev_(s);
+  if (!on_dev_.ok) return (int)hipErrorInvalidHandle;
   const size_t stmp = sort_tmp_bytes(in->n_wf);
   const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf, stmp);
   Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events, stmp);

@@ -8,6 +8,7 @@
 #include <cstdint>
 
 #include "cadence_replay.h"
+#include "stream_device.h"
 
 namespace {
 
@@ -176,6 +177,8 @@ extern "C" int crr_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* results
   if (!in || (in->n_tasks && (!in->tasks || !in->branches || !in->items || !results || !out_items))) return -1;
   if (in->n_tasks == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  crr_internal::StreamDevice on_dev_(s);
+  if (!on_dev_.ok) return (int)hipErrorInvalidHandle;
   hipLaunchKernelGGL(ndc_prepare_kernel, dim3((in->n_tasks + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, results,
                      out_items);
   return (int)hipGetLastError();

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "cadence_replay.h"
+#include "stream_device.h"
 
 namespace crr {
 namespace {
@@ -161,6 +162,8 @@ int crr_widen_events(const crr_packed_events* packed, const crr_inputs* in, void
   if (in->stride != 1 && in->stride != 64) return -1;
   if (in->n_wf == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  crr_internal::StreamDevice on_dev_(s);
+  if (!on_dev_.ok) return (int)hipErrorInvalidHandle;
   const uint32_t n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
   if (n_lane > in->n_wf) return -1;
   if (in->stride == 1 && n_lane) {  // canonical batch: every workflow one wavefront

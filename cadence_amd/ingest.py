@@ -38,6 +38,9 @@ class CIngestSummary(ctypes.Structure):
 
 
 SCRATCH_TOO_SMALL = -100
+# CRR_INGEST_PAD (cadence_ingest.h): blob bytes readable this far past the last blob (the parser loads the
+# two 16-byte-aligned words around its cursor)
+INGEST_PAD = 32
 
 
 class IngestError(RuntimeError):
@@ -102,7 +105,7 @@ class DeviceIngest:
         T = {}
         for k, a in arrs.items():
             raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-            t = torch.empty(max(raw.size, 1) + 32, dtype=torch.uint8, device=dev)   # 16-B window reads past the end
+            t = torch.empty(max(raw.size, 1) + INGEST_PAD, dtype=torch.uint8, device=dev)   # window reads past the end
             if raw.size:
                 t[:raw.size].copy_(torch.from_numpy(raw) if not isinstance(a, torch.Tensor) else a)
             T[k] = t

@@ -105,8 +105,11 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
  * n_wf; act_side / start_side / reset_keys / arena their counts, arena 8-byte padded); the scalar
  * fields of *dst (n_wf, stride, flags, wave_begin, tiers) are the caller's to set from the summary.
  * `summary_host`: the plan's summary, as read back.  Also writes perm[n_wf] (device position ->
- * workflow index of the blob batch) when perm != NULL.  `bytes` of the blob batch must be 16-byte
- * aligned and readable 16 bytes past the last blob (the parser's window loads). */
+ * workflow index of the blob batch) when perm != NULL.  For both calls `bytes` of the blob batch must be
+ * 16-byte aligned and readable CRR_INGEST_PAD bytes past the end of the last blob: the parser's register
+ * window loads the two 16-byte-aligned words around its cursor, so a cursor on the last byte reads up to
+ * 31 bytes beyond it. */
+#define CRR_INGEST_PAD 32
 int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes,
                       const crr_ingest_summary* summary_host, const crr_inputs* dst, uint32_t* perm, void* stream);
 

@@ -134,3 +134,98 @@ def test_device_ingest_reshaped_blobs(eng, rate):
         _canon, want = _host_path(bs)
         ing, out = _ingest(eng, bs)
         _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
+def test_device_ingest_scratch_too_small_then_replans(eng):
+    """A plan whose scratch holds fewer events than the blobs reports CRR_INGEST_SCRATCH_TOO_SMALL (and
+    decodes nothing); DeviceIngest.plan grows the scratch and plans again, matching the host path."""
+    import ctypes
+    from cadence_amd.ingest import SCRATCH_TOO_SMALL, CIngestSummary, DeviceIngest
+    b = synth_native.mixed(700, mean_len=30)
+    bs = encode_batch(b)
+    _canon, want = _host_path(bs)
+    ing = DeviceIngest(eng)
+    db = ing.upload(bs)
+    size = ing.ensure_scratch(db, 1)
+    S = CIngestSummary()
+    s = eng.torch.cuda.current_stream(eng.dev)
+    rc = ing.lib.crr_ingest_plan(ctypes.byref(db.c), ctypes.c_void_p(ing.scratch.data_ptr()), ctypes.c_size_t(size),
+                                 ctypes.byref(S), ctypes.c_void_p(s.cuda_stream))
+    assert rc == 0
+    assert S.err == SCRATCH_TOO_SMALL and S.n_events == want.n_events
+    S2 = ing.plan(db, max_events=1)           # the grow-and-replan loop
+    out = ing.layout(db, S2)
+    _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
+def test_device_ingest_reuses_scratch_across_plans(eng):
+    """One DeviceIngest plans different blob sets in turn (the scratch is reused, not re-zeroed): a set
+    whose reshaped blobs the fast pass defers, then a clean set, a corrupt one and the reshaped one again
+    -- each equal to the host path (or failing with its error), nothing carried over from the plan
+    before."""
+    from thrift_tree import reshape_blobset
+    from cadence_amd.decode import DeserializationError
+    from cadence_amd.ingest import DeviceIngest, IngestError
+    ing = DeviceIngest(eng)
+    hs = synth_mixed.mixed_histories(300, 29, multi_version=True, invalid_rate=0.2, can_rate=0.3)
+    reshaped = reshape_blobset(encode_batch(flatten(hs, known_domains=set(KNOWN_DOMAINS))), seed=5, rate=0.5)
+    clean = encode_batch(synth_native.mixed(900, mean_len=25))
+    corrupt = encode_batch(synth_native.mixed(300, mean_len=25))
+    corrupt.bytes[int(corrupt.blob_off[11]) + 1] = 0x07
+    for bs in (reshaped, clean, corrupt, reshaped, clean):
+        try:
+            _canon, want = _host_path(bs)
+        except DeserializationError as he:
+            with pytest.raises(IngestError) as de:
+                ing.ingest(ing.upload(bs))
+            assert (de.value.code, de.value.blob) == (he.code, he.blob)
+            continue
+        out = ing.ingest(ing.upload(bs))
+        _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
+def test_device_ingest_blobs_flush_against_the_pad(eng):
+    """The blob bytes in a buffer of exactly len + CRR_INGEST_PAD bytes (the header's contract), the last
+    blob ending where the padding starts."""
+    from cadence_amd.ingest import INGEST_PAD, DeviceIngest
+    bs = encode_batch(synth_native.mixed(400, mean_len=20))
+    _canon, want = _host_path(bs)
+    ing = DeviceIngest(eng)
+    host = ing.host_arrays(bs)
+    db = ing.upload(bs, host)
+    end = int(bs.blob_off[-1])
+    t = eng.torch.zeros(end + INGEST_PAD, dtype=eng.torch.uint8, device=eng.dev)
+    t[:end].copy_(eng.torch.from_numpy(np.ascontiguousarray(bs.bytes[:end])))
+    db.tensors["bytes"] = t
+    db.c.bytes = t.data_ptr()
+    out = ing.ingest(db)
+    _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
+def test_device_ingest_ids_beyond_2_40(eng):
+    """Activity completions whose scheduled-event reference equals an inserted ID plus 2^40 are deletes of
+    a missing entry (flatten.live_set_bounds compares exact IDs), so they must not lower the live-set
+    bound on the device either: tiers and capacities stay identical to the host path."""
+    hs = synth_mixed.mixed_histories(600, 31, multi_version=False)
+    n_mod = 0
+    for h in hs:
+        for batch in h.batches:
+            for e in batch:
+                if e.event_type == abi.EventType.ActivityTaskCompleted and n_mod < 400:
+                    e.attrs["scheduled_event_id"] = int(e.attrs["scheduled_event_id"]) + (1 << 40)
+                    n_mod += 1
+    assert n_mod > 50
+    b = flatten(hs, known_domains=set(KNOWN_DOMAINS))
+    bs = encode_batch(b)
+    canon, want = _host_path(bs)
+    ing, out = _ingest(eng, bs)
+    _assert_same_inputs(ing.to_host_batch(out), want)
+    from oracle import oracle
+    eng.launch(out)
+    res = eng.download(out)
+    d = diff_results(want, res, canon, oracle.replay(canon, 8))
+    assert not d, d[:3]

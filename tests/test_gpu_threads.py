@@ -76,3 +76,67 @@ def test_call_from_a_thread_without_device_selection(eng):
     eng.torch.cuda.synchronize()
     assert eng.lib.crr_release() == 0
     assert not diff_results(b, eng.replay(b), b, want)
+
+
+@pytest.mark.gpu
+def test_every_stream_entry_point_from_a_fresh_thread(eng):
+    """The thread model holds for every entry point that takes a stream, not only crr_replay: a fresh
+    thread (no crr_set_device) runs the device ingest (plan + layout), crr_replay, crr_compact_rows,
+    crr_widen_events, crr_checksum and crr_ndc_prepare on a stream of device 0; each result equals the
+    same call made from the main thread."""
+    import torch
+    from cadence_amd import ndc
+    from cadence_amd.blobs import KNOWN_DOMAINS, encode_batch
+    from cadence_amd.ingest import DeviceIngest
+    from cadence_amd.wire import pack_events
+    from test_ndc import random_tasks
+    from cadence_amd.decode import decode_histories
+    bs = encode_batch(flatten(synth_mixed.mixed_histories(400, 91, mean_len=50, can_rate=0.2),
+                              known_domains=set(KNOWN_DOMAINS)))
+    b = interleave(decode_histories(bs.to_sources(), known_domains=KNOWN_DOMAINS))   # the host path's layout
+    want = eng.replay(b)
+    nb = ndc.pack(random_tasks(3000, 5))
+    want_ndc, want_items = ndc.prepare_on_device(eng, nb)
+    db_ref = eng.upload(b)
+    eng.launch(db_ref)
+    want_sums = eng.checksum(db_ref)
+
+    got = {}
+    errors = []
+
+    def worker():
+        try:
+            s = torch.cuda.Stream(eng.dev)
+            ing = DeviceIngest(eng)
+            dblobs = ing.upload(bs)
+            out = ing.layout(dblobs, ing.plan(dblobs, s), s)
+            eng.launch(out, s)
+            s.synchronize()
+            got["ingest"] = eng.download(out)
+            db = eng.upload(b)
+            pk = pack_events(b)
+            eng.attach_packed(db, pk)
+            for c, a in pk.data.items():
+                db.tensors["pk_" + c][:a.size].copy_(torch.from_numpy(a))
+            db.tensors["pk_ts_base"].copy_(torch.from_numpy(pk.ts_base))
+            torch.cuda.synchronize(eng.dev)
+            eng.widen(db, s)
+            eng.launch(db, s)
+            eng.compact(db, s)
+            got["sums"] = eng.checksum(db, s)
+            s.synchronize()
+            got["compact"] = eng.download_compact(db)
+            got["ndc"] = ndc.prepare_on_device(eng, nb, s)
+        except Exception as e:   # noqa: BLE001 -- surfaced below
+            errors.append(e)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join(timeout=300)
+    assert not errors, errors
+    assert not diff_results(b, got["compact"].to_replay_result(b), b, want)
+    assert (got["sums"] == want_sums).all()
+    # the device-ingested batch is in the device order of the same layout the host path builds
+    assert not diff_results(b, got["ingest"], b, want)
+    r, items = got["ndc"]
+    assert r.tobytes() == want_ndc.tobytes() and items.tobytes() == want_items.tobytes()

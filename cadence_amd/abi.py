@@ -158,6 +158,7 @@ IN_LDS_SMALL = 2
 IN_WAVE_TAIL = 4
 IN_EMIT_TASKS = 8
 IN_TIERED = 16              # lane workflows ordered by expected live-set size (large_begin / wide_begin)
+IN_HAS_RESUME = 32          # some workflow resumes a loaded state: the compact tiers continue it in LDS
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([

@@ -14,11 +14,11 @@ __global__ void replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, uin
 template <bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __global__ void replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_wide_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 template <bool EMIT>
@@ -320,7 +320,10 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (in->flags & CRR_IN_TIERED) {
         // segments by expected live-set size: 1 entry per map | 2 | compact tiers 1-3 | more (HBM rows)
         auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
-        const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
+        // loaded states (CRR_IN_HAS_RESUME) continue in the compact tiers' arenas (the 1- and 2-slot tiers
+        // rebuild rows from this call's events only): their segments join compact tier 1, which holds both
+        const bool resume = (in->flags & CRR_IN_HAS_RESUME) != 0;
+        const uint32_t lb = resume ? 0u : clampb(in->large_begin, 0), cb = resume ? 0u : clampb(in->compact_begin, lb);
         const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
         const uint32_t hb = clampb(in->hbm_begin, wb);
         const bool run_small = lb > 0, run_large = cb > lb, run_tail = tail && tail_end > n_lane;
@@ -348,21 +351,22 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
         }
-        if (run_c3) {
-          if (emit) hipLaunchKernelGGL((crr::replay_compact3_kernel<true>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
-          else hipLaunchKernelGGL((crr::replay_compact3_kernel<false>), dim3((hb - wb + 63) / 64), dim3(64), 0, s_wide, *in, *out, phase, wb, hb);
-        }
+        // a compact tier's launch: <EMIT, RESUME> instantiations
+#define CRR_LAUNCH_COMPACT(K, lo_, hi_, strm)                                                                     \
+        do {                                                                                                       \
+          const dim3 g_(((hi_) - (lo_) + 63) / 64), b_(64);                                                       \
+          if (emit && resume) hipLaunchKernelGGL((crr::K<true, true>), g_, b_, 0, strm, *in, *out, phase, lo_, hi_);  \
+          else if (emit) hipLaunchKernelGGL((crr::K<true, false>), g_, b_, 0, strm, *in, *out, phase, lo_, hi_);      \
+          else if (resume) hipLaunchKernelGGL((crr::K<false, true>), g_, b_, 0, strm, *in, *out, phase, lo_, hi_);    \
+          else hipLaunchKernelGGL((crr::K<false, false>), g_, b_, 0, strm, *in, *out, phase, lo_, hi_);               \
+        } while (0)
+        if (run_c3) CRR_LAUNCH_COMPACT(replay_compact3_kernel, wb, hb, s_wide);
         if (run_wide)
           hipLaunchKernelGGL(crr::replay_wide_kernel, dim3((n_lane - hb + kWideBlock - 1) / kWideBlock), dim3(kWideBlock), 0,
                              s_wide, *in, *out, phase, hb, n_lane);
-        if (run_c2) {
-          if (emit) hipLaunchKernelGGL((crr::replay_compact2_kernel<true>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
-          else hipLaunchKernelGGL((crr::replay_compact2_kernel<false>), dim3((wb - c2 + 63) / 64), dim3(64), 0, s_c2, *in, *out, phase, c2, wb);
-        }
-        if (run_c1) {
-          if (emit) hipLaunchKernelGGL((crr::replay_compact1_kernel<true>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
-          else hipLaunchKernelGGL((crr::replay_compact1_kernel<false>), dim3((c2 - cb + 63) / 64), dim3(64), 0, s_c1, *in, *out, phase, cb, c2);
-        }
+        if (run_c2) CRR_LAUNCH_COMPACT(replay_compact2_kernel, c2, wb, s_c2);
+        if (run_c1) CRR_LAUNCH_COMPACT(replay_compact1_kernel, cb, c2, s_c1);
+#undef CRR_LAUNCH_COMPACT
         launch_fast(s_large, false, false, lb, cb);
         // the 1-slot segment of a multi-segment (mixed) batch takes the divergent dispatch; a one-class
         // batch (config 2) replays in lockstep and keeps the plain switch

@@ -1251,16 +1251,42 @@ struct CompactArena {
   u32 p_key[P_SLOTS][LANES];
 };
 
-template <class TIER>
+// RESUME (a separate instantiation, launched when the batch holds loaded states: CRR_IN_HAS_RESUME): a
+// loaded state (CRR_WF_FLAG_RESUME, mutableStateBuilder.Load) continues in the arena.  Steps become
+// virtual: this call's event at local step s is v = vk + s (vk = kMaxCompactSteps - n_ev), and a loaded
+// entry -- whose events precede this call -- is v = its ID - id0 < vk, id0 = NextEventID - vk, so IDs
+// keep ordering by v and lookups by ID compare v exactly as for new entries.  A loaded entry keeps its
+// old slot (the row in HBM stays the source of every field the arena does not hold); finalize writes the
+// live rows sorted by v, so the loaded ones come first in their old order and each moves down (or stays):
+// an in-place compaction that reads every old slot before anything overwrites it.  Whatever cannot be
+// held this way -- a loaded ID outside [id0, id0 + vk), rows out of ID order, more loaded rows than
+// slots -- goes to the general path (CRR_INTERNAL_RETRY) before anything in HBM is changed; a retry
+// later in the replay first restores the one HBM word the lane loop may have overwritten (the loaded
+// last version-history item).
+constexpr int CF_SLOT_SHIFT = 26;        // activity: the loaded entry's old slot (4 bits)
+constexpr int TF_SLOT_SHIFT = 18;        // timer: ditto
+constexpr int IF_SLOT_SHIFT = 28;        // child / request-cancel / signal: ditto
+template <class TIER, bool RESUME = false>
 struct CompactTables {
   CRR_TIER_SLOTS
-  static constexpr bool kResumable = false;  // rows are rebuilt from this call's events
+  static constexpr bool kResumable = RESUME;
   static constexpr bool kFusedMapOps = true;
+  static_assert(A_SLOTS <= 16 && T_SLOTS <= 16 && C_SLOTS <= 8 && R_SLOTS <= 8 && S_SLOTS <= 8, "slot fields");
   using Arena = CompactArena<TIER>;
   Arena* M;
   int t;  // threadIdx.x
   const crr_inputs* in;
-  i64 ev_begin;
+  i64 ev_begin;  // column index of virtual step v: ev_begin + v * 64
+  i32 n_ev = 0;
+  // RESUME: v = provenance step + vshift; loaded entries v < vk; the loaded last VH item and reset points
+  i32 vshift = 0, vk = 0;
+  i32 ld_vh_n = 0, ld_rp = 0;
+  i64 ld_vh_id = 0, ld_vh_ver = 0;
+  const crr_activity_row* ld_act = nullptr;  // slot 0 of the workflow's activity rows
+  i64 ld_st = 64;                            // their slot stride
+  __device__ __forceinline__ const crr_activity_row* G_act_loaded(u32 f) const {
+    return ld_act + (i64)((f >> CF_SLOT_SHIFT) & 15u) * ld_st;
+  }
   // No entry stores its event ID: every insert checks that its event's ID is id0 + its step (Cadence
   // assigns IDs consecutively from the first event), so an entry's ID is id0 + the step it keeps anyway,
   // and a lookup by ID compares steps.  An insert that breaks the rule hands the workflow to the general
@@ -1271,13 +1297,13 @@ struct CompactTables {
   // a map changed since its last batch epilogue; an unchanged map would select the same, already
   // created, timer again (a no-op), so its epilogue is skipped (as WaveTables)
   bool dirty_act = false, dirty_timer = false;
-  __device__ __forceinline__ void load(Lane&, const Geo&) {}
 
-  __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin) {
+  __device__ __forceinline__ void init(Arena* arena, const crr_inputs* inputs, i64 begin, i32 n_events = 0) {
     M = arena;
     t = threadIdx.x;
     in = inputs;
     ev_begin = begin;
+    n_ev = n_events;
 #pragma unroll
     for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] = 0;
 #pragma unroll
@@ -1296,10 +1322,141 @@ struct CompactTables {
   __device__ __forceinline__ i64 ev_ver(i32 step) const { return in->ev.version[ix(step)]; }
   __device__ __forceinline__ i64 ev_ts(i32 step) const { return in->ev.timestamp[ix(step)]; }
   __device__ __forceinline__ i64 batch_first_id(i32 step) const {
-    while (step > 0 && !(in->ev.etype[ix(step)] & CRR_ETYPE_BATCH_FIRST)) --step;
+    while (step > vk && !(in->ev.etype[ix(step)] & CRR_ETYPE_BATCH_FIRST)) --step;
     return ev_id(step);
   }
   __device__ __forceinline__ static u32 step_field(u32 w, int k) { return (w >> (kStepBits * k)) & kStepMask; }
+  // a virtual step as this call's provenance step (rows' *_src)
+  __device__ __forceinline__ i32 prov(i32 v) const { return v - vshift; }
+  // the virtual step of a loaded entry's event ID, or -1 (outside what the arena can hold)
+  __device__ __forceinline__ i32 loaded_v(i64 id) const {
+    const u64 d = (u64)id - (u64)id0;
+    return d < (u64)vk ? (i32)d : -1;
+  }
+
+  // mutableStateBuilder.Load (mutable_state_builder.go:306-349) into the arena: every loaded row's
+  // lookup fields (IDs as virtual steps, keys, flags, each activity's earliest timer candidate), all
+  // issued before the first use; the ActivityID map rebuilt (:311-314: the latest ScheduleID of an
+  // ActivityID wins).  Sets L.status = CRR_INTERNAL_RETRY when the state does not fit (nothing written).
+  __device__ __forceinline__ void load(Lane& L, const Geo& G) {
+    if constexpr (RESUME) {
+      vk = kMaxCompactSteps - n_ev;
+      id0 = (i64)((u64)L.next_event_id - (u64)vk);
+      have_id0 = true;
+      vshift = vk - L.src_base;
+      ev_begin -= (i64)vk * 64;
+      ld_vh_n = L.vh_n; ld_vh_id = L.vh_last_id; ld_vh_ver = L.vh_last_ver;
+      ld_rp = L.n_rp;
+      ld_act = G.act(0);
+      ld_st = G.st;
+      dirty_act = dirty_timer = true;  // the loaded timer masks are re-examined by the first epilogue
+      bool ok = L.n_act <= A_SLOTS && L.n_timer <= T_SLOTS && L.n_child <= C_SLOTS && L.n_rc <= R_SLOTS &&
+                L.n_sig <= S_SLOTS && L.n_rp <= P_SLOTS && vk > 0;
+      if (ok) {
+        i32 prev = -1;
+#pragma unroll
+        for (int j = 0; j < A_SLOTS; ++j) {
+          if (j < L.n_act) {
+            const crr_activity_row r = *G.act(j);
+            const i32 v = loaded_v(r.schedule_id);
+            ok = ok && v > prev && r.timer_task_status >= 0 && r.timer_task_status <= 15;
+            prev = v;
+            const bool started = r.started_id != CRR_EMPTY_EVENT_ID;
+            i64 ct = add_seconds(r.scheduled_time, r.schedule_to_close);
+            i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+            if (!started) {
+              cand_min(ct, cy, add_seconds(r.scheduled_time, r.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+            } else {
+              cand_min(ct, cy, add_seconds(r.started_time, r.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+              if (r.heartbeat > 0)
+                cand_min(ct, cy, add_seconds(max(r.started_time, r.last_heartbeat_time), r.heartbeat), CRR_TIMEOUT_HEARTBEAT);
+            }
+            M->a_key[j][t] = r.key;
+            M->a_cand[j][t] = ct;
+            // loaded started / cancel-requested events: any virtual step below vk (their IDs stay in the row)
+            M->a_src[j][t] = (u32)(v < 0 ? 0 : v) | ((started ? 0u : kStepMask) << kStepBits) |
+                             (((r.flags & CRR_ROW_CANCEL_REQUESTED) ? 0u : kStepMask) << (2 * kStepBits));
+            M->a_fl[j][t] = CRR_ROW_LIVE | (r.flags & (CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY)) |
+                            (started ? LF_STARTED : 0u) | ((u32)r.timer_task_status << LF_TTS_SHIFT) |
+                            ((u32)cy << CF_CAND_SHIFT) | ((u32)j << CF_SLOT_SHIFT);
+          }
+        }
+        prev = -1;
+#pragma unroll
+        for (int j = 0; j < T_SLOTS; ++j) {
+          if (j < L.n_timer) {
+            const crr_timer_row r = *G.timer(j);
+            const i32 v = loaded_v(r.started_id);
+            ok = ok && v > prev && (r.task_status == CRR_TIMER_TASK_STATUS_NONE || r.task_status == CRR_TIMER_TASK_STATUS_CREATED);
+            prev = v;
+            M->t_key[j][t] = r.key;
+            M->t_exp[j][t] = r.expiry_time;
+            M->t_fl[j][t] = CRR_ROW_LIVE | (r.task_status == CRR_TIMER_TASK_STATUS_CREATED ? TF_CREATED : 0u) |
+                            ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << TF_SLOT_SHIFT);
+          }
+        }
+        prev = -1;
+#pragma unroll
+        for (int j = 0; j < C_SLOTS; ++j) {
+          if (j < L.n_child) {
+            const crr_child_row r = *G.child(j);
+            const i32 v = loaded_v(r.initiated_id);
+            ok = ok && v > prev;
+            prev = v;
+            const u32 sst = r.started_id != CRR_EMPTY_EVENT_ID ? 0u : kStepMask;
+            M->c_fl[j][t] = CRR_ROW_LIVE | (kChildBatchNone << CHILD_BATCH_SHIFT) | ((u32)(v < 0 ? 0 : v) << 8) |
+                            (sst << (8 + kStepBits)) | ((u32)j << IF_SLOT_SHIFT);
+          }
+        }
+        prev = -1;
+#pragma unroll
+        for (int j = 0; j < R_SLOTS; ++j) {
+          if (j < L.n_rc) {
+            const i32 v = loaded_v(G.rc(j)->initiated_id);
+            ok = ok && v > prev;
+            prev = v;
+            M->r_fl[j][t] = CRR_ROW_LIVE | ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << IF_SLOT_SHIFT);
+          }
+        }
+        prev = -1;
+#pragma unroll
+        for (int j = 0; j < S_SLOTS; ++j) {
+          if (j < L.n_sig) {
+            const i32 v = loaded_v(G.sig(j)->initiated_id);
+            ok = ok && v > prev;
+            prev = v;
+            M->s_fl[j][t] = CRR_ROW_LIVE | ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << IF_SLOT_SHIFT);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < P_SLOTS; ++i)
+          if (i < L.n_rp) M->p_key[i][t] = G.rp(i)->key;
+        // the ActivityID map: an entry is mapped unless a later-scheduled one holds the same ActivityID
+#pragma unroll
+        for (int j = 0; j < A_SLOTS; ++j) {
+          if (j < L.n_act) {
+            const u32 key = M->a_key[j][t];
+            bool mapped = true;
+#pragma unroll
+            for (int k = j + 1; k < A_SLOTS; ++k)
+              if (k < L.n_act && M->a_key[k][t] == key) mapped = false;
+            if (mapped) M->a_fl[j][t] |= CRR_ROW_MAPPED;
+          }
+        }
+      }
+      if (!ok) L.status = CRR_INTERNAL_RETRY;
+    }
+  }
+  // before handing a resumed workflow back: the one loaded HBM word the lane loop may have changed
+  __device__ __forceinline__ void before_retry(const Lane&, const Geo& G) const {
+    if constexpr (RESUME) {
+      if (ld_vh_n > 0) {
+        crr_vh_item* it = G.vh(ld_vh_n - 1);
+        it->event_id = ld_vh_id;
+        it->version = ld_vh_ver;
+      }
+    }
+  }
   __device__ __forceinline__ i64 id_at(u32 step) const { return (i64)((u64)id0 + step); }
   // the step an entry inserted by event ID `id` holds, or kStepMask (matches no entry)
   __device__ __forceinline__ u32 step_of(i64 id) const {
@@ -1332,7 +1489,7 @@ struct CompactTables {
   // slots finds the entry an operation addresses and the first free slot, then the operation's writes.
   __device__ __forceinline__ int map_op(Lane& L, const Geo& G, u32 op, const Ev& ev, i32 s, i64 bfid,
                                         const crr_activity_side& as) {
-    return map_op_unified(L, G, op, ev, s, bfid, as);
+    return map_op_unified(L, G, op, ev, s + vshift, bfid, as);  // provenance step -> virtual step
   }
   // One code path for every map operation, so a divergent wavefront (lanes with different event types)
   // runs one slot scan and one write-back per step instead of one per map and operation: each lane
@@ -1467,12 +1624,21 @@ struct CompactTables {
     const u32 f = M->a_fl[hit][t];
     if ((f & LF_STARTED) && (f & LF_HB_VIS)) return CRR_INTERNAL_RETRY;  // as LdsTables::act_start
     const u32 w = M->a_src[hit][t];
-    const i64 six = ix((i32)step_field(w, 0));
-    const crr_activity_side sa = in->act_side[in->ev.aux[six]];
-    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);
+    const i32 ss = (i32)step_field(w, 0);
+    i64 sched_t;
+    i32 s2c, st2c, hb;
+    if (RESUME && ss < vk) {  // a loaded activity: its row holds the scheduled event's fields
+      const crr_activity_row* r = G_act_loaded(f);
+      sched_t = r->scheduled_time; s2c = r->schedule_to_close; st2c = r->start_to_close; hb = r->heartbeat;
+    } else {
+      const i64 six = ix(ss);
+      const crr_activity_side sa = in->act_side[in->ev.aux[six]];
+      sched_t = in->ev.timestamp[six]; s2c = sa.schedule_to_close; st2c = sa.start_to_close; hb = sa.heartbeat;
+    }
+    i64 ct = add_seconds(sched_t, s2c);
     i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-    cand_min(ct, cy, add_seconds(ev.ts(), sa.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
-    if (sa.heartbeat > 0) cand_min(ct, cy, add_seconds(ev.ts(), sa.heartbeat), CRR_TIMEOUT_HEARTBEAT);
+    cand_min(ct, cy, add_seconds(ev.ts(), st2c), CRR_TIMEOUT_START_TO_CLOSE);
+    if (hb > 0) cand_min(ct, cy, add_seconds(ev.ts(), hb), CRR_TIMEOUT_HEARTBEAT);
     M->a_cand[hit][t] = ct;
     M->a_fl[hit][t] = (f & ~(3u << CF_CAND_SHIFT)) | LF_STARTED | ((u32)cy << CF_CAND_SHIFT);
     M->a_src[hit][t] = (w & ~(kStepMask << kStepBits)) | ((u32)s << kStepBits);
@@ -1484,6 +1650,7 @@ struct CompactTables {
   // once and only the key the later lookups compare stays in LDS (32 B per lane less in tier 2)
   __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
     if (L.n_rp >= P_SLOTS) return CRR_INTERNAL_RETRY;
+    if (RESUME && L.n_rp < ld_rp) return CRR_INTERNAL_RETRY;  // after a reset: would overwrite a loaded row
     if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
     M->p_key[L.n_rp][t] = row.key;
     *G.rp(L.n_rp) = row;
@@ -1606,6 +1773,34 @@ struct CompactTables {
       const u32 w = M->a_src[i][t];
       const i32 ss = (i32)step_field(w, 0), st = (i32)step_field(w, 1), sc = (i32)step_field(w, 2);
       const bool started = (f & LF_STARTED) != 0, cancel = (f & CRR_ROW_CANCEL_REQUESTED) != 0;
+      if (RESUME && ss < vk) {  // a loaded activity: its row, with what this call changed
+        const i32 slot = (i32)((f >> CF_SLOT_SHIFT) & 15u);
+        const bool new_st = started && st >= vk, new_sc = cancel && sc >= vk;
+        const u32 tts = (f >> LF_TTS_SHIFT) & 0xF;
+        const u32 fl = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
+        crr_activity_row* dst = G.act(i);
+        if (slot == i && !new_st && !new_sc && !(f & LF_HB_VIS)) {  // in place: only the bookkeeping words
+          const crr_activity_row* cur = G.act(i);
+          if ((u32)cur->timer_task_status != tts) dst->timer_task_status = (i32)tts;
+          if (cur->flags != fl) dst->flags = fl;
+          continue;
+        }
+        crr_activity_row r = *G.act(slot);
+        if (new_st) {
+          r.started_id = id_at((u32)st);
+          r.started_time = ev_ts(st);
+          r.started_src = prov(st);
+          r.last_heartbeat_time = r.started_time;
+        }
+        if (new_sc) r.cancel_request_id = id_at((u32)sc);
+        if (new_st || new_sc) r.version = ver_of(L, G, max(new_st ? st : -1, new_sc ? sc : -1));
+        if (f & LF_HB_VIS)
+          r.last_hb_timeout_vis_s = unix_seconds(add_seconds(max(r.started_time, r.last_heartbeat_time), r.heartbeat));
+        r.timer_task_status = (i32)tts;
+        r.flags = fl;
+        *dst = r;
+        continue;
+      }
       // the ActivityTaskScheduled event's own fields: timestamp, side record (timeouts)
       const crr_activity_side as = in->act_side[in->ev.aux[ix(ss)]];
       crr_activity_row r;
@@ -1617,8 +1812,8 @@ struct CompactTables {
       r.started_time = started ? ev_ts(st) : CRR_ZERO_TIME;
       r.cancel_request_id = cancel ? id_at((u32)sc) : CRR_EMPTY_EVENT_ID;
       r.last_hb_timeout_vis_s = (f & LF_HB_VIS) ? unix_seconds(add_seconds(r.started_time, as.heartbeat)) : 0;
-      r.sched_src = ss;
-      r.started_src = started ? st : -1;
+      r.sched_src = prov(ss);
+      r.started_src = started ? prov(st) : -1;
       r.schedule_to_start = as.schedule_to_start; r.schedule_to_close = as.schedule_to_close;
       r.start_to_close = as.start_to_close; r.heartbeat = as.heartbeat;
       r.timer_task_status = (i32)((f >> LF_TTS_SHIFT) & 0xF);
@@ -1631,13 +1826,25 @@ struct CompactTables {
     for (i32 i = 0; i < L.n_timer; ++i) {  // ReplicateTimerStartedEvent image
       const u32 f = M->t_fl[i][t];
       const i32 src = (i32)((f >> 8) & kStepMask);
+      const i32 status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+      if (RESUME && src < vk) {  // a loaded timer: only its task status can have changed
+        const i32 slot = (i32)((f >> TF_SLOT_SHIFT) & 15u);
+        if (slot == i) {
+          if (G.timer(i)->task_status != status) G.timer(i)->task_status = status;
+        } else {
+          crr_timer_row r = *G.timer(slot);
+          r.task_status = status;
+          *G.timer(i) = r;
+        }
+        continue;
+      }
       crr_timer_row r;
       r.started_id = id_at((u32)src);
       r.version = ver_of(L, G, src);
       r.expiry_time = M->t_exp[i][t];
-      r.task_status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+      r.task_status = status;
       r.key = M->t_key[i][t];
-      r.src = src;
+      r.src = prov(src);
       r.flags = CRR_ROW_LIVE;
       *G.timer(i) = r;
     }
@@ -1646,13 +1853,25 @@ struct CompactTables {
       const i32 src = (i32)((f >> 8) & kStepMask), sst = (i32)((f >> (8 + kStepBits)) & kStepMask);
       const u32 bd = (f >> CHILD_BATCH_SHIFT) & kChildBatchNone;
       const bool started = sst != (i32)kStepMask;
+      if (RESUME && src < vk) {  // a loaded child: ChildWorkflowExecutionStarted may have come in this call
+        const i32 slot = (i32)((f >> IF_SLOT_SHIFT) & 7u);
+        const bool new_st = started && sst >= vk;
+        if (slot == i && !new_st) continue;
+        crr_child_row r = *G.child(slot);
+        if (new_st) {
+          r.started_id = id_at((u32)sst);
+          r.started_src = prov(sst);
+        }
+        *G.child(i) = r;
+        continue;
+      }
       crr_child_row r;
       r.initiated_id = id_at((u32)src);
       r.version = ver_of(L, G, src);
       r.initiated_batch_id = bd != kChildBatchNone ? r.initiated_id - (i64)bd : batch_first_id(src);
       r.started_id = started ? id_at((u32)sst) : CRR_EMPTY_EVENT_ID;
-      r.src = src;
-      r.started_src = started ? sst : -1;
+      r.src = prov(src);
+      r.started_src = started ? prov(sst) : -1;
       r.flags = CRR_ROW_LIVE;
       r.reserved = 0;
       *G.child(i) = r;
@@ -1660,22 +1879,32 @@ struct CompactTables {
     for (i32 i = 0; i < L.n_rc; ++i) {
       const u32 f = M->r_fl[i][t];
       const i32 src = (i32)((f >> 8) & kStepMask);
+      if (RESUME && src < vk) {  // a loaded request-cancel: unchanged, moved down over the deleted ones
+        const i32 slot = (i32)((f >> IF_SLOT_SHIFT) & 7u);
+        if (slot != i) *G.rc(i) = *G.rc(slot);
+        continue;
+      }
       crr_initiated_row r;
       r.initiated_id = id_at((u32)src);
       r.version = ver_of(L, G, src);
       r.initiated_batch_id = r.initiated_id - (i64)((f >> (8 + kStepBits)) & kStepMask);
-      r.src = src;
+      r.src = prov(src);
       r.flags = CRR_ROW_LIVE;
       *G.rc(i) = r;
     }
     for (i32 i = 0; i < L.n_sig; ++i) {
       const u32 f = M->s_fl[i][t];
       const i32 src = (i32)((f >> 8) & kStepMask);
+      if (RESUME && src < vk) {  // a loaded signal: unchanged, moved down over the deleted ones
+        const i32 slot = (i32)((f >> IF_SLOT_SHIFT) & 7u);
+        if (slot != i) *G.sig(i) = *G.sig(slot);
+        continue;
+      }
       crr_initiated_row r;
       r.initiated_id = id_at((u32)src);
       r.version = ver_of(L, G, src);
       r.initiated_batch_id = r.initiated_id - (i64)((f >> (8 + kStepBits)) & kStepMask);
-      r.src = src;
+      r.src = prov(src);
       r.flags = CRR_ROW_LIVE;
       *G.sig(i) = r;
     }
@@ -2711,6 +2940,10 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
 }
 
 template <class P, class = void>
+struct BeforeRetry { static constexpr bool value = false; };
+template <class P>
+struct BeforeRetry<P, decltype((void)&P::before_retry)> { static constexpr bool value = true; };
+template <class P, class = void>
 struct LaneDispatch { static constexpr bool value = true; };
 template <class P>
 struct LaneDispatch<P, decltype((void)P::kLaneDispatch)> { static constexpr bool value = P::kLaneDispatch; };
@@ -2870,6 +3103,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         L.vh_last_ver = last.version;
       }
       T.load(L, G);
+      if (L.status != CRR_OK) goto done_events;  // a loaded state the policy cannot hold: general path
     } else {
       L.status = CRR_INTERNAL_RETRY;  // rows rebuilt from events cannot hold a loaded state: general path
       goto done_events;
@@ -3217,6 +3451,7 @@ done_events:
 
   if (L.status == CRR_OK && K.on && L.n_tasks > G.task_cap) L.status = CRR_ERR_CAPACITY;
   if (L.status == CRR_INTERNAL_RETRY) {  // the GlobalTables pass replays this workflow from scratch
+    if constexpr (BeforeRetry<P>::value) T.before_retry(L, G);
     out.exec[w].status = CRR_INTERNAL_RETRY;
     T.retry_push(in, out, w);
     return;
@@ -3477,7 +3712,7 @@ using CompactTier2 = CTier<8, 5, 3, 3, 3, 8, 64>;
 // tier 3: 29 KB per block, 5 per CU (the config-3 shard's tier-3 workflows all but ~2 % fit; the rest
 // join the wave tail)
 using CompactTier3 = CTier<12, 8, 6, 4, 4, 8, 64>;
-template <class TIER, bool EMIT>
+template <class TIER, bool EMIT, bool RESUME>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   __shared__ CompactArena<TIER> arena;
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
@@ -3495,10 +3730,10 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
     uniformize_geo(G, lane);
     ev_begin = uniform64(ev_begin - lane) + lane;
   }
-  CompactTables<TIER> T;
-  T.init(&arena, &in, ev_begin);
+  CompactTables<TIER, RESUME> T;
+  T.init(&arena, &in, ev_begin, ev_count0);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<EMIT, CompactTables<TIER>, LaneSource>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
+  replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
@@ -3508,26 +3743,33 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
 #ifndef CRR_COMPACT2_WAVES_PER_EU
 #define CRR_COMPACT2_WAVES_PER_EU 2
 #endif
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_COMPACT1_WAVES_PER_EU) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier1, EMIT>(in, out, phase, lo, hi);
+  replay_compact<CompactTier1, EMIT, RESUME>(in, out, phase, lo, hi);
 }
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_COMPACT2_WAVES_PER_EU) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier2, EMIT>(in, out, phase, lo, hi);
+  replay_compact<CompactTier2, EMIT, RESUME>(in, out, phase, lo, hi);
 }
-template __global__ void replay_compact1_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
-template __global__ void replay_compact1_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
-template __global__ void replay_compact2_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
-template __global__ void replay_compact2_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact1_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact1_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+// loaded states continued in the arena (CRR_IN_HAS_RESUME)
+template __global__ void replay_compact1_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact1_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact2_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
 // tier 3 (workflows beyond tier 2 that hold no loaded state): 55-KB blocks, 2 per CU -- a segment of a
 // few hundred wavefronts, so what matters is its per-event latency (LDS, not the HBM rows' round trips)
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, 1) replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier3, EMIT>(in, out, phase, lo, hi);
+  replay_compact<CompactTier3, EMIT, RESUME>(in, out, phase, lo, hi);
 }
-template __global__ void replay_compact3_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
-template __global__ void replay_compact3_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact3_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact3_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact3_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_compact3_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
 // Long-tail workflows the host expects to outgrow the fast kernels' per-wave arenas
 // (CRR_IN_TIERED, [big_begin, n_wf)): one wavefront each with the 57 KB row arena, then HBM rows;
 // launched next to the fast kernels, so the longest of them is not replayed after them.

@@ -64,8 +64,9 @@ class HistoryBatch:
         return st
 
     def c_flags(self) -> int:
+        resume = self.tiers is not None and self.n_wf and bool((self.wf["flags"] & abi.WF_FLAG_RESUME).any())
         return ((abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
-                | (abi.IN_TIERED if self.tiers is not None else 0))
+                | (abi.IN_TIERED if self.tiers is not None else 0) | (abi.IN_HAS_RESUME if resume else 0))
 
     @property
     def n_wf(self) -> int:
@@ -425,14 +426,19 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
     tier = tier_classes(batch, bounds) if (tiered and n) else np.zeros(n, np.int64)
     if tiered and n:
         resumed = (batch.wf["flags"] & abi.WF_FLAG_RESUME) != 0
+        if resumed.any():
+            # a loaded state continues in a compact tier's arena (CRR_IN_HAS_RESUME) when the loaded rows
+            # plus this batch's growth fit it; in the long tail it goes to the replay_big_kernel segment
+            # (whose HBM-row pass continues it)
+            bounds, tier = resumed_bounds(batch, bounds, resumed)
+            big_tail = {k: np.where(resumed, np.iinfo(np.int32).max, v) for k, v in bounds.items()}
+        else:
+            big_tail = bounds
         # a short history whose live sets outgrow every compact tier joins the wave tail (one
         # wavefront, a row arena searched by 64 lanes) rather than a lane over HBM rows
         if long_threshold is not None:
             is_long |= (tier[order] == WIDE) & ~resumed[order]
-        # a loaded state is continued in place over its HBM rows: the wide (GlobalTables) segment, and
-        # in the long tail the replay_big_kernel segment (whose HBM-row pass continues it)
-        tier = np.where(resumed, WIDE, tier)
-        bounds = {k: np.where(resumed, np.iinfo(np.int32).max, v) for k, v in bounds.items()}
+        bounds = big_tail
     lanes = order[~is_long]
     longs = order[is_long]
     n_big = 0
@@ -593,6 +599,11 @@ TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER, COMPACT3_TIE
 WIDE = len(TIER_SLOTS)
 
 
+def _pair_keys(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """(a, b) int64 pairs as one 16-byte opaque key each (np.isin / np.unique compare them exactly)."""
+    return np.ascontiguousarray(np.stack([a.astype(np.int64), b.astype(np.int64)], axis=1)).view("V16").ravel()
+
+
 def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
     """Approximate peak live-set size per workflow and map (running inserts - deletes of inserted
     keys; reset points: distinct non-empty binary checksums + previous points).  Used only to pick the LDS tier: a
@@ -630,9 +641,9 @@ def live_set_bounds(batch: HistoryBatch) -> Dict[str, np.ndarray]:
         if dpos.size:
             ipos = np.nonzero(d > 0)[0]
             col, ins_col = ("key", "key") if name == "timer" else ("ref", "event_id")
-            mask40 = np.int64((1 << 40) - 1)
-            ik = (wf_of[ipos].astype(np.int64) << 40) | (batch.cols[ins_col][idx[ipos]].astype(np.int64) & mask40)
-            dk = (wf_of[dpos].astype(np.int64) << 40) | (batch.cols[col][idx[dpos]].astype(np.int64) & mask40)
+            # (workflow, full 64-bit value) pairs, compared exactly (ingest_kernel.hip does the same)
+            ik = _pair_keys(wf_of[ipos], batch.cols[ins_col][idx[ipos]])
+            dk = _pair_keys(wf_of[dpos], batch.cols[col][idx[dpos]])
             valid = np.isin(dk, ik)
             if name != "timer":
                 valid &= batch.cols["ref"][idx[dpos]] < batch.cols["event_id"][idx[dpos]]
@@ -673,6 +684,29 @@ WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp":
 # does a workflow go to replay_big_kernel (whose one-wave blocks hold a 57 KB arena): measured on the config-4
 # long tail, sending everything past the arena there costs more (poor occupancy) than the in-place retries.
 WAVE_BIG_CAPS = {"act": 64, "timer": 64, "child": 64, "rc": 64, "sig": 64, "rp": 64}
+
+
+LOADED_COUNT = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "rc": "n_rc", "sig": "n_signal",
+                "rp": "n_reset_points"}
+
+
+def resumed_bounds(batch: HistoryBatch, bounds: Dict[str, np.ndarray], resumed: np.ndarray):
+    """Live-set bounds and tier classes with the loaded states counted in: a resumed workflow's bound is
+    its loaded rows plus this batch's growth (deletes of loaded entries not subtracted: an upper bound).
+    The compact tiers also need the whole history's event IDs to fit their 10-bit steps (the loaded
+    entries' IDs sit below NextEventID; CompactTables::load hands anything else to the general path)."""
+    ex = batch.init.exec if batch.init is not None else None
+    out = {}
+    for m, v in bounds.items():
+        add = np.maximum(ex[LOADED_COUNT[m]].astype(np.int64), 0) if ex is not None else 0
+        out[m] = np.where(resumed, v + add, v)
+    tier = tier_classes(batch, out)
+    if ex is not None:
+        span = ex["next_event_id"].astype(np.int64) + batch.wf["ev_count"].astype(np.int64)
+        tier = np.where(resumed & (span > COMPACT_MAX_EVENTS), WIDE, tier)
+    else:
+        tier = np.where(resumed, WIDE, tier)
+    return out, tier
 
 
 def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:

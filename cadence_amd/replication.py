@@ -118,6 +118,7 @@ class PassiveReplication:
     prefix: ReplayResult = None
     snapshot: Dict[str, object] = None
     n_events: int = 0                     # events applied per step
+    hbm_rows: bool = False                # continue every lane workflow over its HBM rows (A/B only)
 
     def setup(self):
         eng, torch, b = self.eng, self.eng.torch, self.batch
@@ -135,12 +136,14 @@ class PassiveReplication:
         self.n_events = sb.n_events
         dn = eng.upload(sb)
         dn.c_out = db.c_out                        # apply onto the loaded rows in place
-        # resumed workflows continue over HBM rows: every lane workflow in the wide (GlobalTables)
-        # segment, the long tail in the tail / big kernels (their HBM-row pass resumes)
-        if sb.tiers is not None:
+        # the loaded states continue in the compact tiers' LDS arenas (CRR_IN_HAS_RESUME, set by the
+        # batch's flags): each workflow keeps the segment of its whole history, whose live-set bound covers
+        # the loaded rows plus the new batch's; hbm_rows=True instead continues every lane workflow over its
+        # HBM rows (the wide GlobalTables segment) -- the round-3 path, kept for A/B measurements
+        if sb.tiers is not None and self.hbm_rows:
             dn.c_in.large_begin = dn.c_in.compact_begin = dn.c_in.compact2_begin = dn.c_in.wide_begin = 0
             dn.c_in.hbm_begin = 0
-            dn.c_in.flags &= ~abi.IN_LDS_SMALL
+            dn.c_in.flags &= ~(abi.IN_LDS_SMALL | abi.IN_HAS_RESUME)
         for name, *_ in abi.TABLES:                # only db's outputs are used
             dn.tensors.pop("out_" + name, None)
         dn.tensors.pop("exec", None)

@@ -286,8 +286,8 @@ typedef struct crr_inputs {
          [compact_begin, compact2_begin) compact tier 1 (4 / 3 / 2 / 1 / 1 / 4 slots)
          [compact2_begin, wide_begin)    compact tier 2 (8 / 6 / 3 / 3 / 3 / 8 slots)
          [wide_begin, hbm_begin)         compact tier 3 (16 / 12 / 8 / 6 / 6 / 10 slots)
-         [hbm_begin, lanes)              more, or a loaded state (CRR_WF_FLAG_RESUME): the workflow's
-                                         own HBM rows
+         [hbm_begin, lanes)              more: the workflow's own HBM rows (a loaded state,
+                                         CRR_WF_FLAG_RESUME, stays in its segment with CRR_IN_HAS_RESUME)
        (hbm_begin below wide_begin, e.g. 0, reads as wide_begin: no compact tier 3 segment)
        (activity / timer / child / request-cancel / signal / reset-point slots; flatten.py) */
     uint32_t                 large_begin;
@@ -311,6 +311,11 @@ typedef struct crr_inputs {
                                    size (large_begin / wide_begin); each segment is launched with the
                                    LDS tier that holds it (1, 2 or 8 entries per map).  A hint like
                                    CRR_IN_LDS_SMALL (which it overrides): speed only, never results */
+#define CRR_IN_HAS_RESUME 32u   /* some workflow carries CRR_WF_FLAG_RESUME (CRR_IN_TIERED batches): the
+                                   compact tiers continue loaded states in their LDS arenas, and the 1- and
+                                   2-slot segments [0, compact_begin) join compact tier 1 (which holds
+                                   both).  Without it a loaded state in an LDS segment is replayed by the
+                                   general path over its HBM rows: speed only, never results */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (208 B).  "step" / "*_src" values below are

@@ -20,6 +20,7 @@ def main():
     p.add_argument("--wf", type=int, default=1_250_000)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
+    p.add_argument("--hbm-rows", action="store_true", help="every lane workflow over its HBM rows (round-3 path)")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -38,7 +39,7 @@ def main():
     one_shot = eng.download(db)
     del db
     torch.cuda.empty_cache()
-    pr = PassiveReplication(eng, batch)
+    pr = PassiveReplication(eng, batch, hbm_rows=a.hbm_rows)
     pr.setup()
     setup_s = time.time() - t0
     ms = []
@@ -50,7 +51,7 @@ def main():
         ms.append(sum(x for x in eng.last_kernel_ms()[:2] if x > 0))
     v = pr.verify(one_shot)
     med = float(np.median(ms[1:]))
-    print(json.dumps({"workflows": a.wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
+    print(json.dumps({"hbm_rows": a.hbm_rows, "workflows": a.wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
                       "events_per_s": pr.n_events / (med * 1e-3), "verify": v, "setup_s": setup_s}), flush=True)
 
 

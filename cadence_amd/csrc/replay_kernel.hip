@@ -1690,7 +1690,9 @@ struct CompactTables {
         const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
         if (!((f >> LF_TTS_SHIFT) & timer_mask(y))) {
           M->a_fl[bj][t] = f | (timer_mask(y) << LF_TTS_SHIFT) | (y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
-          K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, bt, id_at(bs), 0, -1);
+          // the task carries ActivityInfo.Attempt: 0 for this call's activities, a loaded row's own
+          const i32 att = (RESUME && K.on && bs < (u32)vk) ? G_act_loaded(f)->attempt : 0;
+          K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, bt, id_at(bs), att, -1);
         }
       }
     }

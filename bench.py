@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the CPUs this process may use)")
     p.add_argument("--cpu-sample", type=int, default=1_000_000, help="config 2 workflows in the CPU baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall seconds per CPU-baseline figure")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="collective backend for N > 1 (nccl = RCCL; gloo: e.g. several ranks sharing one GPU)")
+    p.add_argument("--device", type=int, default=-1, help="GPU of this rank (default LOCAL_RANK)")
     a = p.parse_args()
     if a.steps > MAX_TIMED_STEPS or a.config_steps > MAX_TIMED_STEPS:
         p.error(f"--steps / --config-steps: at most {MAX_TIMED_STEPS} launches are timed per region")
@@ -89,11 +92,16 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(self.local_rank)
+        self.device = args.device if args.device >= 0 else self.local_rank
+        self.backend = args.backend
+        torch.cuda.set_device(self.device)
         if self.world > 1:
-            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", self.local_rank))
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", self.device))
+            else:
+                dist.init_process_group("gloo", init_method="env://")
         from cadence_amd.engine import ReplayEngine
-        self.eng = ReplayEngine(self.local_rank)
+        self.eng = ReplayEngine(self.device)
 
     def barrier(self):
         if self.world > 1:
@@ -101,7 +109,7 @@ class Ctx:
 
     def reduce(self, values, op="max"):
         """All-reduce a list of floats over the ranks (identity at N=1)."""
-        t = self.torch.tensor(values, dtype=self.torch.float64, device="cuda")
+        t = self.torch.tensor(values, dtype=self.torch.float64, device="cuda" if self.backend == "nccl" else "cpu")
         if self.world > 1:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return [float(x) for x in t.cpu()]
@@ -168,16 +176,18 @@ def config2(ctx):
     canon = synth.activity_chain(ids.size, k, synth.SEED_C2, with_keys=False, wf_ids=ids)
     batch = interleave(canon)
     db = eng.upload(batch)
+    # each device position's global workflow ID, as the digest's identity key
+    keys = torch.from_numpy(cdist.device_keys(batch, ids)).to(eng.dev)
     setup_s = time.time() - t0
     n_wf, n_events = batch.n_wf, batch.n_events
 
     def exchange():
-        d = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"])
+        d = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"], keys)
         cdist.all_reduce_digest(torch, ctx.dist, d)
 
     wall, ms = timed_steps(ctx, db, args.steps, args.warmup, per_step=exchange if ctx.world > 1 else None)
     kernel_avg_ms = float(np.mean(ms))
-    digest = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"])
+    digest = cdist.digest_torch(torch, db.tensors["exec"], n_wf, db.tensors["wf"], keys)
     if ctx.world > 1:
         cdist.all_reduce_digest(torch, ctx.dist, digest)
     digest = digest.cpu().numpy()
@@ -217,7 +227,8 @@ def config2(ctx):
                                f"(one {args.workflows * ctx.world}-workflow workload split by history shard), "
                                "wave-interleaved SoA resident in HBM",
                    "workflows_per_gpu": n_wf, "events_per_workflow": n_events // n_wf,
-                   "parallelism": f"shard-partitioned x{ctx.world} (RCCL all-reduce of counters + checksum digest)"},
+                   "parallelism": f"shard-partitioned x{ctx.world} ("
+                                  f"{'RCCL' if ctx.backend == 'nccl' else 'gloo'} all-reduce of counters + checksum digest)"},
         "workflows_per_s": tot_wf * args.steps / wall,
         "all_ok": bool(digest[2] == 0 and digest[1] == tot_wf),
         "digest": [int(x) for x in digest],
@@ -258,7 +269,7 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
     db = eng.upload(batch)
     wall, ms = timed_steps(ctx, db, args.config_steps, 1)
     res = eng.download(db)
-    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"])
+    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"], cdist.device_keys(batch))
     tot_events, tot_wf, tot_ok = ctx.reduce([float(batch.n_events), float(batch.n_wf), float(digest[1])], op="sum")
     grp_ms = float(np.mean(ms))
     out = {"workload": workload, "value": tot_events * args.config_steps / wall, "unit": "events/s",
@@ -340,7 +351,7 @@ def config5(ctx, n_wf, shard):
     wall, ms = timed_steps(ctx, db, args.config_steps, 1)
     res = eng.download(db)
     from cadence_amd import dist as cdist
-    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"])
+    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"], cdist.device_keys(batch))
     tot_ev, tot_wf = ctx.reduce([float(batch.n_events), float(batch.n_wf)], op="sum")
     out = {"workload": f"config 5: {n_wf} multi-version mixed histories per GPU rebuilt onto reset branches "
                        "(state_rebuilder.go:97-191: target branch token, last-item check, RefreshTasks), failover "
@@ -523,9 +534,10 @@ def blob_to_rows(ctx, canon, resident_digest, name, chunks=8):
     sr.run()
     runs = [sr.run() for _ in range(3)]
     med = float(np.median([r["wall_s"] for r in runs]))
-    digest = np.zeros(6, np.int64)
-    for cr, evc in zip(sr.results(), sr.ev_counts()):
-        digest += cdist.digest_numpy(cr.exec, evc)
+    digest = np.zeros(cdist.DIGEST_LEN, np.int64)
+    with np.errstate(over="ignore"):
+        for cr, evc, keys in zip(sr.results(), sr.ev_counts(), sr.device_keys()):
+            digest += cdist.digest_numpy(cr.exec, evc, keys)
     r0 = runs[0]
     fig = {"workload": name, "events_per_s": r0["events"] / med, "ms": med * 1e3, "events": r0["events"],
            "workflows": bs.n_wf, "blobs": bs.n_blobs, "blob_bytes": bs.n_bytes,
@@ -588,9 +600,10 @@ def end_to_end(ctx, n_wf, k, chunks=8):
         runs = [sr.run() for _ in range(3)]
         med = float(np.median([r["wall_s"] for r in runs]))
         r0 = runs[0]
-        digest = np.zeros(6, np.int64)
-        for cr, c in zip(sr.results(), sr.chunks):
-            digest += cdist.digest_numpy(cr.exec, c.batch.wf["ev_count"])
+        digest = np.zeros(cdist.DIGEST_LEN, np.int64)
+        with np.errstate(over="ignore"):
+            for (a, b), cr, c in zip(zip(bounds[:-1], bounds[1:]), sr.results(), sr.chunks):
+                digest += cdist.digest_numpy(cr.exec, c.batch.wf["ev_count"], cdist.device_keys(c.batch, np.arange(a, b)))
         fig = {"events_per_s": r0["events"] / med, "ms": med * 1e3, "events": r0["events"], "chunks": chunks,
                "h2d_bytes": r0["h2d_bytes"], "d2h_bytes": r0["d2h_bytes"], "h2d_bytes_per_event": r0["h2d_bytes"] / r0["events"],
                "h2d_GBs": r0["h2d_bytes"] / med / 1e9, "setup_s": setup, "digest": [int(x) for x in digest]}

@@ -331,6 +331,18 @@ class BlobStreamingReplay:
             out.append(CompactResult(p["host_exec"].numpy().view(abi.EXEC_ROW).copy(), off, rows))
         return out
 
+    def device_keys(self) -> List[np.ndarray]:
+        """Per chunk, the digest identity keys in device order: each position's workflow index in the
+        whole (unsplit) blob set -- the chunk's base plus the layout's perm."""
+        from .dist import workflow_keys
+        out, base = [], 0
+        for p in self.parts:
+            n = p["n"]
+            perm = p["out"].tensors["perm"][:n].cpu().numpy().astype(np.int64)
+            out.append(workflow_keys(base + perm))
+            base += n
+        return out
+
     def ev_counts(self) -> List[np.ndarray]:
         """Per chunk, the descriptors' ev_count in device order (for dist.digest_numpy)."""
         out = []

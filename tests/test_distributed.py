@@ -31,10 +31,19 @@ def _worker(rank, world, port, q):
     # the digest code the GPU ranks run (dist.digest_torch over the raw exec-row bytes), here on CPU tensors
     raw = torch.from_numpy(np.ascontiguousarray(res.exec[mine]).view(np.uint8).reshape(-1).copy())
     wfb = torch.from_numpy(np.ascontiguousarray(batch.wf[mine]).view(np.uint8).reshape(-1).copy())
-    t = cdist.digest_torch(torch, raw, int(mine.sum()), wfb)
-    assert (t.numpy() == cdist.digest_numpy(res.exec[mine], batch.wf["ev_count"][mine])).all()
+    keys = cdist.workflow_keys(np.arange(batch.n_wf))            # global workflow IDs -> identity keys
+    t = cdist.digest_torch(torch, raw, int(mine.sum()), wfb, torch.from_numpy(keys[mine].copy()))
+    assert (t.numpy() == cdist.digest_numpy(res.exec[mine], batch.wf["ev_count"][mine], keys[mine])).all()
+    # a rank that swapped two of its workflows' results (a permutation bug) must not reduce to the whole
+    ok = np.nonzero(mine & (res.exec["status"] == 0))[0]
+    sw = res.exec.copy()
+    sw[[ok[0], ok[1]]] = sw[[ok[1], ok[0]]]
+    t_sw = cdist.digest_torch(torch, torch.from_numpy(np.ascontiguousarray(sw[mine]).view(np.uint8).reshape(-1).copy()),
+                              int(mine.sum()), wfb, torch.from_numpy(keys[mine].copy()))
     cdist.all_reduce_digest(torch, dist, t)
-    q.put((rank, t.numpy().tolist(), cdist.digest_numpy(res.exec, batch.wf["ev_count"]).tolist()))
+    cdist.all_reduce_digest(torch, dist, t_sw)
+    q.put((rank, t.numpy().tolist(), cdist.digest_numpy(res.exec, batch.wf["ev_count"], keys).tolist(),
+           t_sw.numpy().tolist()))
     dist.destroy_process_group()
 
 
@@ -54,6 +63,8 @@ def test_two_rank_shard_partition_and_digest_reduce():
     assert reduced[0] == reduced[1]
     assert reduced[0] == out[0][2]       # sum over disjoint shards == digest of the whole batch
     assert reduced[0][1] == 64 * 8        # every workflow replayed exactly once
+    swapped = out[0][3]
+    assert swapped[:4] == reduced[0][:4] and swapped[4] != reduced[0][4]   # identity-binding fold
 
 
 def test_rank_workflows_partition_one_workload():

@@ -110,13 +110,25 @@ def test_device_digest_equals_host_digest(eng):
     b = interleave(_mixed(2000, 5, mean_len=50, invalid_rate=0.1, can_rate=0.3))
     db = eng.upload(b)
     eng.launch(db)
-    d_dev = dist.digest_torch(torch, db.tensors["exec"], b.n_wf, db.tensors["wf"]).cpu().numpy()
+    keys_h = dist.device_keys(b)
+    keys = torch.from_numpy(keys_h).to(eng.dev)
+    d_dev = dist.digest_torch(torch, db.tensors["exec"], b.n_wf, db.tensors["wf"], keys).cpu().numpy()
     res = eng.download(db)
-    assert (d_dev == dist.digest_numpy(res.exec, b.wf["ev_count"])).all()
+    assert (d_dev == dist.digest_numpy(res.exec, b.wf["ev_count"], keys_h)).all()
     assert d_dev[1] + d_dev[2] == b.n_wf and d_dev[2] > 0
     ok = res.exec["status"] == 0
     assert d_dev[0] == int(b.wf["ev_count"][ok].sum())
     assert (b.wf["flags"] & abi.WF_FLAG_NEW_RUN).any()
+    # identity binding: two OK workflows' results swapped (counts and checksum sum unchanged) change it
+    i, j = [int(x) for x in np.nonzero(ok & (res.exec["checksum"] != res.exec["checksum"][np.argmax(ok)]))[0][:1]] + \
+           [int(np.argmax(ok))]
+    row = abi.EXEC_ROW.itemsize
+    ex = db.tensors["exec"]
+    a, c = ex[i * row:(i + 1) * row].clone(), ex[j * row:(j + 1) * row].clone()
+    ex[i * row:(i + 1) * row].copy_(c)
+    ex[j * row:(j + 1) * row].copy_(a)
+    d_sw = dist.digest_torch(torch, ex, b.n_wf, db.tensors["wf"], keys).cpu().numpy()
+    assert (d_sw[:4] == d_dev[:4]).all() and d_sw[4] != d_dev[4]
 
 
 @pytest.mark.gpu
@@ -131,10 +143,11 @@ def test_device_digest_counts_resumed_events(eng):
     pr.step()
     n = pr.batch.n_wf
     exec_t, wf_t = pr.db.tensors["exec"], pr.db_new.tensors["wf"]     # loaded rows updated in place
-    d_dev = dist.digest_torch(torch, exec_t, n, wf_t).cpu().numpy()
+    keys_h = dist.device_keys(pr.batch)
+    d_dev = dist.digest_torch(torch, exec_t, n, wf_t, torch.from_numpy(keys_h).to(eng.dev)).cpu().numpy()
     res = eng.download(pr.db)
     wf = wf_t[: n * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
-    assert (d_dev == dist.digest_numpy(res.exec, wf["ev_count"])).all()
+    assert (d_dev == dist.digest_numpy(res.exec, wf["ev_count"], keys_h)).all()
     ok = res.exec["status"] == 0
     assert d_dev[0] == int(wf["ev_count"][ok].sum()) and 0 < d_dev[0] <= pr.n_events
     # NextEventID - 1 would count the loaded prefix too

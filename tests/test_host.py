@@ -154,11 +154,52 @@ def test_digest_numpy_matches_torch():
     rows["inconsistencies"] = [0, 1, 0, 2, 0]
     wf = np.zeros(5, abi.WORKFLOW)
     wf["ev_count"] = [29, 23, 4, 3, 2 ** 31 - 1]
+    rows["fail_step"] = [-1, -1, 2, -1, -1]
     raw = torch.from_numpy(rows.view(np.uint8).copy())
-    d = dist.digest_numpy(rows, wf["ev_count"])
-    assert (dist.digest_torch(torch, raw, 5, torch.from_numpy(wf.view(np.uint8).copy())).numpy() == d).all()
+    keys = dist.workflow_keys(np.array([10, 11, 12, 2 ** 40, 7]))
+    d = dist.digest_numpy(rows, wf["ev_count"], keys)
+    tk = torch.from_numpy(keys.copy())
+    assert (dist.digest_torch(torch, raw, 5, torch.from_numpy(wf.view(np.uint8).copy()), tk).numpy() == d).all()
     assert d[0] == 29 + 23 + 3 + 2 ** 31 - 1
     assert d[1] == 4 and d[2] == 1 and d[5] == 3
+
+
+def test_digest_binds_results_to_workflow_identity():
+    """Swapping two workflows' results keeps every count and the plain checksum sum, but changes the
+    identity fold (and so does swapping two failures); the folds are sums, so any partition of the
+    workflows over ranks reduces to the whole job's digest."""
+    import torch
+    from cadence_amd import dist
+    rng = np.random.default_rng(3)
+    n = 1000
+    rows = np.zeros(n, abi.EXEC_ROW)
+    rows["status"] = np.where(rng.random(n) < 0.1, 7, 0)
+    rows["checksum"] = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    rows["fail_step"] = np.where(rows["status"] != 0, rng.integers(0, 50, n), -1)
+    ev = rng.integers(1, 60, n)
+    keys = dist.workflow_keys(rng.permutation(10 ** 6)[:n])
+    d = dist.digest_numpy(rows, ev, keys)
+    ok = np.nonzero(rows["status"] == 0)[0]
+    bad = np.nonzero(rows["status"] != 0)[0]
+    sw = rows.copy()
+    sw[[ok[0], ok[1]]] = sw[[ok[1], ok[0]]]
+    ev_sw = ev.copy()
+    ev_sw[[ok[0], ok[1]]] = ev_sw[[ok[1], ok[0]]]
+    d_sw = dist.digest_numpy(sw, ev_sw, keys)
+    assert (d_sw[[0, 1, 2, 3, 5, 6]] == d[[0, 1, 2, 3, 5, 6]]).all() and d_sw[4] != d[4]
+    sf = rows.copy()
+    sf["fail_step"][bad[0]] += 1
+    assert dist.digest_numpy(sf, ev, keys)[6] != d[6]
+    # partitions reduce to the whole (wrapping int64 sums)
+    part = rng.integers(0, 4, n)
+    with np.errstate(over="ignore"):
+        tot = sum(dist.digest_numpy(rows[part == r], ev[part == r], keys[part == r]) for r in range(4))
+    assert (tot == d).all()
+    raw = torch.from_numpy(rows.view(np.uint8).copy())
+    wf = np.zeros(n, abi.WORKFLOW)
+    wf["ev_count"] = ev
+    t = dist.digest_torch(torch, raw, n, torch.from_numpy(wf.view(np.uint8).copy()), torch.from_numpy(keys.copy()))
+    assert (t.numpy() == d).all()
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="library not built")

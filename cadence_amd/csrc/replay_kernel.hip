@@ -3714,9 +3714,31 @@ using CompactTier2 = CTier<8, 5, 3, 3, 3, 8, 64>;
 // tier 3: 29 KB per block, 5 per CU (the config-3 shard's tier-3 workflows all but ~2 % fit; the rest
 // join the wave tail)
 using CompactTier3 = CTier<12, 8, 6, 4, 4, 8, 64>;
-template <class TIER, bool EMIT, bool RESUME>
+// CRC tables in LDS for a compact tier's checksum (copied from the constant-memory ones at block start)
+// instead of per-lane gathers from kCrcGlobal through the L1: an 8-KB table gather touches many lines per
+// instruction, and with few events per workflow (a resume) the checksum is a large part of its work
+// (passive replication on the config-3 shard: 1.02 -> 0.91 ms per step with the resume instantiations'
+// tables in LDS, A/B on one box; their occupancy is register-limited, so the 8 KB costs no waves)
+#ifndef CRR_COMPACT_LDS_CRC_MASK  // bit k: tier k+1's resume instantiation (bit 3+k: its fresh one)
+#define CRR_COMPACT_LDS_CRC_MASK 7
+#endif
+template <int TIER_NO, bool RESUME>
+struct CompactLdsCrc {
+  static constexpr bool value = ((CRR_COMPACT_LDS_CRC_MASK >> ((TIER_NO - 1) + (RESUME ? 0 : 3))) & 1) != 0;
+};
+template <class TIER, bool EMIT, bool RESUME, int TIER_NO>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   __shared__ CompactArena<TIER> arena;
+  const u32* crc_tables = kCrcGlobal.v;
+  if constexpr (CompactLdsCrc<TIER_NO, RESUME>::value) {
+    __shared__ u32 crc_lds[8 * 256];
+    const uint4* src = reinterpret_cast<const uint4*>(kCrcGlobal.v);
+    uint4* dst = reinterpret_cast<uint4*>(crc_lds);
+#pragma unroll
+    for (int i = 0; i < 8 * 256 / 4 / 64; ++i) dst[i * 64 + threadIdx.x] = src[i * 64 + threadIdx.x];
+    __syncthreads();
+    crc_tables = crc_lds;
+  }
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
   if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
@@ -3735,23 +3757,27 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   CompactTables<TIER, RESUME> T;
   T.init(&arena, &in, ev_begin, ev_count0);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, kCrcGlobal.v);
+  replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables);
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
 #ifndef CRR_COMPACT1_WAVES_PER_EU
 #define CRR_COMPACT1_WAVES_PER_EU 3
 #endif
+// the resume instantiation at 2: its loaded-row reads and in-place finalize spill at 168 VGPRs
+#ifndef CRR_COMPACT1_RESUME_WAVES_PER_EU
+#define CRR_COMPACT1_RESUME_WAVES_PER_EU 2
+#endif
 #ifndef CRR_COMPACT2_WAVES_PER_EU
 #define CRR_COMPACT2_WAVES_PER_EU 2
 #endif
 template <bool EMIT, bool RESUME>
-__global__ void __launch_bounds__(64, CRR_COMPACT1_WAVES_PER_EU) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier1, EMIT, RESUME>(in, out, phase, lo, hi);
+__global__ void __launch_bounds__(64, RESUME ? CRR_COMPACT1_RESUME_WAVES_PER_EU : CRR_COMPACT1_WAVES_PER_EU) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
+  replay_compact<CompactTier1, EMIT, RESUME, 1>(in, out, phase, lo, hi);
 }
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_COMPACT2_WAVES_PER_EU) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier2, EMIT, RESUME>(in, out, phase, lo, hi);
+  replay_compact<CompactTier2, EMIT, RESUME, 2>(in, out, phase, lo, hi);
 }
 template __global__ void replay_compact1_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact1_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
@@ -3766,7 +3792,7 @@ template __global__ void replay_compact2_kernel<true, true>(crr_inputs, crr_outp
 // few hundred wavefronts, so what matters is its per-event latency (LDS, not the HBM rows' round trips)
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, 1) replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier3, EMIT, RESUME>(in, out, phase, lo, hi);
+  replay_compact<CompactTier3, EMIT, RESUME, 3>(in, out, phase, lo, hi);
 }
 template __global__ void replay_compact3_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact3_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);

@@ -40,6 +40,22 @@ PATCHES = {
                   "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",
                   "    crr_activity_side sa{}; sa.schedule_to_close = 20; sa.start_to_close = 10; (void)six;\n"
                   "    i64 ct = add_seconds(ev.ts(), sa.schedule_to_close);")],
+    # passive replication in the compact tiers (CompactTables<TIER, true>), tools/prof_replication.py --lib:
+    # the whole step without the checksum
+    "rnocrc": [("  const bool want_crc = L.status == CRR_OK;", "  const bool want_crc = false;")],
+    # resumed compact workflows stopping early (the exec row written back as loaded): after the exec-row
+    # read / after the arena load -- the floor of each part of the step
+    "rnop": [("      const crr_exec_row X = out.exec[w];\n",
+              "      const crr_exec_row X = out.exec[w];\n"
+              "      if constexpr (FusedMapOps<P>::value) { out.exec[w] = X; return; }\n")],
+    "rload": [("      if (L.status != CRR_OK) goto done_events;  // a loaded state the policy cannot hold: general path\n",
+               "      if (L.status != CRR_OK) goto done_events;  // a loaded state the policy cannot hold: general path\n"
+               "      if constexpr (FusedMapOps<P>::value) { out.exec[w] = X; return; }\n")],
+    # ... without the checksum and the finalize
+    "rtail": [("  const bool want_crc = L.status == CRR_OK;", "  const bool want_crc = false;"),
+              ("  T.finalize(L, G);\n\n  crr_exec_row R;", "  if (0) T.finalize(L, G);\n\n  crr_exec_row R;")],
+    # ... without the finalize (no rows written)
+    "rnofin": [("  T.finalize(L, G);\n\n  crr_exec_row R;", "  if (0) T.finalize(L, G);\n\n  crr_exec_row R;")],
 }
 
 

@@ -2626,8 +2626,11 @@ struct TokenWords {
 };
 
 template <class IDS>
+// last_id / last_ver (have_last): the last version-history item as the replay holds it in registers (the
+// row it just wrote is not read back: a store -> load round trip per workflow)
 __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids, const Geo& G, const TokenWords& TW,
-                                           const uint8_t* arena, const u32* tables, u32* out_len) {
+                                           const uint8_t* arena, const u32* tables, u32* out_len,
+                                           bool have_last = false, i64 last_id = 0, i64 last_ver = 0) {
   Crc K;
   K.init(tables);
   K.u8(0x59);                                                            // preambleVersion0
@@ -2671,9 +2674,11 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
   }
   K.list_header(20, 12, (u32)R.n_vh_items);
   for (i32 i = 0; i < R.n_vh_items; ++i) {                               //   VersionHistoryItem (shared.go:92375)
-    const crr_vh_item* it = G.vh(i);
-    K.field(10, 10); K.be64(it->event_id);
-    K.field(10, 20); K.be64(it->version);
+    const bool reg = have_last && i == R.n_vh_items - 1;
+    const i64 eid = reg ? last_id : G.vh(i)->event_id;
+    const i64 ever = reg ? last_ver : G.vh(i)->version;
+    K.field(10, 10); K.be64(eid);
+    K.field(10, 20); K.be64(ever);
     K.u8(0);
   }
   K.u8(0);  // VersionHistory stop
@@ -3066,6 +3071,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step) + L.src_base; goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
 
+  // step 0's columns in flight first: a loaded state's exec row and rows (below) are read meanwhile
+  src.start();
   if (!P::fits(n_ev)) {
     L.status = CRR_INTERNAL_RETRY;  // beyond the policy's encodings (CompactTables' 10-bit steps)
     goto done_events;
@@ -3112,7 +3119,6 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     }
   }
 
-  src.start();
   if constexpr (std::is_same<SRC, WaveSource>::value) {
     // Wavefront per workflow, a 64-event chunk at a time (lane l: event c0 + l).  The prologue of
     // :98-129 for every event of the chunk runs lane-parallel: each lane checks its (ID, version)
@@ -3510,7 +3516,7 @@ done_events:
   R.expiration_ns = L.expiration_ns;
   R.src_next = L.src_base + n_ev;
   R.reserved = 0;
-  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len);
+  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len, true, L.vh_last_id, L.vh_last_ver);
   out.exec[w] = R;
 }
 

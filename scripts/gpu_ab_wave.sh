@@ -13,7 +13,7 @@ fi
 for r in $(seq 1 ${REPS:-2}); do
   for V in ${VARIANTS:-product}; do
     L=cadence_amd/libcadence_replay.so; [ "$V" != product ] && L=tools/variants/$V.so
-    if [ -n "${C4:-1}" ]; then
+    if [ -n "${C4-1}" ]; then
       timeout -k 10 300 python tools/prof_longtail.py --native --n 2000 --thresholds 256 --reps 3 --lib $L > gpurun_out/ab_c4_${V}_$r.log 2>&1
       rc=$?; log "c4 $V $r rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/ab_c4_${V}_$r.log; exit $rc; }
       echo "c4 $V $(grep -o '"median_ms": [0-9.]*' gpurun_out/ab_c4_${V}_$r.log | head -1) $(grep -o '"ok": [0-9]*' gpurun_out/ab_c4_${V}_$r.log | head -1)"

@@ -132,6 +132,8 @@ class Status(enum.IntEnum):
     TIMER_SEQUENCE = 14
     REBUILD_LAST_ITEM = 15
     NEW_RUN_MISSING = 16
+    MISSING_START_EVENT = 17          # ErrMissingWorkflowStartEvent (RefreshTasks)
+    MISSING_COMPLETION_EVENT = 18     # ErrMissingWorkflowCompletionEvent (RefreshTasks)
     NDC_NO_LCA = 20
     NDC_LCA_NOT_IN_BRANCH = 21
     NDC_FIRST_ITEM_MISMATCH = 22
@@ -159,6 +161,7 @@ IN_WAVE_TAIL = 4
 IN_EMIT_TASKS = 8
 IN_TIERED = 16              # lane workflows ordered by expected live-set size (large_begin / wide_begin)
 IN_HAS_RESUME = 32          # some workflow resumes a loaded state: the compact tiers continue it in LDS
+IN_ADVANCED_VISIBILITY = 64  # RefreshTasks emits the search-attributes task
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([
@@ -169,7 +172,7 @@ ACTIVITY_SIDE = np.dtype([
 START_SIDE = np.dtype([
     ("decision_start_to_close", "<i4"), ("workflow_timeout", "<i4"), ("first_decision_backoff", "<i4"),
     ("initiator", "<i4"), ("parent_domain_status", "<i4"), ("prev_reset_key_off", "<u4"),
-    ("prev_reset_count", "<i4"), ("attempt", "<i4"), ("expiration_ns", "<i8"), ("reserved", "<i8")])
+    ("prev_reset_count", "<i4"), ("attempt", "<i4"), ("expiration_ns", "<i8"), ("refresh_jitter", "<i8")])
 
 WORKFLOW = np.dtype([
     ("ev_begin", "<i8"), ("ev_count", "<i4"), ("empty_batch_at", "<i4"),

@@ -234,7 +234,8 @@ class WfFlattener {
     d.rc_cap = (i32)n_rc_; d.sig_cap = (i32)n_sig_; d.vh_cap = (i32)vh_items_;
     d.rp_cap = (i32)(max_prev_ * std::max<i64>(1, n_started_) + n_dtc_);
     d.flags = m.flags;
-    d.task_cap = (i32)n_tasks_;
+    // + RefreshTasks' search-attributes task (its other tasks fit the replay's bound)
+    d.task_cap = (i32)n_tasks_ + ((m.flags & CRR_WF_FLAG_REFRESH_TASKS) ? 1 : 0);
     d.retention_days = m.retention_days;
     k_.wf.push_back(d);
   }

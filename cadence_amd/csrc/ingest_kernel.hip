@@ -776,7 +776,7 @@ __device__ __forceinline__ void decode_blob(const crr_blob_batch& in, const Plan
             ss.parent_domain_status = domain_status(in, P.dom_table, P.dom_cap, a.dom_off, a.dom_len);
             ss.attempt = a.attempt;
             ss.expiration_ns = a.expiration_ts;
-            ss.reserved = 0;
+            ss.refresh_jitter = 0;
             // prev_reset_key_off: the blob-local index of the first point until wf_pass adds the blob's
             // prefix (for an empty list too: where the next point would go, host_flatten.h)
             ss.prev_reset_key_off = n_prev;
@@ -1014,7 +1014,7 @@ __device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& 
         ss.decision_start_to_close = 0; ss.workflow_timeout = 0; ss.first_decision_backoff = 0;
         ss.initiator = CRR_INITIATOR_NIL; ss.parent_domain_status = CRR_DOMAIN_NOT_SET;
         ss.prev_reset_key_off = n_prev;   // blob-local until wf_pass adds the blob's prefix
-        ss.prev_reset_count = -1; ss.attempt = 0; ss.expiration_ns = 0; ss.reserved = 0;
+        ss.prev_reset_count = -1; ss.attempt = 0; ss.expiration_ns = 0; ss.refresh_jitter = 0;
         P.start[x] = ss;
       } else if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) {
         crr_activity_side as;
@@ -1467,7 +1467,8 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   wi[WI_COUNT * nw + w] = (i32)n; wi[WI_EMPTY_AT * nw + w] = empty_at;
   wi[WI_ACT * nw + w] = n_act; wi[WI_TIMER * nw + w] = n_timer; wi[WI_CHILD * nw + w] = n_child;
   wi[WI_RC * nw + w] = n_rc; wi[WI_SIG * nw + w] = n_sig; wi[WI_VH * nw + w] = vh; wi[WI_RP * nw + w] = rp_cap;
-  wi[WI_TASKS * nw + w] = tasks; wi[WI_STARTED * nw + w] = n_started; wi[WI_TIER * nw + w] = tier;
+  // + RefreshTasks' search-attributes task (CRR_WF_FLAG_REFRESH_TASKS: its other tasks fit the replay's bound)
+  wi[WI_TASKS * nw + w] = tasks + ((src.flags & CRR_WF_FLAG_REFRESH_TASKS) ? 1 : 0); wi[WI_STARTED * nw + w] = n_started; wi[WI_TIER * nw + w] = tier;
   wi[WI_LONG * nw + w] = is_long; wi[WI_BIG * nw + w] = big;
   // device order (flatten.interleave): lanes by (tier, -length, index), then the long tail by (big, -length, index)
   const u64 cls = is_long ? (u64)big : (u64)tier;

@@ -3033,6 +3033,117 @@ __device__ __forceinline__ int apply_event_lanes(const crr_inputs& in, const crr
   return map_op_and_after(L, G, T, op, ev, s, batch_first_id, as, K);
 }
 
+// ---- RefreshTasks' tasks (mutable_state_task_refresher.go:77-496) after a Rebuild's replay ---------------
+// getNextDecisionTimeout (mutable_state_task_generator.go:1051-1064), durations in ns, rand.Intn(jitterPortion)
+// taken as the injected draw mod jitterPortion (crr_start_side.refresh_jitter)
+__device__ __forceinline__ i64 next_decision_timeout(i64 attempt, i64 default_ns, i64 draw) {
+  if (attempt <= 1) return default_ns;
+  double next = attempt >= 5 ? 300e9 : 60e9 * (double)(1ll << (attempt - 2));  // 1m * 2^(attempt-2): exact
+  next = next < 300e9 ? next : 300e9;                                          // capped at 5m
+  i64 jp = (i64)(0.2 * next);
+  if (jp < 1) jp = 1;
+  next = next * 0.8 + (double)(i64)((u64)draw % (u64)jp);  // (1 - defaultJitterCoefficient): the constant 0.8
+  return (i64)next;
+}
+// Head of RefreshTasks, before the rows are final: the start / close / record-started / decision tasks
+// (refreshTasksForWorkflowStart, ...Close, ...RecordWorkflowStarted, ...Decision, :172-276).  Returns a
+// Go error's status (GetStartEvent / GetCompletionEvent find nothing, a bad delayed-decision initiator).
+template <class SRC>
+__device__ __forceinline__ int refresh_tasks_head(const crr_inputs& in, Lane& L, const Geo& G, const TaskSink& K,
+                                                  const SRC& src, i32 n_ev, i64 now_ns, i32 retention_days) {
+  L.n_tasks = 0;  // CloseTransactionAsSnapshot (state_rebuilder.go:181) dropped the replay's tasks
+  // GetStartEvent (mutable_state_builder.go:1131-1157): the event with ID FirstEventID, the start event
+  const i32 ss = L.start_src - L.src_base;
+  if (L.start_src < 0 || ss < 0 || ss >= n_ev) return CRR_ERR_MISSING_START_EVENT;
+  const i64 sx = src.begin + (i64)ss * src.st;
+  if (src.E.event_id[sx] != CRR_FIRST_EVENT_ID) return CRR_ERR_MISSING_START_EVENT;
+  const crr_start_side sd = in.start_side[src.E.aux[sx]];
+  const i64 sver = src.E.version[sx];
+  // GenerateWorkflowStartTasks (task_generator.go:143-166), startTime = the rebuild's now (state_rebuilder.go:186)
+  i64 vis = add_seconds(now_ns, (i64)sd.workflow_timeout + (i64)sd.first_decision_backoff);
+  if (sd.attempt > 0 && L.expiration_ns != 0 && vis > L.expiration_ns) vis = L.expiration_ns;
+  K.add(L, G, CRR_TASK_WORKFLOW_TIMEOUT, 0, sver, vis, 0, 0, L.start_src);
+  // !HasProcessedOrPendingDecision (decision_task_manager.go:750-752): GenerateDelayedDecisionTasks (:260-299)
+  if (L.decision_schedule_id == CRR_EMPTY_EVENT_ID && L.last_processed_event == CRR_EMPTY_EVENT_ID &&
+      sd.first_decision_backoff > 0) {
+    if (sd.initiator != CRR_INITIATOR_NIL && sd.initiator != CRR_INITIATOR_RETRY_POLICY && sd.initiator != CRR_INITIATOR_CRON)
+      return CRR_ERR_BAD_INITIATOR;
+    K.add(L, G, CRR_TASK_WORKFLOW_BACKOFF, sd.initiator == CRR_INITIATOR_RETRY_POLICY ? CRR_BACKOFF_RETRY : CRR_BACKOFF_CRON,
+          sver, add_seconds(src.E.timestamp[sx], sd.first_decision_backoff), 0, 0, L.start_src);
+  }
+  if (L.close_status != CRR_CLOSE_NONE) {
+    // GetCompletionEvent (mutable_state_builder.go:1085-1128): event NextEventID - 1 from the batch that
+    // starts at CompletionEventBatchID -- the last event, its batch the last one
+    if (L.state != CRR_STATE_COMPLETED || L.completion_event_batch_id == CRR_EMPTY_EVENT_ID || n_ev < 1 ||
+        L.completion_event_batch_id != L.last_first_event_id)
+      return CRR_ERR_MISSING_COMPLETION_EVENT;
+    const i64 cx = src.begin + (i64)(n_ev - 1) * src.st;
+    if (src.E.event_id[cx] != L.next_event_id - 1) return CRR_ERR_MISSING_COMPLETION_EVENT;
+    close_tasks(L, G, K, src.E.version[cx], src.E.timestamp[cx], n_ev - 1 + L.src_base, retention_days);
+  } else {  // GenerateRecordWorkflowStartedTasks (task_generator.go:301-313)
+    K.add(L, G, CRR_TASK_RECORD_WORKFLOW_STARTED, 0, sver, 0, 0, 0, L.start_src);
+  }
+  if (L.decision_schedule_id != CRR_EMPTY_EVENT_ID) {
+    if (L.decision_started_id != CRR_EMPTY_EVENT_ID) {  // GenerateDecisionStartTasks (:352-388)
+      i64 stc = (i64)((u64)L.decision_timeout * (u64)kSecond);
+      if (L.decision_attempt > 1) {  // the exponential decision timeout, written back (UpdateDecision)
+        stc = next_decision_timeout(L.decision_attempt, (i64)((u64)L.decision_start_to_close * (u64)kSecond),
+                                    sd.refresh_jitter);
+        L.decision_timeout = (i32)(stc / kSecond);
+      }
+      K.add(L, G, CRR_TASK_DECISION_TIMEOUT, CRR_TIMEOUT_START_TO_CLOSE, L.decision_version,
+            (i64)((u64)L.decision_started_ts + (u64)stc), L.decision_schedule_id, (i32)L.decision_attempt, -1);
+    } else {  // GenerateDecisionScheduleTasks (:315-350): executionInfo.TaskList, the start event's
+      K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, L.start_src);
+    }
+  }
+  return CRR_OK;
+}
+// The rest, from the final rows (slots 0..n-1 in event-ID order: Go ranges over the maps, an unspecified
+// order): each not-started activity's transfer task, the activity timer and the user timer the refresh's
+// epilogue created (the only marked activity / timer), each not-started child's, each request-cancel's and
+// signal's transfer task, the search-attributes task (:278-490)
+__device__ __forceinline__ void refresh_tasks_rows(const crr_inputs& in, Lane& L, const Geo& G, const TaskSink& K) {
+  for (i32 i = 0; i < L.n_act; ++i) {
+    const crr_activity_row* r = G.act(i);
+    if (r->started_id == CRR_EMPTY_EVENT_ID) K.add(L, G, CRR_TASK_ACTIVITY, 0, r->version, 0, r->schedule_id, 0, r->sched_src);
+  }
+  for (i32 i = 0; i < L.n_act; ++i) {  // CreateNextActivityTimer's task (timer_sequence.go:162-199)
+    const crr_activity_row* r = G.act(i);
+    const u32 tts = (u32)r->timer_task_status;
+    if (tts == 0) continue;
+    const i32 y = (tts & CRR_TTS_CREATED_START_TO_CLOSE) ? CRR_TIMEOUT_START_TO_CLOSE
+                : (tts & CRR_TTS_CREATED_SCHEDULE_TO_START) ? CRR_TIMEOUT_SCHEDULE_TO_START
+                : (tts & CRR_TTS_CREATED_SCHEDULE_TO_CLOSE) ? CRR_TIMEOUT_SCHEDULE_TO_CLOSE : CRR_TIMEOUT_HEARTBEAT;
+    const i64 t = y == CRR_TIMEOUT_SCHEDULE_TO_CLOSE ? add_seconds(r->scheduled_time, r->schedule_to_close)
+                : y == CRR_TIMEOUT_SCHEDULE_TO_START ? add_seconds(r->scheduled_time, r->schedule_to_start)
+                : y == CRR_TIMEOUT_START_TO_CLOSE ? add_seconds(r->started_time, r->start_to_close)
+                : add_seconds(max(r->started_time, r->last_heartbeat_time), r->heartbeat);
+    K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, t, r->schedule_id, r->attempt, -1);
+    break;
+  }
+  for (i32 i = 0; i < L.n_timer; ++i) {  // CreateNextUserTimer's task (:127-160)
+    const crr_timer_row* r = G.timer(i);
+    if (r->task_status != CRR_TIMER_TASK_STATUS_CREATED) continue;
+    K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, r->expiry_time, r->started_id, 0, -1);
+    break;
+  }
+  for (i32 i = 0; i < L.n_child; ++i) {  // GenerateChildWorkflowTasks (task_generator.go:449-495)
+    const crr_child_row* r = G.child(i);
+    if (r->started_id == CRR_EMPTY_EVENT_ID) K.add(L, G, CRR_TASK_START_CHILD, 0, r->version, 0, r->initiated_id, 0, r->src);
+  }
+  for (i32 i = 0; i < L.n_rc; ++i) {  // GenerateRequestCancelExternalTasks (:497-546)
+    const crr_initiated_row* r = G.rc(i);
+    K.add(L, G, CRR_TASK_CANCEL_EXECUTION, 0, r->version, 0, r->initiated_id, 0, r->src);
+  }
+  for (i32 i = 0; i < L.n_sig; ++i) {  // GenerateSignalExternalTasks (:548-597)
+    const crr_initiated_row* r = G.sig(i);
+    K.add(L, G, CRR_TASK_SIGNAL_EXECUTION, 0, r->version, 0, r->initiated_id, 0, r->src);
+  }
+  if (in.flags & CRR_IN_ADVANCED_VISIBILITY)  // refreshTasksForWorkflowSearchAttr (:484-490)
+    K.add(L, G, CRR_TASK_UPSERT_SEARCH_ATTRIBUTES, 0, L.current_version, 0, 0, 0, -1);
+}
+
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
 // the replay loop of a launch that does not ask for tasks carries none of its registers.
 // CRC (compile time): the checksum computed here (every product launch sets it).
@@ -3070,6 +3181,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   TokenDesc tok{0, 0, 0, 0};  // read after the loop (failed workflows have no checksum: left zero)
 #define FAIL(code, step) do { L.status = (code); L.fail_step = (step) + L.src_base; goto done_events; } while (0)
 #define CHECK(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, s); } while (0)
+#define CHECK_N(expr) do { int rc_ = (expr); if (rc_) FAIL(rc_, n_ev); } while (0)
 
   // step 0's columns in flight first: a loaded state's exec row and rows (below) are read meanwhile
   src.start();
@@ -3447,13 +3559,17 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       if (want_id < 0 || (want_ver < 0 && want_ver != CRR_EMPTY_VERSION)) FAIL(CRR_ERR_VH_INVALID_ITEM, n_ev);
       if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
     }
-    if (wf_flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:183)
-      T.refresh(L, G);
-      L.n_tasks = 0;  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
+    if (wf_flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:181-186)
+      T.refresh(L, G);  // the state effects (the timers re-created: a task each, emitted from the rows below)
+      L.n_tasks = 0;    // CloseTransactionAsSnapshot drops the replay's tasks
+      if constexpr (EMIT) {
+        if (K.on) CHECK_N(refresh_tasks_head(in, L, G, K, src, n_ev, now_ns, retention_days));
+      }
     }
   }
 done_events:
 #undef CHECK
+#undef CHECK_N
 #undef FAIL
   if (!task_read && last_task_step >= 0) L.last_event_task_id = src.task_id(last_task_step);
 
@@ -3465,7 +3581,7 @@ done_events:
     return;
   }
   // the checksum's branch-token words go out before the row write-back, whose work hides their latency
-  const bool want_crc = L.status == CRR_OK;
+  bool want_crc = L.status == CRR_OK;
   TokenWords TW;
   TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
   // the wave path's items were written by the lanes of their events; the checksum reads them all
@@ -3476,6 +3592,17 @@ done_events:
     it->version = L.vh_last_ver;
   }
   T.finalize(L, G);
+  if constexpr (EMIT) {  // RefreshTasks' tasks from the final rows
+    if (K.on && want_crc && (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS)) {
+      if constexpr (std::is_same<SRC, WaveSource>::value) wave_sync_global();
+      refresh_tasks_rows(in, L, G, K);
+      if (L.n_tasks > G.task_cap) {
+        L.status = CRR_ERR_CAPACITY;
+        L.fail_step = n_ev + L.src_base;
+        want_crc = false;
+      }
+    }
+  }
 
   crr_exec_row R;
   R.status = L.status;

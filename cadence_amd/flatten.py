@@ -45,6 +45,8 @@ class HistoryBatch:
     wave_begin: Optional[int] = None
     # write the transfer / timer tasks ApplyEvents generates (CRR_IN_EMIT_TASKS)
     emit_tasks: bool = False
+    # config.AdvancedVisibilityWritingMode != off: RefreshTasks' search-attributes task (CRR_IN_ADVANCED_VISIBILITY)
+    advanced_visibility: bool = False
     # CRR_IN_TIERED: (large_begin, compact_begin, compact2_begin, wide_begin, hbm_begin, big_begin) --
     # lane workflows ordered by expected live-set size (TIER_SLOTS, then HBM rows); long-tail workflows
     # no fast per-wave arena is expected to hold from big_begin on
@@ -66,7 +68,8 @@ class HistoryBatch:
     def c_flags(self) -> int:
         resume = self.tiers is not None and self.n_wf and bool((self.wf["flags"] & abi.WF_FLAG_RESUME).any())
         return ((abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
-                | (abi.IN_TIERED if self.tiers is not None else 0) | (abi.IN_HAS_RESUME if resume else 0))
+                | (abi.IN_TIERED if self.tiers is not None else 0) | (abi.IN_HAS_RESUME if resume else 0)
+                | (abi.IN_ADVANCED_VISIBILITY if self.advanced_visibility else 0))
 
     @property
     def n_wf(self) -> int:
@@ -258,7 +261,7 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
                     start_side.append((a("task_start_to_close_timeout_seconds", 0), a("execution_start_to_close_timeout_seconds", 0),
                                        a("first_decision_task_backoff_seconds", 0),
                                        abi.INITIATOR_NIL if init is None else int(init), pstat, prev_off, prev_cnt,
-                                       a("attempt", 0), a("expiration_timestamp", 0), 0))
+                                       a("attempt", 0), a("expiration_timestamp", 0), h.refresh_jitter))
                     aux = len(start_side) - 1
                 elif t == ET.DecisionTaskScheduled:
                     ref = a("attempt", 0)
@@ -354,7 +357,8 @@ def flatten(histories: Sequence[WorkflowHistory], known_domains=None,
         caps["rc_cap"][w] = n_rc
         caps["sig_cap"][w] = n_sig
         caps["vh_cap"][w] = vh_items
-        caps["task_cap"][w] = n_tasks
+        # + RefreshTasks' search-attributes task (its other tasks fit the replay's bound)
+        caps["task_cap"][w] = n_tasks + (1 if h.refresh_tasks else 0)
         r["retention_days"] = h.retention_days
         caps["rp_cap"][w] = max_prev * max(1, sum(1 for e in h.events if e.event_type == ET.WorkflowExecutionStarted)) + n_dtc
     if loaded is not None:   # the loaded rows plus this call's inserts
@@ -528,7 +532,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
                        wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks,
-                       tiers=tiers, init=batch.init.permuted(perm) if batch.init is not None else None,
+                       advanced_visibility=batch.advanced_visibility, tiers=tiers, init=batch.init.permuted(perm) if batch.init is not None else None,
                        key_dict=kd, interners=[batch.interners[i] for i in perm] if batch.interners else None)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)

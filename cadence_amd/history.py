@@ -51,6 +51,7 @@ class WorkflowHistory:
     rebuild_last_event_version: int = 0
     is_new_run: bool = False                  # CAN newRunHistory replayed by the outer workflow
     refresh_tasks: bool = False               # Rebuild: RefreshTasks after the replay (state_rebuilder.go:183)
+    refresh_jitter: int = 0                   # injected rand draw for RefreshTasks' decision backoff jitter
     retention_days: int = 1                   # domain retention (defaultWorkflowRetentionInDays = 1 when unknown)
 
     @property

@@ -161,6 +161,8 @@ enum crr_status_code {
     CRR_ERR_TIMER_SEQUENCE = 14,          /* InternalService  timer_sequence.go:141-145,176-180    */
     CRR_ERR_REBUILD_LAST_ITEM = 15,       /* BadRequest       state_rebuilder.go:160-176           */
     CRR_ERR_NEW_RUN_MISSING = 16,         /* engine: CAN new-run workflow index out of range       */
+    CRR_ERR_MISSING_START_EVENT = 17,     /* ErrMissingWorkflowStartEvent mutable_state_builder.go:1150-1155 (RefreshTasks) */
+    CRR_ERR_MISSING_COMPLETION_EVENT = 18,/* ErrMissingWorkflowCompletionEvent :1085-1128 (RefreshTasks)      */
     /* NDC branch decisions (crr_ndc_prepare) */
     CRR_ERR_NDC_NO_LCA = 20,              /* BadRequest       versionHistory.go:270-272 "No joint point found" */
     CRR_ERR_NDC_LCA_NOT_IN_BRANCH = 21,   /* BadRequest       versionHistory.go:147-149 DuplicateUntilLCAItem  */
@@ -222,7 +224,9 @@ typedef struct crr_start_side {
     int32_t prev_reset_count;          /* -1 == PrevAutoResetPoints nil (or Points nil) */
     int32_t attempt;                   /* GetAttempt() (GenerateWorkflowStartTasks, task_generator.go:156) */
     int64_t expiration_ns;             /* GetExpirationTimestamp() (0: unset; mutable_state_builder.go:1800-1802) */
-    int64_t reserved;
+    int64_t refresh_jitter;            /* injected rand draw (>= 0) for RefreshTasks' decision backoff jitter:
+                                          getNextDecisionTimeout's rand.Intn(jitterPortion) is taken as
+                                          refresh_jitter % jitterPortion (task_generator.go:1051-1064) */
 } crr_start_side;
 
 /* Per-workflow descriptor (168 B). */
@@ -249,9 +253,22 @@ typedef struct crr_workflow {
 } crr_workflow;
 
 #define CRR_WF_FLAG_NEW_RUN 1
-/* After the replay (and the rebuild last-item check), apply Rebuild's RefreshTasks state effects
- * (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): clear every pending activity's
- * TimerTaskStatus and user timer's TaskStatus, then CreateNextActivityTimer / CreateNextUserTimer. */
+/* After the replay (and the rebuild last-item check), Rebuild's RefreshTasks (state_rebuilder.go:183-186
+ * -> mutable_state_task_refresher.go:77-496).  State effects: every pending activity's TimerTaskStatus and
+ * user timer's TaskStatus cleared, then CreateNextActivityTimer / CreateNextUserTimer; a started decision
+ * with Attempt > 1 gets getNextDecisionTimeout's DecisionTimeout (the jitter injected as
+ * crr_start_side.refresh_jitter).  With CRR_IN_EMIT_TASKS the replay's own tasks are dropped
+ * (CloseTransactionAsSnapshot) and the task rows hold RefreshTasks' tasks, in its order:
+ *   workflow timeout (startTime = now_ns) [+ delayed decision], close tasks or record-started, the
+ *   decision's schedule / start task, each pending not-started activity's transfer task, the activity
+ *   timer, the user timer, each pending not-started child's, request-cancel's and signal's transfer task,
+ *   the search-attributes task (CRR_IN_ADVANCED_VISIBILITY).
+ * Go ranges over maps for the activity / child / request-cancel / signal groups (an unspecified order);
+ * here each group is in ascending event ID.  The start event is the event with ID 1 of this call's
+ * history (GetStartEvent), the close event the one with ID NextEventID - 1 in the completion batch
+ * (GetCompletionEvent, read from the store); a missing one fails the call (CRR_ERR_MISSING_*_EVENT at
+ * fail_step = ev_count).  The decision schedule-to-start timer follows the default dynamic config
+ * (NormalDecisionScheduleToStartMaxAttempts = 0: none). */
 #define CRR_WF_FLAG_REFRESH_TASKS 2
 /* ApplyEvents onto a LOADED mutable state (NewStateBuilder(shard, logger, mutableState, ...) with the
  * state mutableStateBuilder.Load (mutable_state_builder.go:306-349) built from persistence; the passive
@@ -311,6 +328,8 @@ typedef struct crr_inputs {
                                    size (large_begin / wide_begin); each segment is launched with the
                                    LDS tier that holds it (1, 2 or 8 entries per map).  A hint like
                                    CRR_IN_LDS_SMALL (which it overrides): speed only, never results */
+#define CRR_IN_ADVANCED_VISIBILITY 64u /* config.AdvancedVisibilityWritingMode != off: RefreshTasks also emits
+                                   the search-attributes task (mutable_state_task_refresher.go:160-167) */
 #define CRR_IN_HAS_RESUME 32u   /* some workflow carries CRR_WF_FLAG_RESUME (CRR_IN_TIERED batches): the
                                    compact tiers continue loaded states in their LDS arenas, and the 1- and
                                    2-slot segments [0, compact_begin) join compact tier 1 (which holds

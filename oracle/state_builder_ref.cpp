@@ -555,6 +555,123 @@ Err CreateNextUserTimer(MutableState& ms) {
   return Err{};
 }
 
+// GenerateWorkflowCloseTasks (task_generator.go:168-258): close transfer task + DeleteHistoryEventTask
+void GenerateWorkflowCloseTasks(MutableState& ms, const WfView& v, int s) {
+  ms.AddTask(CRR_TASK_CLOSE_EXECUTION, 0, v.version(s), 0, 0, 0, s);
+  ms.AddTask(CRR_TASK_DELETE_HISTORY, 0, v.version(s), wadd(v.ts(s), wmul((i64)v.wf->retention_days * 86400, kSecond)),
+             0, 0, s);
+}
+
+// ---- RefreshTasks (mutable_state_task_refresher.go) --------------------------------------------------
+// getNextDecisionTimeout (mutable_state_task_generator.go:1051-1064) with rand.Intn(jitterPortion) taken as
+// the injected draw mod jitterPortion (crr_start_side.refresh_jitter); durations in ns
+i64 NextDecisionTimeout(i64 attempt, i64 default_ns, i64 draw) {
+  if (attempt <= 1) return default_ns;
+  // float64(defaultInitIntervalForDecisionRetry = 1m) * math.Pow(2, attempt-2), capped at 5m: exact doubles
+  double next = attempt >= 5 ? 300e9 : 60e9 * (double)(1ll << (attempt - 2));
+  next = next < 300e9 ? next : 300e9;                    // math.Min
+  i64 jp = (i64)(0.2 * next);                            // int(defaultJitterCoefficient * nextInterval)
+  if (jp < 1) jp = 1;
+  next = next * 0.8 + (double)(i64)((uint64_t)draw % (uint64_t)jp);   // (1 - 0.2) is the exact constant 0.8
+  return (i64)next;                                      // time.Duration(nextInterval)
+}
+
+// Each pending map in ascending event ID (Go ranges over the maps: an unspecified order).
+template <class M>
+std::vector<i64> sorted_keys(const M& m) {
+  std::vector<i64> k;
+  k.reserve(m.size());
+  for (const auto& kv : m) k.push_back(kv.first);
+  std::sort(k.begin(), k.end());
+  return k;
+}
+
+// RefreshTasks (:77-170) on the rebuilt state; startTime = the rebuild's now (state_rebuilder.go:186)
+Err RefreshTasks(const WfView& v, MutableState& ms, int n) {
+  ExecutionInfo& x = ms.exec;
+  // refreshTasksForWorkflowStart (:172-202): GetStartEvent reads the event with ID FirstEventID
+  // (mutable_state_builder.go:1131-1157) -- here the start event this replay applied
+  const int ss = x.start_src;
+  if (ss < v.sb || ss >= n || v.id(ss) != CRR_FIRST_EVENT_ID) return mk(CRR_ERR_MISSING_START_EVENT);
+  const crr_start_side& sd = v.in->start_side[v.aux(ss)];
+  const i64 sver = v.version(ss);
+  {  // GenerateWorkflowStartTasks (task_generator.go:143-166)
+    i64 vis = wadd(v.wf->now_ns, wmul(wadd(sd.workflow_timeout, sd.first_decision_backoff), kSecond));
+    if (sd.attempt > 0 && ms.expiration_ns != 0 && vis > ms.expiration_ns) vis = ms.expiration_ns;
+    ms.AddTask(CRR_TASK_WORKFLOW_TIMEOUT, 0, sver, vis, 0, 0, ss);
+  }
+  // !HasProcessedOrPendingDecision (decision_task_manager.go:750-752) && backoff > 0
+  const bool processed_or_pending = ms.HasPendingDecision() || x.last_processed_event != CRR_EMPTY_EVENT_ID;
+  if (!processed_or_pending && sd.first_decision_backoff > 0) {  // GenerateDelayedDecisionTasks (:260-299)
+    if (sd.initiator != CRR_INITIATOR_NIL && sd.initiator != CRR_INITIATOR_RETRY_POLICY && sd.initiator != CRR_INITIATOR_CRON)
+      return mk(CRR_ERR_BAD_INITIATOR);
+    ms.AddTask(CRR_TASK_WORKFLOW_BACKOFF, sd.initiator == CRR_INITIATOR_RETRY_POLICY ? CRR_BACKOFF_RETRY : CRR_BACKOFF_CRON,
+               sver, wadd(v.ts(ss), wmul(sd.first_decision_backoff, kSecond)), 0, 0, ss);
+  }
+  // refreshTasksForWorkflowClose (:204-222): GetCompletionEvent (mutable_state_builder.go:1085-1128), the
+  // event NextEventID - 1 read from the batch that starts at CompletionEventBatchID
+  if (x.close_status != CRR_CLOSE_NONE) {
+    if (x.state != CRR_STATE_COMPLETED || x.completion_event_batch_id == CRR_EMPTY_EVENT_ID)
+      return mk(CRR_ERR_MISSING_COMPLETION_EVENT);
+    int cs = -1;
+    for (int k = n - 1; k >= v.sb && cs < 0; --k)
+      if (v.id(k) == x.next_event_id - 1) cs = k;
+    if (cs < 0) return mk(CRR_ERR_MISSING_COMPLETION_EVENT);
+    int bf = cs;  // the first event of its batch
+    while (bf > v.sb && !v.first(bf)) --bf;
+    if (v.id(bf) != x.completion_event_batch_id) return mk(CRR_ERR_MISSING_COMPLETION_EVENT);
+    GenerateWorkflowCloseTasks(ms, v, cs);
+  } else {  // refreshTasksForRecordWorkflowStarted (:224-244)
+    ms.AddTask(CRR_TASK_RECORD_WORKFLOW_STARTED, 0, sver, 0, 0, 0, ss);
+  }
+  // refreshTasksForDecision (:246-276)
+  if (ms.HasPendingDecision()) {
+    if (x.decision_started_id != CRR_EMPTY_EVENT_ID) {  // GenerateDecisionStartTasks (task_generator.go:352-388)
+      i64 stc = wmul(x.decision_timeout, kSecond);
+      if (x.decision_attempt > 1) {
+        stc = NextDecisionTimeout(x.decision_attempt, wmul(x.decision_start_to_close_timeout, kSecond), sd.refresh_jitter);
+        x.decision_timeout = (i32)(stc / kSecond);  // int32(startToCloseTimeout.Seconds()); UpdateDecision
+      }
+      ms.AddTask(CRR_TASK_DECISION_TIMEOUT, CRR_TIMEOUT_START_TO_CLOSE, x.decision_version,
+                 wadd(x.decision_started_ts, stc), x.decision_schedule_id, (int)x.decision_attempt, -1);
+    } else {  // GenerateDecisionScheduleTasks (:315-350): executionInfo.TaskList (the start event's)
+      ms.AddTask(CRR_TASK_DECISION, 0, x.decision_version, 0, x.decision_schedule_id, 0, ss);
+    }
+  }
+  // refreshTasksForActivity (:278-336): TimerTaskStatus cleared; not-started activities' transfer tasks
+  for (i64 id : sorted_keys(ms.pendingActivityInfoIDs)) {
+    ActivityInfo& ai = ms.pendingActivityInfoIDs[id];
+    ai.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
+    if (ai.started_id == CRR_EMPTY_EVENT_ID)  // GenerateActivityTransferTasks (:390-427)
+      ms.AddTask(CRR_TASK_ACTIVITY, 0, ai.version, 0, ai.schedule_id, 0, ai.sched_src);
+  }
+  Err er = CreateNextActivityTimer(ms);
+  if (!er.ok()) return er;
+  // refreshTasksForTimer (:338-365)
+  for (auto& kv : ms.pendingTimerInfoIDs) kv.second.task_status = CRR_TIMER_TASK_STATUS_NONE;
+  er = CreateNextUserTimer(ms);
+  if (!er.ok()) return er;
+  // refreshTasksForChildWorkflow (:367-406): GenerateChildWorkflowTasks (task_generator.go:449-495)
+  for (i64 id : sorted_keys(ms.pendingChildExecutionInfoIDs)) {
+    const ChildExecutionInfo& ci = ms.pendingChildExecutionInfoIDs[id];
+    if (ci.started_id == CRR_EMPTY_EVENT_ID) ms.AddTask(CRR_TASK_START_CHILD, 0, ci.version, 0, ci.initiated_id, 0, ci.src);
+  }
+  // refreshTasksForRequestCancelExternalWorkflow / SignalExternalWorkflow (:408-482): the initiated
+  // event's version and ID (task_generator.go:497-597)
+  for (i64 id : sorted_keys(ms.pendingRequestCancelInfoIDs)) {
+    const InitiatedInfo& ri = ms.pendingRequestCancelInfoIDs[id];
+    ms.AddTask(CRR_TASK_CANCEL_EXECUTION, 0, ri.version, 0, ri.initiated_id, 0, ri.src);
+  }
+  for (i64 id : sorted_keys(ms.pendingSignalInfoIDs)) {
+    const InitiatedInfo& si = ms.pendingSignalInfoIDs[id];
+    ms.AddTask(CRR_TASK_SIGNAL_EXECUTION, 0, si.version, 0, si.initiated_id, 0, si.src);
+  }
+  // refreshTasksForWorkflowSearchAttr (:484-490), AdvancedVisibilityWritingMode != off
+  if (v.in->flags & CRR_IN_ADVANCED_VISIBILITY)
+    ms.AddTask(CRR_TASK_UPSERT_SEARCH_ATTRIBUTES, 0, ms.currentVersion, 0, 0, 0, -1);
+  return Err{};
+}
+
 // ---- the replay driver ----------------------------------------------------------------------------
 struct Outcome {
   int status = CRR_OK;
@@ -606,29 +723,18 @@ class Replayer {
         return out;
       }
     }
-    // Rebuild's RefreshTasks (state_rebuilder.go:183 -> mutable_state_task_refresher.go:278-365): every
-    // pending activity's TimerTaskStatus and user timer's TaskStatus cleared, then one
-    // CreateNextActivityTimer / CreateNextUserTimer (LastHeartbeatTimeoutVisibilityInSeconds is kept)
+    // Rebuild: CloseTransactionAsSnapshot drops the replay's tasks, then RefreshTasks
+    // (state_rebuilder.go:181-186 -> mutable_state_task_refresher.go:77-496)
     if (wf->flags & CRR_WF_FLAG_REFRESH_TASKS) {
-      ms.emit_tasks = false;
-      for (auto& kv : ms.pendingActivityInfoIDs) kv.second.timer_task_status = CRR_TIMER_TASK_STATUS_NONE;
-      Err er = CreateNextActivityTimer(ms);
+      ms.tasks.clear();
+      Err er = RefreshTasks(v, ms, n);
       if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
-      for (auto& kv : ms.pendingTimerInfoIDs) kv.second.task_status = CRR_TIMER_TASK_STATUS_NONE;
-      er = CreateNextUserTimer(ms);
-      if (!er.ok()) { out.status = er.code; out.fail_step = n; return out; }
-      ms.tasks.clear();  // CloseTransactionAsSnapshot drops the replay's tasks; RefreshTasks' own are not emitted
     }
     return out;
   }
 
  private:
-  // GenerateWorkflowCloseTasks (task_generator.go:168-258): close transfer task + DeleteHistoryEventTask
-  static void CloseTasks(MutableState& ms, const WfView& v, int s) {
-    ms.AddTask(CRR_TASK_CLOSE_EXECUTION, 0, v.version(s), 0, 0, 0, s);
-    ms.AddTask(CRR_TASK_DELETE_HISTORY, 0, v.version(s), wadd(v.ts(s), wmul((i64)v.wf->retention_days * 86400, kSecond)),
-               0, 0, s);
-  }
+  static void CloseTasks(MutableState& ms, const WfView& v, int s) { GenerateWorkflowCloseTasks(ms, v, s); }
 
   // stateBuilderImpl.ApplyEvents (state_builder.go:90-648) for history = steps [b, e)
   Outcome ApplyEvents(const WfView& v, MutableState& ms, int b, int e) {

@@ -151,10 +151,19 @@ def test_rebuild_refresh_tasks_all_paths(engine):
                synth_mixed.long_tail_histories(60, 42, max_len=3000, run_cap=1500, multi_version=True)):
         for h in hs:
             h.refresh_tasks = rng.random() < 0.5
+            h.refresh_jitter = rng.randrange(1 << 40)
         b = flatten(hs, known_domains=KNOWN)
         check(engine, interleave(b))
         check(engine, interleave(b, long_threshold=None))
         check(engine, b)
+        # with task emission: RefreshTasks' own tasks (mutable_state_task_refresher.go:77-496) in the rows,
+        # search-attributes task on (CRR_IN_ADVANCED_VISIBILITY)
+        b.emit_tasks = True
+        b.advanced_visibility = True
+        for lb in (interleave(b), interleave(b, long_threshold=None), b):
+            lb.emit_tasks = True
+            lb.advanced_visibility = True
+            check(engine, lb)
 
 
 def test_decoded_blobs_replay_on_device(engine):

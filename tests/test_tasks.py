@@ -99,11 +99,104 @@ def test_failure_keeps_tasks_generated_before_it():  # no rollback (state_builde
     assert [x[0] for x in t] == [K.RecordWorkflowStarted, K.WorkflowTimeout, K.Decision]
 
 
-def test_rebuild_drops_replay_tasks():  # CloseTransactionAsSnapshot clears them (state_rebuilder.go:178-181)
-    h = WorkflowHistory(batches=[[ev(ET.WorkflowExecutionStarted, 1), ev(ET.DecisionTaskScheduled, 2)]],
-                        refresh_tasks=True)
-    ex, t = tasks_of(h)
-    assert ex["status"] == 0 and t == []
+# ---- Rebuild's RefreshTasks (state_rebuilder.go:181-186 -> mutable_state_task_refresher.go:77-496): the
+# replay's tasks are dropped (CloseTransactionAsSnapshot) and RefreshTasks' own are the task rows ----
+REB_NOW = NOW + 10_000 * SEC       # the rebuild's now: RefreshTasks' startTime
+
+
+def refresh_of(batches, adv=False, **kw):
+    h = WorkflowHistory(batches=batches, refresh_tasks=True, now_ns=REB_NOW, retention_days=3, **kw)
+    b = flatten([h], known_domains=KNOWN)
+    b.emit_tasks = True
+    b.advanced_visibility = adv
+    r = oracle.replay(b, 1)
+    rows = r.live_rows(b, 0)["tasks"]
+    return r, [(K(int(x["kind"])), int(x["aux"]), int(x["version"]), int(x["visibility_ts"]),
+                int(x["event_id"]), int(x["attempt"]), int(x["src"])) for x in rows]
+
+
+def _start(i=1, **a):
+    return ev(ET.WorkflowExecutionStarted, i, execution_start_to_close_timeout_seconds=3600,
+              task_start_to_close_timeout_seconds=10, **a)
+
+
+def test_refresh_scheduled_decision():
+    # refreshTasksForWorkflowStart (:172-202): WorkflowTimeout from startTime = now; RecordWorkflowStarted
+    # (:224-244, not closed); refreshTasksForDecision (:246-276): only scheduled -> GenerateDecisionScheduleTasks
+    r, t = refresh_of([[_start(), ev(ET.DecisionTaskScheduled, 2, start_to_close_timeout_seconds=10)]])
+    assert r.exec["status"][0] == 0
+    assert t == [(K.WorkflowTimeout, 0, 12, REB_NOW + 3600 * SEC, 0, 0, 0),
+                 (K.RecordWorkflowStarted, 0, 12, 0, 0, 0, 0),
+                 (K.Decision, 0, 12, 0, 2, 0, 0)]
+
+
+def test_refresh_started_decision_and_activities():
+    # decision started -> GenerateDecisionStartTasks (task_generator.go:352-388); refreshTasksForActivity
+    # (:278-336): a transfer task per not-started activity, then CreateNextActivityTimer; refreshTasksForTimer
+    # (:338-365): CreateNextUserTimer; children not started, request-cancels, signals (:367-482)
+    r, t = refresh_of([
+        [_start(), ev(ET.DecisionTaskScheduled, 2, start_to_close_timeout_seconds=10)],
+        [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+        [ev(ET.DecisionTaskCompleted, 4, started_event_id=3),
+         ev(ET.ActivityTaskScheduled, 5, activity_id="a", schedule_to_start_timeout_seconds=30,
+            schedule_to_close_timeout_seconds=60, start_to_close_timeout_seconds=20),
+         ev(ET.ActivityTaskScheduled, 6, activity_id="b", schedule_to_start_timeout_seconds=40,
+            schedule_to_close_timeout_seconds=90, start_to_close_timeout_seconds=20),
+         ev(ET.TimerStarted, 7, timer_id="t1", start_to_fire_timeout_seconds=500),
+         ev(ET.TimerStarted, 8, timer_id="t2", start_to_fire_timeout_seconds=5),
+         ev(ET.StartChildWorkflowExecutionInitiated, 9, domain="domain-a"),
+         ev(ET.StartChildWorkflowExecutionInitiated, 10, domain="domain-b"),
+         ev(ET.RequestCancelExternalWorkflowExecutionInitiated, 11, domain="domain-a"),
+         ev(ET.SignalExternalWorkflowExecutionInitiated, 12, domain="domain-b"),
+         ev(ET.DecisionTaskScheduled, 13, start_to_close_timeout_seconds=15)],
+        [ev(ET.ActivityTaskStarted, 14, scheduled_event_id=5), ev(ET.ChildWorkflowExecutionStarted, 15,
+                                                                  initiated_event_id=9),
+         ev(ET.DecisionTaskStarted, 16, scheduled_event_id=13)]], adv=True)
+    assert r.exec["status"][0] == 0
+    ts = lambda i: NOW + i * SEC  # noqa: E731
+    assert t == [
+        (K.WorkflowTimeout, 0, 12, REB_NOW + 3600 * SEC, 0, 0, 0),
+        (K.RecordWorkflowStarted, 0, 12, 0, 0, 0, 0),
+        (K.DecisionTimeout, abi.TimeoutType.StartToClose, 12, ts(16) + 15 * SEC, 13, 0, -1),
+        (K.Activity, 0, 12, 0, 6, 0, 5),                     # activity 5 is started: no transfer task
+        # the earliest activity timer after the masks are cleared: 5's StartToClose (14 + 20 s) vs 6's
+        # ScheduleToStart (6 + 40 s = 46 s) -> 34 s
+        (K.ActivityTimeout, abi.TimeoutType.StartToClose, 12, ts(14) + 20 * SEC, 5, 0, -1),
+        (K.UserTimer, 0, 12, ts(8) + 5 * SEC, 8, 0, -1),     # t2 fires first
+        (K.StartChild, 0, 12, 0, 10, 0, 9),                  # child 9 is started
+        (K.CancelExecution, 0, 12, 0, 11, 0, 10),
+        (K.SignalExecution, 0, 12, 0, 12, 0, 11),
+        (K.UpsertSearchAttributes, 0, 12, 0, 0, 0, -1)]      # AdvancedVisibilityWritingMode on (:160-167)
+
+
+def test_refresh_closed_workflow_and_delayed_decision():
+    # closed: GenerateWorkflowCloseTasks from the completion event (:204-222), no RecordWorkflowStarted
+    r, t = refresh_of([[_start(), ev(ET.DecisionTaskScheduled, 2)], [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+                       [ev(ET.DecisionTaskCompleted, 4, started_event_id=3), ev(ET.WorkflowExecutionCompleted, 5)]])
+    assert r.exec["status"][0] == 0
+    assert t == [(K.WorkflowTimeout, 0, 12, REB_NOW + 3600 * SEC, 0, 0, 0),
+                 (K.CloseExecution, 0, 12, 0, 0, 0, 4),
+                 (K.DeleteHistory, 0, 12, NOW + 5 * SEC + 3 * 86400 * SEC, 0, 0, 4)]
+    # no decision processed or pending and a first-decision backoff: GenerateDelayedDecisionTasks
+    r, t = refresh_of([[_start(first_decision_task_backoff_seconds=30, initiator=abi.INITIATOR_CRON)]])
+    assert r.exec["status"][0] == 0
+    assert t == [(K.WorkflowTimeout, 0, 12, REB_NOW + (3600 + 30) * SEC, 0, 0, 0),
+                 (K.WorkflowBackoff, abi.BACKOFF_CRON, 12, NOW + SEC + 30 * SEC, 0, 0, 0),
+                 (K.RecordWorkflowStarted, 0, 12, 0, 0, 0, 0)]
+    r, t = refresh_of([[_start(first_decision_task_backoff_seconds=30, initiator=abi.INITIATOR_DECIDER)]])
+    assert r.exec["status"][0] == abi.Status.BAD_INITIATOR
+
+
+def test_refresh_missing_start_or_completion_event():
+    # GetStartEvent (mutable_state_builder.go:1131-1157): no event with ID 1 to read
+    r, _t = refresh_of([[ev(ET.DecisionTaskScheduled, 2)]])
+    assert r.exec["status"][0] == abi.Status.MISSING_START_EVENT
+    # GetCompletionEvent (:1085-1128) reads event NextEventID - 1 from the completion batch: a signal in a
+    # later batch is not in it
+    r, _t = refresh_of([[_start(), ev(ET.DecisionTaskScheduled, 2)], [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+                        [ev(ET.DecisionTaskCompleted, 4, started_event_id=3), ev(ET.WorkflowExecutionCompleted, 5)],
+                        [ev(ET.WorkflowExecutionSignaled, 6)]])
+    assert r.exec["status"][0] == abi.Status.MISSING_COMPLETION_EVENT
 
 
 def _mixed():

@@ -1353,84 +1353,106 @@ struct CompactTables {
       bool ok = L.n_act <= A_SLOTS && L.n_timer <= T_SLOTS && L.n_child <= C_SLOTS && L.n_rc <= R_SLOTS &&
                 L.n_sig <= S_SLOTS && L.n_rp <= P_SLOTS && vk > 0;
       if (ok) {
+        // The loaded rows' reads: the first slots of every table without a branch (a slot past the loaded
+        // ones reads a dummy -- the batch's first descriptor, one uniform line), so they are all in flight
+        // together (one round trip for the common loaded states); the rest slot by slot.
+        const void* dummy = in->wf;
+        auto act_at = [&](int j) { return j < L.n_act ? G.act(j) : reinterpret_cast<const crr_activity_row*>(dummy); };
+        auto timer_at = [&](int j) { return j < L.n_timer ? G.timer(j) : reinterpret_cast<const crr_timer_row*>(dummy); };
+        auto child_at = [&](int j) { return j < L.n_child ? G.child(j) : reinterpret_cast<const crr_child_row*>(dummy); };
+        auto rc_at = [&](int j) { return j < L.n_rc ? G.rc(j) : reinterpret_cast<const crr_initiated_row*>(dummy); };
+        auto sig_at = [&](int j) { return j < L.n_sig ? G.sig(j) : reinterpret_cast<const crr_initiated_row*>(dummy); };
+        auto rp_at = [&](int j) { return j < L.n_rp ? G.rp(j) : reinterpret_cast<const crr_reset_point_row*>(dummy); };
+        constexpr int FA = A_SLOTS < 2 ? A_SLOTS : 2, FP = P_SLOTS < 2 ? P_SLOTS : 2;
+        crr_activity_row ra[FA];
+        crr_timer_row rt0 = *timer_at(0);
+        crr_child_row rc0 = *child_at(0);
+        const i64 rq0 = rc_at(0)->initiated_id, rs0 = sig_at(0)->initiated_id;
+        u32 rpk[FP];
+#pragma unroll
+        for (int j = 0; j < FA; ++j) ra[j] = *act_at(j);
+#pragma unroll
+        for (int j = 0; j < FP; ++j) rpk[j] = rp_at(j)->key;
+        // every read above is issued before any is used: pinned here, the compiler can neither sink a read
+        // into its use's branch nor split a row into dependent reads
+#pragma unroll
+        for (int j = 0; j < FA; ++j) {
+          asm volatile("" ::"v"(ra[j].schedule_id), "v"(ra[j].scheduled_time), "v"(ra[j].started_id),
+                       "v"(ra[j].started_time), "v"(ra[j].last_heartbeat_time));
+          asm volatile("" ::"v"(ra[j].schedule_to_start), "v"(ra[j].schedule_to_close), "v"(ra[j].start_to_close),
+                       "v"(ra[j].heartbeat), "v"(ra[j].timer_task_status), "v"(ra[j].key), "v"(ra[j].flags));
+        }
+        asm volatile("" ::"v"(rt0.started_id), "v"(rt0.expiry_time), "v"(rt0.task_status), "v"(rt0.key),
+                     "v"(rc0.initiated_id), "v"(rc0.started_id), "v"(rq0), "v"(rs0));
+#pragma unroll
+        for (int j = 0; j < FP; ++j) asm volatile("" ::"v"(rpk[j]));
         i32 prev = -1;
-#pragma unroll
-        for (int j = 0; j < A_SLOTS; ++j) {
-          if (j < L.n_act) {
-            const crr_activity_row r = *G.act(j);
-            const i32 v = loaded_v(r.schedule_id);
-            ok = ok && v > prev && r.timer_task_status >= 0 && r.timer_task_status <= 15;
-            prev = v;
-            const bool started = r.started_id != CRR_EMPTY_EVENT_ID;
-            i64 ct = add_seconds(r.scheduled_time, r.schedule_to_close);
-            i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
-            if (!started) {
-              cand_min(ct, cy, add_seconds(r.scheduled_time, r.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
-            } else {
-              cand_min(ct, cy, add_seconds(r.started_time, r.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
-              if (r.heartbeat > 0)
-                cand_min(ct, cy, add_seconds(max(r.started_time, r.last_heartbeat_time), r.heartbeat), CRR_TIMEOUT_HEARTBEAT);
-            }
-            M->a_key[j][t] = r.key;
-            M->a_cand[j][t] = ct;
-            // loaded started / cancel-requested events: any virtual step below vk (their IDs stay in the row)
-            M->a_src[j][t] = (u32)(v < 0 ? 0 : v) | ((started ? 0u : kStepMask) << kStepBits) |
-                             (((r.flags & CRR_ROW_CANCEL_REQUESTED) ? 0u : kStepMask) << (2 * kStepBits));
-            M->a_fl[j][t] = CRR_ROW_LIVE | (r.flags & (CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY)) |
-                            (started ? LF_STARTED : 0u) | ((u32)r.timer_task_status << LF_TTS_SHIFT) |
-                            ((u32)cy << CF_CAND_SHIFT) | ((u32)j << CF_SLOT_SHIFT);
+        auto put_act = [&](int j, const crr_activity_row& r) {
+          const i32 v = loaded_v(r.schedule_id);
+          ok = ok && v > prev && r.timer_task_status >= 0 && r.timer_task_status <= 15;
+          prev = v;
+          const bool started = r.started_id != CRR_EMPTY_EVENT_ID;
+          i64 ct = add_seconds(r.scheduled_time, r.schedule_to_close);
+          i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
+          if (!started) {
+            cand_min(ct, cy, add_seconds(r.scheduled_time, r.schedule_to_start), CRR_TIMEOUT_SCHEDULE_TO_START);
+          } else {
+            cand_min(ct, cy, add_seconds(r.started_time, r.start_to_close), CRR_TIMEOUT_START_TO_CLOSE);
+            if (r.heartbeat > 0)
+              cand_min(ct, cy, add_seconds(max(r.started_time, r.last_heartbeat_time), r.heartbeat), CRR_TIMEOUT_HEARTBEAT);
           }
-        }
+          M->a_key[j][t] = r.key;
+          M->a_cand[j][t] = ct;
+          // loaded started / cancel-requested events: any virtual step below vk (their IDs stay in the row)
+          M->a_src[j][t] = (u32)(v < 0 ? 0 : v) | ((started ? 0u : kStepMask) << kStepBits) |
+                           (((r.flags & CRR_ROW_CANCEL_REQUESTED) ? 0u : kStepMask) << (2 * kStepBits));
+          M->a_fl[j][t] = CRR_ROW_LIVE | (r.flags & (CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY)) |
+                          (started ? LF_STARTED : 0u) | ((u32)r.timer_task_status << LF_TTS_SHIFT) |
+                          ((u32)cy << CF_CAND_SHIFT) | ((u32)j << CF_SLOT_SHIFT);
+        };
+#pragma unroll
+        for (int j = 0; j < FA; ++j)
+          if (j < L.n_act) put_act(j, ra[j]);
+        for (int j = FA; j < L.n_act; ++j) put_act(j, *G.act(j));
         prev = -1;
-#pragma unroll
-        for (int j = 0; j < T_SLOTS; ++j) {
-          if (j < L.n_timer) {
-            const crr_timer_row r = *G.timer(j);
-            const i32 v = loaded_v(r.started_id);
-            ok = ok && v > prev && (r.task_status == CRR_TIMER_TASK_STATUS_NONE || r.task_status == CRR_TIMER_TASK_STATUS_CREATED);
-            prev = v;
-            M->t_key[j][t] = r.key;
-            M->t_exp[j][t] = r.expiry_time;
-            M->t_fl[j][t] = CRR_ROW_LIVE | (r.task_status == CRR_TIMER_TASK_STATUS_CREATED ? TF_CREATED : 0u) |
-                            ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << TF_SLOT_SHIFT);
-          }
-        }
+        auto put_timer = [&](int j, const crr_timer_row& r) {
+          const i32 v = loaded_v(r.started_id);
+          ok = ok && v > prev && (r.task_status == CRR_TIMER_TASK_STATUS_NONE || r.task_status == CRR_TIMER_TASK_STATUS_CREATED);
+          prev = v;
+          M->t_key[j][t] = r.key;
+          M->t_exp[j][t] = r.expiry_time;
+          M->t_fl[j][t] = CRR_ROW_LIVE | (r.task_status == CRR_TIMER_TASK_STATUS_CREATED ? TF_CREATED : 0u) |
+                          ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << TF_SLOT_SHIFT);
+        };
+        if (L.n_timer > 0) put_timer(0, rt0);
+        for (int j = 1; j < L.n_timer; ++j) put_timer(j, *G.timer(j));
         prev = -1;
-#pragma unroll
-        for (int j = 0; j < C_SLOTS; ++j) {
-          if (j < L.n_child) {
-            const crr_child_row r = *G.child(j);
-            const i32 v = loaded_v(r.initiated_id);
-            ok = ok && v > prev;
-            prev = v;
-            const u32 sst = r.started_id != CRR_EMPTY_EVENT_ID ? 0u : kStepMask;
-            M->c_fl[j][t] = CRR_ROW_LIVE | (kChildBatchNone << CHILD_BATCH_SHIFT) | ((u32)(v < 0 ? 0 : v) << 8) |
-                            (sst << (8 + kStepBits)) | ((u32)j << IF_SLOT_SHIFT);
-          }
-        }
+        auto put_child = [&](int j, const crr_child_row& r) {
+          const i32 v = loaded_v(r.initiated_id);
+          ok = ok && v > prev;
+          prev = v;
+          const u32 sst = r.started_id != CRR_EMPTY_EVENT_ID ? 0u : kStepMask;
+          M->c_fl[j][t] = CRR_ROW_LIVE | (kChildBatchNone << CHILD_BATCH_SHIFT) | ((u32)(v < 0 ? 0 : v) << 8) |
+                          (sst << (8 + kStepBits)) | ((u32)j << IF_SLOT_SHIFT);
+        };
+        if (L.n_child > 0) put_child(0, rc0);
+        for (int j = 1; j < L.n_child; ++j) put_child(j, *G.child(j));
         prev = -1;
-#pragma unroll
-        for (int j = 0; j < R_SLOTS; ++j) {
-          if (j < L.n_rc) {
-            const i32 v = loaded_v(G.rc(j)->initiated_id);
-            ok = ok && v > prev;
-            prev = v;
-            M->r_fl[j][t] = CRR_ROW_LIVE | ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << IF_SLOT_SHIFT);
-          }
-        }
+        auto put_init = [&](u32 (*fl)[LANES], int j, i64 id) {
+          const i32 v = loaded_v(id);
+          ok = ok && v > prev;
+          prev = v;
+          fl[j][t] = CRR_ROW_LIVE | ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << IF_SLOT_SHIFT);
+        };
+        if (L.n_rc > 0) put_init(M->r_fl, 0, rq0);
+        for (int j = 1; j < L.n_rc; ++j) put_init(M->r_fl, j, G.rc(j)->initiated_id);
         prev = -1;
+        if (L.n_sig > 0) put_init(M->s_fl, 0, rs0);
+        for (int j = 1; j < L.n_sig; ++j) put_init(M->s_fl, j, G.sig(j)->initiated_id);
 #pragma unroll
-        for (int j = 0; j < S_SLOTS; ++j) {
-          if (j < L.n_sig) {
-            const i32 v = loaded_v(G.sig(j)->initiated_id);
-            ok = ok && v > prev;
-            prev = v;
-            M->s_fl[j][t] = CRR_ROW_LIVE | ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << IF_SLOT_SHIFT);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < P_SLOTS; ++i)
-          if (i < L.n_rp) M->p_key[i][t] = G.rp(i)->key;
+        for (int i = 0; i < FP; ++i)
+          if (i < L.n_rp) M->p_key[i][t] = rpk[i];
+        for (int i = FP; i < L.n_rp; ++i) M->p_key[i][t] = G.rp(i)->key;
         // the ActivityID map: an entry is mapped unless a later-scheduled one holds the same ActivityID
 #pragma unroll
         for (int j = 0; j < A_SLOTS; ++j) {
@@ -2499,10 +2521,10 @@ struct LaneSource {
   }
   // step 0: every column with both type bytes, no load waiting on another (one round trip)
   __device__ __forceinline__ void start() {
-    if (n > 0) {
+    if (n > 0) {  // one branch: step 1's type byte (step 0's again for a one-event history) with the rest
       const i64 i = ix(0);
       nx.et = E.etype[i];
-      if (n > 1) et_nx = E.etype[ix(1)];
+      et_nx = E.etype[ix(n > 1 ? 1 : 0)];
       nx.id_ = E.event_id[i];
       nx.ver_ = E.version[i];
       nx.ts_ = E.timestamp[i];
@@ -3147,15 +3169,22 @@ __device__ __forceinline__ void refresh_tasks_rows(const crr_inputs& in, Lane& L
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
 // the replay loop of a launch that does not ask for tasks carries none of its registers.
 // CRC (compile time): the checksum computed here (every product launch sets it).
+// pre_x: the workflow's exec row already read by the caller (a kernel that expects loaded states issues it
+// with the descriptor, one round trip earlier), else nullptr
 template <bool EMIT, class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
-                                            const Geo& G, P& T, SRC& src, const u32* crc_tables) {
+                                            const Geo& G, P& T, SRC& src, const u32* crc_tables,
+                                            const crr_exec_row* pre_x = nullptr) {
   const i32 n_ev = wfp->ev_count;
   const i32 empty_at = wfp->empty_batch_at;
   const i64 now_ns = wfp->now_ns;
   // read once: a descriptor field read inside the loop is reloaded every event (stores in between may
   // alias it), and its wait drains the prefetched columns with it
   const i32 retention_days = wfp->retention_days;
+  // before any column load: a wait for it would otherwise also wait for those (vmcnt counts in order);
+  // pinned, so the (cache-hit) reads complete before the columns are issued
+  const u32 wf_flags0 = wfp->flags;
+  asm volatile("" ::"v"(wf_flags0), "v"(n_ev), "v"(empty_at));
 
   // newMutableStateBuilder (mutable_state_builder.go:174-242) + NewMutableStateBuilderWithVersionHistories (:245-254)
   Lane L;
@@ -3189,10 +3218,10 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     L.status = CRR_INTERNAL_RETRY;  // beyond the policy's encodings (CompactTables' 10-bit steps)
     goto done_events;
   }
-  if (wfp->flags & CRR_WF_FLAG_RESUME) {
+  if (wf_flags0 & CRR_WF_FLAG_RESUME) {
     if constexpr (P::kResumable) {
       // the loaded state (mutableStateBuilder.Load, mutable_state_builder.go:306-349) from the rows
-      const crr_exec_row X = out.exec[w];
+      const crr_exec_row X = pre_x ? *pre_x : out.exec[w];
       L.state = X.state; L.close_status = X.close_status;
       L.next_event_id = X.next_event_id; L.last_first_event_id = X.last_first_event_id;
       L.last_event_task_id = X.last_event_task_id; L.last_processed_event = X.last_processed_event;
@@ -3863,7 +3892,19 @@ template <class TIER, bool EMIT, bool RESUME, int TIER_NO>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   __shared__ CompactArena<TIER> arena;
   const u32* crc_tables = kCrcGlobal.v;
-  if constexpr (CompactLdsCrc<TIER_NO, RESUME>::value) {
+  const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
+  const bool in_range = w < hi;
+  const crr_workflow* wfp = in.wf + (in_range ? w : lo);
+  const i64 lane = threadIdx.x & 63;
+  Geo G;  // the descriptor in one round trip, as in replay_lds
+  load_geo(G, wfp, out, 64);
+  i64 ev_begin = wfp->ev_begin;
+  const i32 ev_count0 = wfp->ev_count;
+  const u32 wf_flags = wfp->flags;
+  // a kernel that expects loaded states reads every exec row with its descriptor (one round trip)
+  crr_exec_row X0;
+  if constexpr (RESUME) X0 = out.exec[in_range ? w : lo];
+  if constexpr (CompactLdsCrc<TIER_NO, RESUME>::value) {  // the tables' copy in the same round trip
     __shared__ u32 crc_lds[8 * 256];
     const uint4* src = reinterpret_cast<const uint4*>(kCrcGlobal.v);
     uint4* dst = reinterpret_cast<uint4*>(crc_lds);
@@ -3872,15 +3913,7 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
     __syncthreads();
     crc_tables = crc_lds;
   }
-  const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
-  if (w >= hi) return;
-  const crr_workflow* wfp = in.wf + w;
-  const i64 lane = threadIdx.x & 63;
-  Geo G;  // the descriptor in one round trip, as in replay_lds
-  load_geo(G, wfp, out, 64);
-  i64 ev_begin = wfp->ev_begin;
-  const i32 ev_count0 = wfp->ev_count;
-  const u32 wf_flags = wfp->flags;
+  if (!in_range) return;
   asm volatile("" ::"v"(ev_begin), "v"(ev_count0), "v"(wf_flags));
   if (((wf_flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   if ((lo & 63u) == 0) {  // wavefront == one interleaved group: group-uniform geometry in SGPRs
@@ -3890,7 +3923,8 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   CompactTables<TIER, RESUME> T;
   T.init(&arena, &in, ev_begin, ev_count0);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables,
+                                                             RESUME ? &X0 : nullptr);
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)

@@ -3252,7 +3252,23 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         L.vh_last_id = last.event_id;
         L.vh_last_ver = last.version;
       }
-      T.load(L, G);
+      if constexpr (FusedMapOps<P>::value) {
+        // an arena-held loaded state (compact tiers): the lines the tail reads -- the branch token the
+        // checksum covers, the last event's TaskID -- fetched now, with the rows, so those reads hit the L2
+        const u32 toff = L.token_src == 2 ? wfp->final_token_off : wfp->start_token_off;
+        const u32 tlen = L.token_src == 2 ? wfp->final_token_len : wfp->start_token_len;
+        u32 pf0 = 0, pf1 = 0;
+        u64 pf2 = 0;
+        if ((L.token_src == 1 || L.token_src == 2) && tlen != 0xFFFFFFFFu && tlen > 0) {
+          pf0 = in.arena[toff];
+          pf1 = in.arena[toff + tlen - 1];
+        }
+        if (n_ev > 0) pf2 = (u64)src.task_id(n_ev - 1);
+        T.load(L, G);
+        asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));
+      } else {
+        T.load(L, G);
+      }
       if (L.status != CRR_OK) goto done_events;  // a loaded state the policy cannot hold: general path
     } else {
       L.status = CRR_INTERNAL_RETRY;  // rows rebuilt from events cannot hold a loaded state: general path

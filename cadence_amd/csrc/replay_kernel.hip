@@ -792,6 +792,11 @@ constexpr u32 LF_STARTED = 32u;
 constexpr u32 LF_HB_VIS = 64u;  // a heartbeat timer was created: LastHeartbeatTimeoutVisibilityInSeconds set
 constexpr int LF_TTS_SHIFT = 8;
 constexpr u32 TF_CREATED = 2u;  // timer LDS flag: TaskStatus == TimerTaskStatusCreated
+// CompactTables<TIER, true>: a loaded activity whose row image changed (MAPPED, TimerTaskStatus) and a loaded
+// timer's TaskStatus as loaded -- finalize rewrites a loaded row in place only when it differs
+constexpr u32 LF_DIRTY = 128u;
+constexpr u32 LF_LOADED_MAPPED = 16u;   // the loaded row's persisted MAPPED bit
+constexpr u32 TF_LOADED_CREATED = 4u;
 
 template <class TIER>
 struct LdsArena {
@@ -1407,6 +1412,7 @@ struct CompactTables {
           M->a_src[j][t] = (u32)(v < 0 ? 0 : v) | ((started ? 0u : kStepMask) << kStepBits) |
                            (((r.flags & CRR_ROW_CANCEL_REQUESTED) ? 0u : kStepMask) << (2 * kStepBits));
           M->a_fl[j][t] = CRR_ROW_LIVE | (r.flags & (CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY)) |
+                          ((r.flags & CRR_ROW_MAPPED) ? LF_LOADED_MAPPED : 0u) |
                           (started ? LF_STARTED : 0u) | ((u32)r.timer_task_status << LF_TTS_SHIFT) |
                           ((u32)cy << CF_CAND_SHIFT) | ((u32)j << CF_SLOT_SHIFT);
         };
@@ -1421,7 +1427,8 @@ struct CompactTables {
           prev = v;
           M->t_key[j][t] = r.key;
           M->t_exp[j][t] = r.expiry_time;
-          M->t_fl[j][t] = CRR_ROW_LIVE | (r.task_status == CRR_TIMER_TASK_STATUS_CREATED ? TF_CREATED : 0u) |
+          M->t_fl[j][t] = CRR_ROW_LIVE |
+                          (r.task_status == CRR_TIMER_TASK_STATUS_CREATED ? TF_CREATED | TF_LOADED_CREATED : 0u) |
                           ((u32)(v < 0 ? 0 : v) << 8) | ((u32)j << TF_SLOT_SHIFT);
         };
         if (L.n_timer > 0) put_timer(0, rt0);
@@ -1462,7 +1469,8 @@ struct CompactTables {
 #pragma unroll
             for (int k = j + 1; k < A_SLOTS; ++k)
               if (k < L.n_act && M->a_key[k][t] == key) mapped = false;
-            if (mapped) M->a_fl[j][t] |= CRR_ROW_MAPPED;
+            const u32 f = M->a_fl[j][t];
+            M->a_fl[j][t] = f | (mapped ? CRR_ROW_MAPPED : 0u) | (mapped != ((f & LF_LOADED_MAPPED) != 0) ? LF_DIRTY : 0u);
           }
         }
       }
@@ -1570,7 +1578,7 @@ struct CompactTables {
         d = -1;
         if (is_act && !(f & CRR_ROW_MAPPED)) {  // DeleteActivity of an entry another one's ActivityID shadows
           const i32 m = find_act_mapped(M->a_key[hit][t]);
-          if (m >= 0) M->a_fl[m][t] &= ~CRR_ROW_MAPPED;
+          if (m >= 0) M->a_fl[m][t] = (M->a_fl[m][t] & ~CRR_ROW_MAPPED) | LF_DIRTY;
           else ++L.inconsistencies;
         }
       }
@@ -1595,7 +1603,7 @@ struct CompactTables {
                  (is_child ? (kStepMask << (8 + kStepBits)) | ((bd < kChildBatchNone ? bd : kChildBatchNone) << CHILD_BATCH_SHIFT)
                            : (bd << (8 + kStepBits)));
         if (is_act) {
-          if (hit >= 0) M->a_fl[hit][t] &= ~CRR_ROW_MAPPED;
+          if (hit >= 0) M->a_fl[hit][t] = (M->a_fl[hit][t] & ~CRR_ROW_MAPPED) | LF_DIRTY;
           // not started: ScheduleToClose and ScheduleToStart
           i64 ct = add_seconds(ev.ts(), as.schedule_to_close);
           i32 cy = CRR_TIMEOUT_SCHEDULE_TO_CLOSE;
@@ -1711,7 +1719,7 @@ struct CompactTables {
         const u32 f = M->a_fl[bj][t];
         const i32 y = (i32)((f >> CF_CAND_SHIFT) & 3u);
         if (!((f >> LF_TTS_SHIFT) & timer_mask(y))) {
-          M->a_fl[bj][t] = f | (timer_mask(y) << LF_TTS_SHIFT) | (y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u);
+          M->a_fl[bj][t] = f | (timer_mask(y) << LF_TTS_SHIFT) | (y == CRR_TIMEOUT_HEARTBEAT ? LF_HB_VIS : 0u) | LF_DIRTY;
           // the task carries ActivityInfo.Attempt: 0 for this call's activities, a loaded row's own
           const i32 att = (RESUME && K.on && bs < (u32)vk) ? G_act_loaded(f)->attempt : 0;
           K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, bt, id_at(bs), att, -1);
@@ -1749,7 +1757,7 @@ struct CompactTables {
   // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
   __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
 #pragma unroll
-    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] &= ~(0xFu << LF_TTS_SHIFT);
+    for (int j = 0; j < A_SLOTS; ++j) M->a_fl[j][t] = (M->a_fl[j][t] & ~(0xFu << LF_TTS_SHIFT)) | LF_DIRTY;
 #pragma unroll
     for (int j = 0; j < T_SLOTS; ++j) M->t_fl[j][t] &= ~TF_CREATED;
     dirty_act = dirty_timer = true;
@@ -1803,10 +1811,11 @@ struct CompactTables {
         const u32 tts = (f >> LF_TTS_SHIFT) & 0xF;
         const u32 fl = f & (CRR_ROW_LIVE | CRR_ROW_MAPPED | CRR_ROW_CANCEL_REQUESTED | CRR_ROW_HAS_RETRY);
         crr_activity_row* dst = G.act(i);
-        if (slot == i && !new_st && !new_sc && !(f & LF_HB_VIS)) {  // in place: only the bookkeeping words
-          const crr_activity_row* cur = G.act(i);
-          if ((u32)cur->timer_task_status != tts) dst->timer_task_status = (i32)tts;
-          if (cur->flags != fl) dst->flags = fl;
+        if (slot == i && !new_st && !new_sc && !(f & LF_HB_VIS)) {  // in place: only the bookkeeping words,
+          if (f & LF_DIRTY) {                                        // and only if they changed
+            dst->timer_task_status = (i32)tts;
+            dst->flags = fl;
+          }
           continue;
         }
         crr_activity_row r = *G.act(slot);
@@ -1853,8 +1862,8 @@ struct CompactTables {
       const i32 status = (f & TF_CREATED) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
       if (RESUME && src < vk) {  // a loaded timer: only its task status can have changed
         const i32 slot = (i32)((f >> TF_SLOT_SHIFT) & 15u);
-        if (slot == i) {
-          if (G.timer(i)->task_status != status) G.timer(i)->task_status = status;
+        if (slot == i) {  // in place: the status word, if it changed
+          if (((f & TF_CREATED) != 0) != ((f & TF_LOADED_CREATED) != 0)) G.timer(i)->task_status = status;
         } else {
           crr_timer_row r = *G.timer(slot);
           r.task_status = status;
@@ -3169,12 +3178,27 @@ __device__ __forceinline__ void refresh_tasks_rows(const crr_inputs& in, Lane& L
 // EMIT (compile time): task emission compiled in.  The fast kernels are also built without it, so
 // the replay loop of a launch that does not ask for tasks carries none of its registers.
 // CRC (compile time): the checksum computed here (every product launch sets it).
+// Profiling aid (variant builds only, -DCRR_PHASE_PROF=1; tools/prof_replication.py --phases): wave clock at
+// the phase boundaries of replay_body, summed per phase over lane 0 of every lane-path wavefront.
+#ifndef CRR_PHASE_PROF
+#define CRR_PHASE_PROF 0
+#endif
+#if CRR_PHASE_PROF
+__device__ unsigned long long g_phase_prof[8];
+#define CRR_PHASE(k) do { if constexpr (!std::is_same<SRC, WaveSource>::value) ph[k] = __builtin_readcyclecounter(); } while (0)
+#else
+#define CRR_PHASE(k) do {} while (0)
+#endif
 // pre_x: the workflow's exec row already read by the caller (a kernel that expects loaded states issues it
 // with the descriptor, one round trip earlier), else nullptr
 template <bool EMIT, class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
                                             const Geo& G, P& T, SRC& src, const u32* crc_tables,
                                             const crr_exec_row* pre_x = nullptr) {
+#if CRR_PHASE_PROF
+  u64 ph[7] = {0, 0, 0, 0, 0, 0, 0};
+#endif
+  CRR_PHASE(0);
   const i32 n_ev = wfp->ev_count;
   const i32 empty_at = wfp->empty_batch_at;
   const i64 now_ns = wfp->now_ns;
@@ -3270,6 +3294,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         T.load(L, G);
       }
       if (L.status != CRR_OK) goto done_events;  // a loaded state the policy cannot hold: general path
+      CRR_PHASE(1);
     } else {
       L.status = CRR_INTERNAL_RETRY;  // rows rebuilt from events cannot hold a loaded state: general path
       goto done_events;
@@ -3613,6 +3638,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     }
   }
 done_events:
+  CRR_PHASE(2);
 #undef CHECK
 #undef CHECK_N
 #undef FAIL
@@ -3636,7 +3662,9 @@ done_events:
     it->event_id = L.vh_last_id;
     it->version = L.vh_last_ver;
   }
+  CRR_PHASE(3);
   T.finalize(L, G);
+  CRR_PHASE(4);
   if constexpr (EMIT) {  // RefreshTasks' tasks from the final rows
     if (K.on && want_crc && (wfp->flags & CRR_WF_FLAG_REFRESH_TASKS)) {
       if constexpr (std::is_same<SRC, WaveSource>::value) wave_sync_global();
@@ -3689,8 +3717,31 @@ done_events:
   R.src_next = L.src_base + n_ev;
   R.reserved = 0;
   if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len, true, L.vh_last_id, L.vh_last_ver);
+  CRR_PHASE(5);
   out.exec[w] = R;
+#if CRR_PHASE_PROF
+  if constexpr (!std::is_same<SRC, WaveSource>::value) {
+    if ((wfp->flags & CRR_WF_FLAG_RESUME) && (threadIdx.x & 63) == 0 && ph[1] != 0) {
+      atomicAdd(&g_phase_prof[0], ph[1] - ph[0]);  // prologue + load
+      atomicAdd(&g_phase_prof[1], ph[2] - ph[1]);  // event loop + tail reads
+      atomicAdd(&g_phase_prof[2], ph[3] - ph[2]);  // token issue, VH write
+      atomicAdd(&g_phase_prof[3], ph[4] - ph[3]);  // finalize
+      atomicAdd(&g_phase_prof[4], ph[5] - ph[4]);  // refresh / exec row / checksum
+      atomicAdd(&g_phase_prof[5], 1ull);
+    }
+  }
+#endif
 }
+#if CRR_PHASE_PROF
+extern "C" int crr_phase_prof(unsigned long long* host, int reset) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase_prof), sizeof(g_phase_prof)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // ---- kernels ---------------------------------------------------------------------------------------
 // Workflows [0, n_lane) use the batch stride (wave-interleaved: lane per workflow); workflows

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
     p.add_argument("--hbm-rows", action="store_true", help="every lane workflow over its HBM rows (round-3 path)")
+    p.add_argument("--phases", action="store_true", help="a -DCRR_PHASE_PROF=1 library: per-phase wave clocks")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -43,16 +44,27 @@ def main():
     pr.setup()
     setup_s = time.time() - t0
     ms = []
+    if a.phases:
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        eng.lib.crr_phase_prof(buf, 1)
     for _ in range(a.reps + 1):
         pr.restore()
         torch.cuda.synchronize()
         eng.launch(pr.db_new)
         torch.cuda.synchronize()
         ms.append(sum(x for x in eng.last_kernel_ms()[:2] if x > 0))
+    phases = None
+    if a.phases:
+        eng.lib.crr_phase_prof(buf, 0)
+        n = max(int(buf[5]), 1)
+        phases = {k: buf[i] / n for i, k in enumerate(["prologue_load", "events_tail", "token_vh", "finalize",
+                                                          "exec_crc"])}
+        phases["waves"] = int(buf[5])
     v = pr.verify(one_shot)
     med = float(np.median(ms[1:]))
     print(json.dumps({"hbm_rows": a.hbm_rows, "workflows": a.wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
-                      "events_per_s": pr.n_events / (med * 1e-3), "verify": v, "setup_s": setup_s}), flush=True)
+                      "events_per_s": pr.n_events / (med * 1e-3), "verify": v, "setup_s": setup_s, "phase_clocks_per_wave": phases}), flush=True)
 
 
 if __name__ == "__main__":

@@ -72,7 +72,8 @@ __constant__ int8_t kTasksPerEvent[CRR_EV_TYPE_COUNT] = {
 struct KeyRef {     // a string to intern (an event's key or a previous reset point): where, and its hash
   u64 off;          // byte offset of the string in `bytes`
   u32 len;
-  u32 hash;         // FNV-1a 32 of its bytes
+  u32 hash;         // str_hash of its bytes
+  u64 head[2];      // its first 16 bytes, zero-padded: a string up to 16 bytes compares without a read
 };
 // the Points list of a start event's PrevAutoResetPoints (kept in its key slot: Started has no key)
 struct PrevRef {
@@ -93,6 +94,8 @@ struct Plan {       // pointers into the caller's scratch (carved by carve())
   crr_activity_side* act;    // [max_events] at the ActivityTaskScheduled event's own slot
   crr_start_side* start;     // [max_events] at the WorkflowExecutionStarted event's own slot
   KeyRef* keys;              // [max_events] a keyed event's string (a Started event's PrevRef)
+  KeyRef* dom_refs;          // [max_events] domain names the fast decode left to domain_resolve_kernel
+                             // (aliases `table`, which only wf_pass uses, after the resolve)
   KeyRef* resets;            // [max_events] previous reset points, canonical reset_keys order
   u32* reset_ids;            // [max_events] their interned ids (= the reset_keys array)
   u64* table;                // per-workflow hash tables [8 * max_events + 64 * n_wf]
@@ -122,6 +125,19 @@ __host__ __device__ inline size_t align_up(size_t x) { return (x + 255) & ~(size
 constexpr size_t kDomainBytes = 64 * 1024;   // the known-domain set (<= 8192 names)
 constexpr i32 kErrScratch = -100;            // CRR_INGEST_SCRATCH_TOO_SMALL
 
+// ---- the device's string hash (interning and the known-domain set; never leaves the ingest) -------------
+// Eight little-endian bytes per step (the tail zero-padded, the length in the seed), a 32-bit
+// multiply per half, a final avalanche so a table's low bits see every byte.
+__device__ __forceinline__ u32 str_hash_init(u32 len) { return 2166136261u ^ (len * 0x9E3779B1u); }
+__device__ __forceinline__ u32 str_hash_step(u32 h, u64 v) {
+  h = (h ^ (u32)v) * 16777619u;
+  return (h ^ (u32)(v >> 32)) * 16777619u;
+}
+__device__ __forceinline__ u32 str_hash_final(u32 h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
 // ---- byte reader over one blob: a 32-byte aligned window in registers ----------------------------------
 // The window holds bytes [wb, wb + 32); any read of up to 8 bytes starting in its first half is served
 // from registers.  A sequential walk shifts it by 16 bytes with one dwordx4 load.  `bytes` is readable
@@ -137,16 +153,30 @@ __device__ __attribute__((noinline)) Cursor skip_nested(const u8* b, u64 p, u64 
 // state (reader, event) in scratch memory.
 constexpr int kDeferGeneral = -90;
 constexpr u32 kDeferMark = 0xFFFFFFFFu;   // cnt[1][blob] of a deferred blob, until the general pass
-template <bool G>
+// L: the window loads come from an LDS copy of the bytes [base, ...) (blob_decode_kernel stages each
+// wavefront's blobs there with coalesced loads), positions stay offsets into `bytes`.
+typedef const u8 __attribute__((address_space(3))) lds_u8;
+typedef const v4u __attribute__((address_space(3))) lds_v4u;
+template <bool G, bool L = false>
 struct RdT {
   const u8* b;
+  lds_u8* lb;        // L: the staged copy, lb[0] = bytes[base]
+  u64 base;
   u64 p, end;
   u64 wb;            // window base (16-aligned), ~0: none
   v4u w0, w1;     // native vectors: HIP's uint4 struct is copied by memcpy, which keeps the reader in scratch
   int err;           // CRR_DECODE_* (0 ok)
 
   __device__ __forceinline__ void init(const u8* bytes, u64 begin, u64 e) {
-    b = bytes; p = begin; end = e; wb = ~0ull; err = 0;
+    b = bytes; lb = nullptr; base = 0; p = begin; end = e; wb = ~0ull; err = 0;
+  }
+  __device__ __forceinline__ void init_staged(const u8* bytes, lds_u8* staged, u64 staged_base, u64 begin, u64 e) {
+    init(bytes, begin, e);
+    lb = staged; base = staged_base;
+  }
+  __device__ __forceinline__ v4u ld16(u64 a) const {
+    if constexpr (L) return *reinterpret_cast<lds_v4u*>(lb + (u32)(a - base));
+    else return *reinterpret_cast<const v4u*>(b + a);
   }
   __device__ __forceinline__ bool need(u64 n) {
     if (err) return false;
@@ -160,9 +190,9 @@ struct RdT {
       if (a == wb + 16) {
         w0 = w1;
       } else {
-        w0 = *reinterpret_cast<const v4u*>(b + a);
+        w0 = ld16(a);
       }
-      w1 = *reinterpret_cast<const v4u*>(b + a + 16);
+      w1 = ld16(a + 16);
       wb = a;
     }
     // dwords k, k+1, k+2 of the window (k = o / 4) by two bit-selects, then the byte shift: no dynamic
@@ -218,17 +248,28 @@ struct RdT {
     len = (u32)n;
     p += (u64)n;
   }
-  // FNV-1a 32 over bytes [off, off + len) through the window (the string was just walked past)
+  // a string's KeyRef (len > 0): where, its hash and its first 16 bytes, through the window
+  __device__ __forceinline__ u64 head8(u64 off, u32 len) {   // bytes [off, off + min(len, 8)), zero-padded
+    const u64 v = peek8(off);
+    return len < 8 ? v & ((1ull << (8 * len)) - 1) : v;
+  }
+  __device__ __forceinline__ KeyRef key_ref(u64 off, u32 len) {
+    KeyRef k;
+    k.off = off; k.len = len; k.hash = 0; k.head[0] = 0; k.head[1] = 0;
+    if (len == 0) return k;
+    k.hash = hash(off, len);
+    k.head[0] = head8(off, len);
+    if (len > 8) k.head[1] = head8(off + 8, len - 8);
+    return k;
+  }
+  // str_hash of bytes [off, off + len) through the window (the string was just walked past)
   __device__ __forceinline__ u32 hash(u64 off, u32 len) {
-    u32 h = 2166136261u;
-    u32 i = 0;
-    while (i < len) {
+    u32 h = str_hash_init(len);
+    for (u32 i = 0; i < len; i += 8) {
       const u64 v = peek8(off + i);
-      const u32 m = len - i < 8 ? len - i : 8;
-      for (u32 j = 0; j < m; ++j) h = (h ^ (u32)((v >> (8 * j)) & 0xff)) * 16777619u;
-      i += m;
+      h = str_hash_step(h, len - i < 8 ? v & ((1ull << (8 * (len - i))) - 1) : v);
     }
-    return h;
+    return str_hash_final(h);
   }
   // skip one value of `type` (history_decode.cpp Reader::skip: a value nested deeper than 64 is
   // BAD_TYPE).  Inline: scalars, strings, structs (a count of open structs) and lists / sets / maps of
@@ -410,10 +451,8 @@ __device__ __forceinline__ void read_retry_policy(RdT<G>& r, Attr& a) {
 // kept; its strings are read once the event is complete (WfFlattener::add interns them there).  Out of
 // reader of its own, result by value.
 struct PrevPoints { u64 p; u64 pos; i32 err, mode, n; u32 et; };
-template <bool G>
-__device__ __forceinline__ PrevPoints read_reset_points(const u8* b, u64 p, u64 end) {
-  RdT<G> r;
-  r.init(b, p, end);
+template <class R>
+__device__ __forceinline__ PrevPoints walk_reset_points(R r) {
   PrevPoints o{0, 0, 0, -2, 0, 0};
   u32 ft;
   i32 id;
@@ -443,6 +482,12 @@ __device__ __forceinline__ PrevPoints read_reset_points(const u8* b, u64 p, u64 
   o.p = r.p;
   o.err = r.err;
   return o;
+}
+template <bool G>
+__device__ __forceinline__ PrevPoints read_reset_points(const u8* b, u64 p, u64 end) {
+  RdT<G> r;
+  r.init(b, p, end);
+  return walk_reset_points(r);
 }
 
 // history_decode.cpp read_attributes
@@ -599,23 +644,27 @@ __device__ __forceinline__ bool keyed_type(i32 t) {
          t == CRR_EV_TIMER_CANCELED;
 }
 
-__device__ __forceinline__ u32 fnv1a(const u8* b, u64 off, u32 len) {   // (known domain names)
-  u32 h = 2166136261u;
-  for (u32 i = 0; i < len; ++i) h = (h ^ b[off + i]) * 16777619u;
-  return h;
+__device__ __forceinline__ u32 str_hash_bytes(const u8* b, u64 off, u32 len) {   // (known domain names)
+  u32 h = str_hash_init(len);
+  for (u32 i = 0; i < len; i += 8) {
+    u64 v = 0;
+    for (u32 j = 0; j < 8 && i + j < len; ++j) v |= (u64)b[off + i + j] << (8 * j);
+    h = str_hash_step(h, v);
+  }
+  return str_hash_final(h);
 }
 
 // ---- domain-cache stand-in: the known domain names as an open-addressed set -----------------------------
 __device__ __forceinline__ bool bytes_equal(const u8* a, u64 ao, const u8* b, u64 bo, u32 n) {
-  for (u32 i = 0; i < n; ++i)
-    if (a[ao + i] != b[bo + i]) return false;
-  return true;
+  u32 d = 0;   // no early exit: the byte loads are independent, not a chain of round trips
+  for (u32 i = 0; i < n; ++i) d |= (u32)(a[ao + i] ^ b[bo + i]);
+  return d == 0;
 }
 
 __global__ void domains_build_kernel(crr_blob_batch in, u32* table, u32 cap) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= in.n_domains) return;
-  u32 h = fnv1a(in.strings, in.domain_off[i], in.domain_len[i]) & (cap - 1);
+  u32 h = str_hash_bytes(in.strings, in.domain_off[i], in.domain_len[i]) & (cap - 1);
   for (u32 probe = 0; probe < cap; ++probe) {
     const u32 prev = atomicCAS(table + h, 0u, i + 1);
     if (prev == 0) return;
@@ -628,7 +677,7 @@ __device__ __forceinline__ i32 domain_status(const crr_blob_batch& in, const u32
   if (len == 0) return CRR_DOMAIN_NOT_SET;
   if (in.n_domains == 0xFFFFFFFFu) return CRR_DOMAIN_RESOLVED;
   if (cap == 0) return CRR_DOMAIN_UNKNOWN;
-  u32 h = fnv1a(in.bytes, off, len) & (cap - 1);
+  u32 h = str_hash_bytes(in.bytes, off, len) & (cap - 1);
   for (u32 probe = 0; probe < cap; ++probe) {
     const u32 e = table[h];
     if (e == 0) return CRR_DOMAIN_UNKNOWN;
@@ -639,7 +688,7 @@ __device__ __forceinline__ i32 domain_status(const crr_blob_batch& in, const u32
   return CRR_DOMAIN_UNKNOWN;
 }
 
-// the same, the name's FNV-1a already computed (through the reader's window)
+// the same, the name's str_hash already computed (through the reader's window)
 __device__ __forceinline__ i32 domain_status_h(const crr_blob_batch& in, const u32* table, u32 cap, u64 off, u32 len,
                                                u32 hash) {
   if (len == 0) return CRR_DOMAIN_NOT_SET;
@@ -654,6 +703,21 @@ __device__ __forceinline__ i32 domain_status_h(const crr_blob_batch& in, const u
     h = (h + 1) & (cap - 1);
   }
   return CRR_DOMAIN_UNKNOWN;
+}
+
+// The fast decode's domain lookups: the constant outcomes at once, a lookup in the known-domain set
+// deferred (the name's reference kept at the event's slot, kDomainPending in the field) to
+// domain_resolve_kernel, a lane per event -- so no walk waits on the set's round trips.
+constexpr i32 kDomainPending = 0x7FFF0D0D;
+template <class R>
+__device__ __forceinline__ i32 domain_fast(R& r, const crr_blob_batch& in, const Plan& P, u64 x, u64 off, u32 len) {
+  if (len == 0) return CRR_DOMAIN_NOT_SET;
+  if (in.n_domains == 0xFFFFFFFFu) return CRR_DOMAIN_RESOLVED;
+  if (P.dom_cap == 0) return CRR_DOMAIN_UNKNOWN;
+  KeyRef d;
+  d.off = off; d.len = len; d.hash = r.hash(off, len); d.head[0] = 0; d.head[1] = 0;
+  P.dom_refs[x] = d;
+  return kDomainPending;
 }
 
 // every blob decoded and the canonical scratch large enough: the later passes may read it
@@ -823,8 +887,7 @@ __device__ __forceinline__ void decode_blob(const crr_blob_batch& in, const Plan
           default: break;
         }
         if (valid && keyed_type(t)) {   // "" when the attribute is absent (key 0)
-          KeyRef kr;
-          kr.off = a.key_off; kr.len = a.key_len; kr.hash = a.key_len ? r.hash(a.key_off, a.key_len) : 0u;
+          const KeyRef kr = r.key_ref(a.key_off, a.key_len);
           P.keys[x] = kr;
         }
         P.ref[x] = ref;
@@ -863,7 +926,8 @@ __device__ __forceinline__ bool domain_aux_type(i32 t) {
 }
 
 // the attribute fields read_attributes takes, stored where decode_blob puts them
-__device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_blob_batch& in, const Plan& P, u64 x,
+template <class R>
+__device__ __forceinline__ void fast_attributes(R& r, i32 t, const crr_blob_batch& in, const Plan& P, u64 x,
                                                 u32& seen, u32& n_prev) {
   u32 ft;
   i32 id;
@@ -878,7 +942,7 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
         if (id == 12 && ft == T_STRING) {
           u64 o; u32 l;
           r.str(o, l);
-          if (!r.err) ss->parent_domain_status = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u);
+          if (!r.err) ss->parent_domain_status = domain_fast(r, in, P, x, o, l);
         }
         else if (id == 40 && ft == T_I32) ss->workflow_timeout = r.be32();
         else if (id == 50 && ft == T_I32) ss->decision_start_to_close = r.be32();
@@ -887,7 +951,7 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
         else if (id == 90 && ft == T_I64) ss->expiration_ns = r.be64();
         else if (id == 110 && ft == T_I32) ss->first_decision_backoff = r.be32();
         else if (id == 130 && ft == T_STRUCT) {
-          const PrevPoints q = read_reset_points<false>(r.b, r.p, r.end);
+          const PrevPoints q = walk_reset_points(r);   // a copy of the reader, window included
           r.p = q.p;
           r.err = q.err;
           if (!r.err) {
@@ -916,12 +980,12 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
         if (id == 10 && ft == T_STRING) {
           u64 o; u32 l;
           r.str(o, l);
-          if (!r.err) { KeyRef kr; kr.off = o; kr.len = l; kr.hash = l ? r.hash(o, l) : 0u; P.keys[x] = kr; }
+          if (!r.err) P.keys[x] = r.key_ref(o, l);
         }
         else if (id == 25 && ft == T_STRING) {
           u64 o; u32 l;
           r.str(o, l);
-          if (!r.err) as->domain_status = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u);
+          if (!r.err) as->domain_status = domain_fast(r, in, P, x, o, l);
         }
         else if (id == 45 && ft == T_I32) as->schedule_to_close = r.be32();
         else if (id == 50 && ft == T_I32) as->schedule_to_start = r.be32();
@@ -946,7 +1010,7 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
         if (id == key_id && ft == T_STRING) {
           u64 o; u32 l;
           r.str(o, l);
-          if (!r.err) { KeyRef kr; kr.off = o; kr.len = l; kr.hash = l ? r.hash(o, l) : 0u; P.keys[x] = kr; }
+          if (!r.err) P.keys[x] = r.key_ref(o, l);
         }
         else if (id == ref_id && ft == T_I64) { P.ref[x] = r.be64(); seen |= S_REF; }
         else used = false;
@@ -959,7 +1023,7 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
         if (id == dom_id && ft == T_STRING) {
           u64 o; u32 l;
           r.str(o, l);
-          if (!r.err) { P.aux[x] = domain_status_h(in, P.dom_table, P.dom_cap, o, l, l ? r.hash(o, l) : 0u); seen |= S_AUX; }
+          if (!r.err) { P.aux[x] = domain_fast(r, in, P, x, o, l); seen |= S_AUX; }
         }
         else used = false;
         break;
@@ -991,8 +1055,9 @@ __device__ __forceinline__ void fast_attributes(RdT<false>& r, i32 t, const crr_
 }
 
 // one event into slot x (decode_blob's loop body for a canonical event)
-__device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& in, const Plan& P, u64 x, i32 new_run,
-                                           u32& n_prev) {
+template <class R>
+__device__ __forceinline__ void fast_event(R& r, const crr_blob_batch& in, const Plan& P, u64 x, i32 new_run,
+                                           u32& n_prev, u32 boundary) {
   u32 seen = 0;
   i32 t = -1;
   bool have_type = false;
@@ -1023,9 +1088,7 @@ __device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& 
         P.act[x] = as;
       }
       if (t >= 0 && t < CRR_EV_TYPE_COUNT && keyed_type(t)) {
-        KeyRef kr;
-        kr.off = 0; kr.len = 0; kr.hash = 0;
-        P.keys[x] = kr;
+        P.keys[x] = r.key_ref(0, 0);
       }
     }
     else if (id == 35 && ft == T_I64) { P.ver[x] = r.be64(); seen |= S_VER; }
@@ -1041,7 +1104,7 @@ __device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& 
   if (r.err) return;
   if (!have_type) { r.err = kDeferGeneral; return; }   // the type's zero default: the general pass
   const bool valid = t >= 0 && t < CRR_EV_TYPE_COUNT;
-  P.etype[x] = (u8)(valid ? t : CRR_EV_PAD - 1);
+  P.etype[x] = (u8)((valid ? t : CRR_EV_PAD - 1) | boundary);
   if (!(seen & S_ID)) P.id[x] = 0;
   if (!(seen & S_TS)) P.ts[x] = 0;
   if (!(seen & S_VER)) P.ver[x] = 0;
@@ -1052,17 +1115,17 @@ __device__ __forceinline__ void fast_event(RdT<false>& r, const crr_blob_batch& 
   P.key[x] = 0;
 }
 
-__device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const Plan& P, u32 bi) {
-  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
-  const u64 NB = (u64)P.n_blobs + 1;
-  u64 x = P.off[0 * NB + bi];
-  const u64 x_end = P.off[0 * NB + bi + 1];
+// The blob's slots [x, x_end) and its workflow's new_run_wf come from the caller (loaded before the
+// staging).  Batch boundaries are set as the events are written: a count that was wrong sends the plan
+// back to the recount and this decode runs again, so x_end is exact whenever the results are used.
+template <bool L>
+__device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const Plan& P, u32 bi, u64 b0, u64 b1,
+                                                 u64 x, u64 x_end, i32 new_run, lds_u8* staged, u64 staged_base) {
   u32 n_prev = 0;
   if (b1 > b0) {
-    RdT<false> r;
-    r.init(in.bytes, b0, b1);
+    RdT<false, L> r;
+    r.init_staged(in.bytes, staged, staged_base, b0, b1);
     if (r.u8_() != 0x59) { record_error(P.err, bi, CRR_DECODE_BAD_PREAMBLE); return; }  // version0Thriftrw.go:53-58
-    const i32 new_run = in.wf[P.blob_wf[bi]].new_run_wf;
     const u64 x_first = x;
     u32 ft;
     i32 fid;
@@ -1075,7 +1138,8 @@ __device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const
       if (et != T_STRUCT && n > 0) { r.err = CRR_DECODE_BAD_TYPE; break; }
       for (i32 i = 0; i < n; ++i) {
         if (x >= x_end) { r.err = kDeferGeneral; break; }   // more events than announced
-        fast_event(r, in, P, x, new_run, n_prev);
+        fast_event(r, in, P, x, new_run, n_prev,
+                   (x == x_first ? CRR_ETYPE_BATCH_FIRST : 0u) | (x + 1 == x_end ? CRR_ETYPE_BATCH_LAST : 0u));
         if (r.err) break;
         ++x;
       }
@@ -1086,24 +1150,75 @@ __device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const
       return;
     }
     if (r.err) { record_error(P.err, bi, r.err); return; }
-    if (x > x_first) {   // batch boundaries
-      P.etype[x_first] |= CRR_ETYPE_BATCH_FIRST;
-      P.etype[x - 1] |= CRR_ETYPE_BATCH_LAST;
-    }
   }
   if (x != x_end) atomicOr(P.flags, 1u);   // fewer events than the header announced: recount
   P.cnt[1 * (u64)P.n_blobs + bi] = n_prev;
 }
 
-__global__ __launch_bounds__(kBlock) void blob_decode_kernel(crr_blob_batch in, Plan P) {
-  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bi >= in.n_blobs) return;
+// A wavefront per 64 consecutive blobs.  Their bytes are contiguous: the wavefront copies them into LDS
+// with coalesced 16-byte loads (up to kStageBytes at a time), then every lane walks its own blob from
+// LDS, so a walk's window loads are LDS round trips instead of a chain of dependent HBM reads.  A
+// window holding only some of the blobs serves those; the rest are staged again from the first one left.
+// A blob larger than the window alone is walked from HBM.
+constexpr u32 kStageBytes = 20 * 1024;   // 8 wavefronts per CU (the walk's registers allow 2 per SIMD)
+__global__ __launch_bounds__(64) void blob_decode_kernel(crr_blob_batch in, Plan P) {
+  __shared__ __attribute__((aligned(16))) u8 stage[kStageBytes];
+  const u32 lane = threadIdx.x;
+  const u32 bi = blockIdx.x * 64 + lane;
+  const bool mine = bi < in.n_blobs;
   const u64 NB = (u64)P.n_blobs + 1;
   // this plan's mark, never an earlier plan's: a blob whose fast decode fails or is skipped leaves no
   // stale kDeferMark (the scratch is reused across plans) for the general pass to act on
-  P.cnt[1 * (u64)P.n_blobs + bi] = 0;
+  if (mine) P.cnt[1 * (u64)P.n_blobs + bi] = 0;
   if (P.off[0 * NB + P.n_blobs] > P.max_events) return;   // the summary reports it
-  decode_blob_fast(in, P, bi);
+  const u32 last = blockIdx.x * 64 + 64 < in.n_blobs ? blockIdx.x * 64 + 64 : in.n_blobs;
+  // readable up to 32 bytes past the last blob (cadence_ingest.h): a walk's window reads end before
+  // ((b1 - 1) & ~15) + 32 <= (b1 + 31) & ~15
+  const u64 stage_cap = (in.blob_off[last] + 31) & ~15ull;
+  const u64 b0 = mine ? in.blob_off[bi] : 0, b1 = mine ? in.blob_off[bi + 1] : 0;
+  const u64 x0 = mine ? P.off[0 * NB + bi] : 0, x1 = mine ? P.off[0 * NB + bi + 1] : 0;
+  const i32 new_run = mine && b1 > b0 ? in.wf[P.blob_wf[bi]].new_run_wf : 0;
+  lds_u8* lb = (lds_u8*)stage;
+  bool done = !mine;
+  for (;;) {
+    const u64 pending = __ballot(!done);
+    if (pending == 0) break;
+    const int f = __builtin_ctzll(pending);
+    const u64 s = (u64)__shfl((long long)b0, f) & ~15ull;
+    const u64 lim = s + kStageBytes < stage_cap ? s + kStageBytes : stage_cap;
+    __syncthreads();   // the previous window's walks are done with it
+    for (u64 o = s + 16ull * lane; o < lim; o += 64 * 16)
+      *reinterpret_cast<v4u*>(stage + (o - s)) = *reinterpret_cast<const v4u*>(in.bytes + o);
+    __syncthreads();
+    const bool fits = !done && (b1 == b0 || (b0 >= s && ((b1 - 1) & ~15ull) + 32 <= lim));
+    if (fits) {
+      decode_blob_fast<true>(in, P, bi, b0, b1, x0, x1, new_run, lb, s);
+      done = true;
+    } else if (!done && (int)lane == f) {   // larger than the window: from HBM
+      decode_blob_fast<false>(in, P, bi, b0, b1, x0, x1, new_run, lb, 0);
+      done = true;
+    }
+  }
+}
+
+// the fast decode's deferred domain lookups (domain_fast), a lane per event; only when the plan has a
+// known-domain set
+__global__ __launch_bounds__(kBlock) void domain_resolve_kernel(crr_blob_batch in, Plan P) {
+  const u64 NB = (u64)P.n_blobs + 1;
+  const u64 n = P.off[0 * NB + P.n_blobs];
+  if (n > P.max_events || *P.flags || *P.err != ~0ull) return;   // the plan reports / recounts
+  const u64 n_bytes = in.blob_off[in.n_blobs];
+  for (u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (u64)gridDim.x * blockDim.x) {
+    const i32 t = P.etype[x] & CRR_ETYPE_MASK;
+    i32* dst = t == CRR_EV_WORKFLOW_EXECUTION_STARTED ? &P.start[x].parent_domain_status
+               : t == CRR_EV_ACTIVITY_TASK_SCHEDULED  ? &P.act[x].domain_status
+               : domain_aux_type(t)                    ? P.aux + x
+                                                       : nullptr;
+    if (!dst || *dst != kDomainPending) continue;
+    const KeyRef d = P.dom_refs[x];
+    if (d.off > n_bytes || d.len > n_bytes - d.off) continue;   // (never: written by this plan's decode)
+    *dst = domain_status_h(in, P.dom_table, P.dom_cap, d.off, d.len, d.hash);
+  }
 }
 
 // the blobs the fast pass deferred (a container of structs / containers), with the general reader
@@ -1141,9 +1256,7 @@ __global__ void reset_refs_kernel(crr_blob_batch in, Plan P) {
           else r.skip(t2);
         }
       }
-      KeyRef kr;
-      kr.off = so; kr.len = sl; kr.hash = sl ? r.hash(so, sl) : 0u;
-      P.resets[k++] = kr;
+      P.resets[k++] = r.key_ref(so, sl);
     }
   }
 }
@@ -1260,6 +1373,263 @@ __device__ __forceinline__ bool same_bytes(const u8* b, u64 x, u64 y, u32 len) {
   return true;
 }
 
+// the workflows wf_pass_wave_kernel takes (a wavefront per workflow): at most 64 events and 63 batches
+// (their 64 offsets one load), no previous reset points to intern; wf_pass_kernel takes the rest
+__device__ __forceinline__ bool wave_shaped(u32 n, u32 nr, u32 n_batches) {
+  return n <= 64 && nr == 0 && n_batches < 64;
+}
+
+// the live-set map of an event type and its direction (flatten.live_set_bounds)
+__device__ __forceinline__ int bound_map_of(u32 t, int& dir) {
+  dir = 0;
+  switch (t) {
+    case CRR_EV_ACTIVITY_TASK_SCHEDULED: dir = 1; return 0;
+    case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED: case CRR_EV_ACTIVITY_TASK_TIMED_OUT:
+    case CRR_EV_ACTIVITY_TASK_CANCELED: dir = -1; return 0;
+    case CRR_EV_TIMER_STARTED: dir = 1; return 1;
+    case CRR_EV_TIMER_FIRED: case CRR_EV_TIMER_CANCELED: dir = -1; return 1;
+    case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED: dir = 1; return 2;
+    case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
+    case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED:
+    case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT: case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED:
+      dir = -1; return 2;
+    case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED: dir = 1; return 3;
+    case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:
+      dir = -1; return 3;
+    case CRR_EV_SIGNAL_EXTERNAL_INITIATED: dir = 1; return 4;
+    case CRR_EV_SIGNAL_EXTERNAL_FAILED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED: dir = -1; return 4;
+    default: return -1;
+  }
+}
+
+// the per-workflow tail both passes share: tier class, counters, info words, sort key, token bytes
+struct WfSummary {
+  i32 n, empty_at, n_act, n_timer, n_child, n_rc, n_sig, vh, rp_cap, tasks, n_started;
+  i32 bound[kMaps];
+  bool compact_ok;
+};
+// tier_classes; returns the counter slots this workflow adds one to (bit k: counter k)
+__device__ __forceinline__ u32 wf_finish(const crr_blob_batch& in, const Plan& P, u32 w, const crr_blob_wf& src,
+                                         const WfSummary& S, i32* info /* [kWfInfo] */, u64& sort_key, u64& arena) {
+  const i32* bound = S.bound;
+  int tier = kWide;
+  for (int k = kWide - 1; k >= 0; --k) {
+    bool fit = true;
+    for (int m = 0; m < kMaps; ++m) fit = fit && bound[m] <= kTierSlots[k][m];
+    if (k >= 2) fit = fit && S.compact_ok;
+    if (fit) tier = k;
+  }
+  if (tier == 1 && S.compact_ok) tier = 2;
+  const u32 n = (u32)S.n;
+  const bool is_long = (i32)n > kLongHistory || tier == kWide;
+  bool big = false;
+  for (int m = 0; m < kMaps; ++m) big = big || bound[m] > kWaveBigCap;
+  u32 cnt = 0;
+  if (is_long && !big) {
+    bool small = true;
+    for (int m = 0; m < kMaps; ++m) small = small && bound[m] <= kWaveSmallTier[m];
+    if (!small) cnt |= 1u << C_SMALL_TAIL_BAD;
+  }
+  if (is_long) { if (big) cnt |= 1u << C_N_BIG; }
+  else cnt |= (1u << C_N_LANE) | (1u << (C_TIER0 + tier));
+  if (src.flags & CRR_WF_FLAG_NEW_RUN) cnt |= 1u << C_NEW_RUN;
+  info[WI_COUNT] = (i32)n; info[WI_EMPTY_AT] = S.empty_at;
+  info[WI_ACT] = S.n_act; info[WI_TIMER] = S.n_timer; info[WI_CHILD] = S.n_child;
+  info[WI_RC] = S.n_rc; info[WI_SIG] = S.n_sig; info[WI_VH] = S.vh; info[WI_RP] = S.rp_cap;
+  // + RefreshTasks' search-attributes task (CRR_WF_FLAG_REFRESH_TASKS: its other tasks fit the replay's bound)
+  info[WI_TASKS] = S.tasks + ((src.flags & CRR_WF_FLAG_REFRESH_TASKS) ? 1 : 0); info[WI_STARTED] = S.n_started;
+  info[WI_TIER] = tier; info[WI_LONG] = is_long; info[WI_BIG] = big;
+  // device order (flatten.interleave): lanes by (tier, -length, index), then the long tail by (big, -length, index)
+  const u64 cls = is_long ? (u64)big : (u64)tier;
+  const u64 len = n < 0x1FFFFFFFu ? n : 0x1FFFFFFFu;
+  sort_key = ((u64)is_long << 63) | (cls << 60) | ((0x1FFFFFFFull - len) << 31) | (u64)w;
+  // the branch tokens' bytes (NewHistoryBranchTokenByBranchID) + the final token
+  arena = 24ull + src.run_id_len + src.branch_id_len + (src.final_token_len != 0xFFFFFFFFu ? src.final_token_len : 0);
+  return cnt;
+}
+
+__device__ __forceinline__ i32 wave_incl_sum(i32 v, u32 lane) {
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const i32 o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+__device__ __forceinline__ i32 wave_max(i32 v) {
+  for (int d = 32; d >= 1; d >>= 1) { const i32 o = __shfl_xor(v, d); v = o > v ? o : v; }
+  return v;
+}
+__device__ __forceinline__ u32 bcast_u32(u32 v, int j) { return (u32)__builtin_amdgcn_readlane((int)v, j); }
+__device__ __forceinline__ u64 bcast_u64(u64 v, int j) {
+  return ((u64)bcast_u32((u32)(v >> 32), j) << 32) | bcast_u32((u32)v, j);
+}
+
+// 5 (wave form): a wavefront per workflow, a lane per event (and per batch).  The same results as
+// wf_pass_kernel's serial walk, by wave-wide prefix counts and pairwise compares:
+//   key ids     a key's first occurrence (the lowest earlier lane with the same bytes) and its rank among
+//               the first occurrences: WfFlattener::key_of's first-seen numbering
+//   VH items    lanes whose version exceeds every earlier one
+//   ordinals    prefix counts of Started / ActivityTaskScheduled lanes
+//   bounds      each map's +1 / -1 (a delete valid as live_set_bounds decides: its key / ID inserted
+//               anywhere in the workflow, ref < ID, the first delete of that ref), inclusive prefix sums,
+//               their maximum
+// Workflows are taken grid-stride; a wavefront's counter increments are summed in registers and added
+// once at the end.
+constexpr u32 kWfWaveBlock = 256;
+__global__ __launch_bounds__(kWfWaveBlock) void wf_pass_wave_kernel(crr_blob_batch in, Plan P) {
+  if (!plan_ok(P)) return;
+  const u32 lane = threadIdx.x & 63;
+  const u32 wave0 = blockIdx.x * (kWfWaveBlock / 64) + threadIdx.x / 64;
+  const u32 n_waves = gridDim.x * (kWfWaveBlock / 64);
+  const u64 NB = P.n_blobs + 1;
+  const u64 lt = (1ull << lane) - 1;
+  const u64 nw = in.n_wf;
+  u32 my_count = 0;   // lane k: counter k's increments
+  // the next workflow's record and batch offsets are fetched while this one is worked on
+  crr_blob_wf nsrc;
+  nsrc.blob_begin = 0; nsrc.blob_count = 64;
+  u64 nob = 0, nrv = 0;   // lane k: the offset of batch k (events), of batches 0 and count (reset points)
+  auto fetch_src = [&](u32 w) {
+    if (w < in.n_wf) nsrc = in.wf[w];
+  };
+  auto fetch_off = [&](u32 w) {
+    if (w >= in.n_wf) return;
+    const u32 bb = nsrc.blob_begin, c = nsrc.blob_count;
+    nob = lane <= c && c < 64 ? P.off[0 * NB + bb + lane] : 0;
+    nrv = (lane == 0 || lane == c) && c < 64 ? P.off[1 * NB + bb + lane] : 0;
+  };
+  fetch_src(wave0);
+  fetch_off(wave0);
+  for (u32 w = wave0; w < in.n_wf; w += n_waves) {
+    const crr_blob_wf src = nsrc;
+    const u64 ob = nob, rv = nrv;
+    fetch_src(w + n_waves);
+    const u32 nbat = src.blob_count;
+    if (nbat >= 64) { fetch_off(w + n_waves); continue; }   // wf_pass_kernel's
+    const u64 e0 = (u64)__shfl((long long)ob, 0), e1 = (u64)__shfl((long long)ob, (int)nbat);
+    const u64 r0 = (u64)__shfl((long long)rv, 0), r1 = (u64)__shfl((long long)rv, (int)nbat);
+    const u32 n = (u32)(e1 - e0);
+    if (!wave_shaped(n, (u32)(r1 - r0), nbat)) { fetch_off(w + n_waves); continue; }
+    // -- batches: the first empty one, two tasks per non-empty one --
+    const bool has_b = lane < nbat;
+    const u64 bx0 = ob, bx1 = (u64)__shfl_down((long long)ob, 1);
+    // -- events --
+    const bool ev = lane < n;
+    const u64 x = e0 + lane;
+    const u32 t = ev ? (u32)(P.etype[x] & CRR_ETYPE_MASK) : 0xFFu;
+    const i64 v = ev ? P.ver[x] : INT64_MIN;
+    const i64 id = ev ? P.id[x] : 0;
+    const i64 ref = ev ? P.ref[x] : 0;
+    const bool keyed = ev && t < CRR_EV_TYPE_COUNT && keyed_type((i32)t);
+    // every event's KeyRef slot with the columns (one round trip; a non-keyed event's is ignored)
+    KeyRef kr;
+    kr.off = 0; kr.len = 0; kr.hash = 0; kr.head[0] = 0; kr.head[1] = 0;
+    if (ev) kr = P.keys[x];
+    if (!keyed) { kr.len = 0; kr.hash = 0; }
+    const bool started = t == CRR_EV_WORKFLOW_EXECUTION_STARTED;
+    i32 pc = -1;
+    if (started) pc = P.start[x].prev_reset_count;
+    fetch_off(w + n_waves);
+
+    const u64 empty_mask = __ballot(has_b && bx0 == bx1);
+    const i32 empty_at = src.blob_count == 0 ? 0
+                         : empty_mask ? (i32)((u64)__shfl((long long)bx0, __builtin_ctzll(empty_mask)) - e0) : -1;
+    const i32 tasks = 2 * __popcll(__ballot(has_b && bx1 > bx0)) +
+                      __shfl(wave_incl_sum(t < CRR_EV_TYPE_COUNT ? (i32)kTasksPerEvent[t] : 0, lane), 63);
+    // VH items: a version above every earlier one (the first event's always)
+    i64 run_max = v;
+    for (u32 d = 1; d < 64; d <<= 1) {
+      const i64 o = __shfl_up(run_max, d);
+      if (lane >= d && o > run_max) run_max = o;
+    }
+    const i64 before = __shfl_up(run_max, 1);
+    const i32 vh = __popcll(__ballot(ev && (lane == 0 || v > before)));
+    // ordinals and counts
+    const u64 m_started = __ballot(started), m_act = __ballot(t == CRR_EV_ACTIVITY_TASK_SCHEDULED);
+    const u64 m_dtc = __ballot(t == CRR_EV_DECISION_TASK_COMPLETED);
+    const i32 n_started = __popcll(m_started), n_act = __popcll(m_act), n_dtc = __popcll(m_dtc);
+    const i32 n_timer = __popcll(__ballot(t == CRR_EV_TIMER_STARTED));
+    const i32 n_child = __popcll(__ballot(t == CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED));
+    const i32 n_rc = __popcll(__ballot(t == CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED));
+    const i32 n_sig = __popcll(__ballot(t == CRR_EV_SIGNAL_EXTERNAL_INITIATED));
+    const i32 pc_max = wave_max(pc), max_prev = pc_max > 0 ? pc_max : 0;   // 0 here: no points to intern
+    if (started) {
+      if (pc >= 0) P.start[x].prev_reset_key_off += (u32)r0;   // the blob-local index made global (all 0 here)
+      P.aux[x] = __popcll(m_started & lt);
+    }
+    if (t == CRR_EV_ACTIVITY_TASK_SCHEDULED) P.aux[x] = __popcll(m_act & lt);
+
+    // -- interning: the first occurrence of each key's bytes --
+    const bool named = keyed && kr.len != 0;
+    const u64 m_named = __ballot(named);
+    i32 first = named ? -1 : (i32)lane;
+    u32 from = 0;
+    for (;;) {
+      const bool pending = first < 0;
+      if (!__ballot(pending)) break;
+      i32 c = -1;
+      for (u64 mm = m_named; mm; mm &= mm - 1) {
+        const int j = __builtin_ctzll(mm);
+        const u32 hj = bcast_u32(kr.hash, j), lj = bcast_u32(kr.len, j);
+        if (pending && c < 0 && (u32)j >= from && (u32)j < lane && hj == kr.hash && lj == kr.len) c = j;
+      }
+      const int cs = c < 0 ? (int)lane : c;
+      const u64 c_off = (u64)__shfl((long long)kr.off, cs);
+      const u64 c_h0 = (u64)__shfl((long long)kr.head[0], cs), c_h1 = (u64)__shfl((long long)kr.head[1], cs);
+      if (pending) {
+        if (c < 0) first = (i32)lane;
+        else if (kr.len <= 16 ? (c_h0 == kr.head[0] && c_h1 == kr.head[1]) : same_bytes(in.bytes, kr.off, c_off, kr.len))
+          first = c;
+        else from = (u32)c + 1;
+      }
+    }
+    const u64 m_first = __ballot(named && first == (i32)lane);
+    const u32 key = named ? 1u + (u32)__popcll(m_first & ((1ull << first) - 1)) : 0u;
+    if (keyed) P.key[x] = key;
+
+    // -- live-set bounds --
+    int dir = 0;
+    const int m = ev ? bound_map_of(t, dir) : -1;
+    bool compact_ok = n <= (u32)kCompactMaxEvents && !__ballot(ev && id > (i64)0xFFFFFFFFll);
+    const bool dtc_named = t == CRR_EV_DECISION_TASK_COMPLETED && key != 0;
+    const u64 ins_val = m == 1 ? (u64)key : (u64)id;        // an insert's value
+    const u64 del_val = m == 1 ? (u64)key : (u64)ref;       // what a delete looks up
+    bool inserted = false, deleted_before = false, rp_dup = false;
+    for (u64 mm = __ballot(m >= 0 || dtc_named); mm; mm &= mm - 1) {
+      const int j = __builtin_ctzll(mm);
+      const int mj = (int)bcast_u32((u32)m, j), dj = (int)bcast_u32((u32)dir, j);
+      const u64 ij = bcast_u64(ins_val, j), rj = bcast_u64(del_val, j);
+      const u32 kj = bcast_u32(key, j), tj = bcast_u32(t, j);
+      if (dir < 0 && mj == m) {
+        if (dj > 0 && ij == del_val) inserted = true;
+        if (m != 1 && dj < 0 && (u32)j < lane && rj == del_val) deleted_before = true;
+      }
+      if (dtc_named && tj == CRR_EV_DECISION_TASK_COMPLETED && (u32)j < lane && kj == key) rp_dup = true;
+    }
+    const bool valid = dir > 0 || (dir < 0 && (m == 1 ? inserted : inserted && ref < id && !deleted_before));
+    WfSummary S;
+    for (int k = 0; k < 5; ++k) {
+      const i32 run = wave_incl_sum(m == k && valid ? dir : 0, lane);
+      const i32 hi = wave_max(run);
+      S.bound[k] = hi > 0 ? hi : 0;
+    }
+    S.bound[5] = __popcll(__ballot(dtc_named && !rp_dup)) + max_prev;
+    S.n = (i32)n; S.empty_at = empty_at; S.n_act = n_act; S.n_timer = n_timer; S.n_child = n_child; S.n_rc = n_rc;
+    S.n_sig = n_sig; S.vh = vh; S.rp_cap = max_prev * (n_started > 1 ? n_started : 1) + n_dtc; S.tasks = tasks;
+    S.n_started = n_started; S.compact_ok = compact_ok;
+    i32 info[kWfInfo];
+    u64 sort_key, arena;
+    const u32 cnt = wf_finish(in, P, w, src, S, info, sort_key, arena);
+    my_count += (cnt >> lane) & 1u;
+    i32 mine = 0;
+#pragma unroll
+    for (int k = 0; k < kWfInfo; ++k) mine = lane == (u32)k ? info[k] : mine;
+    if (lane < kWfInfo) P.wf_info[lane * nw + w] = mine;
+    if (lane == 0) { P.sort_in[w] = sort_key; P.arena_off[w] = arena; }
+  }
+  if (lane < 16 && my_count) atomicAdd(P.counters + lane, my_count);
+}
+
 __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= in.n_wf || !plan_ok(P)) return;
@@ -1270,6 +1640,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u64 r0 = P.off[1 * NB + bb], r1 = P.off[1 * NB + be];
   const u32 n = (u32)(e1 - e0);
   const u32 nr = (u32)(r1 - r0);
+  if (wave_shaped(n, nr, src.blob_count)) return;   // wf_pass_wave_kernel's
   // this workflow's scratch table: 4 * (events + reset points) + 64 u64 words from its own base
   const u64 tbase = 4 * e0 + 4 * r0 + 64ull * w;
   u64* tab = P.table + tbase;
@@ -1441,41 +1812,18 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
     }
     bound[5] = rp + (max_prev > 0 ? max_prev : 0);
   }
-  // tier_classes
-  int tier = kWide;
-  for (int k = kWide - 1; k >= 0; --k) {
-    bool fit = true;
-    for (int m = 0; m < kMaps; ++m) fit = fit && bound[m] <= kTierSlots[k][m];
-    if (k >= 2) fit = fit && compact_ok;
-    if (fit) tier = k;
-  }
-  if (tier == 1 && compact_ok) tier = 2;
-  const bool is_long = (i32)n > kLongHistory || tier == kWide;
-  bool big = false;
-  for (int m = 0; m < kMaps; ++m) big = big || bound[m] > kWaveBigCap;
-  if (is_long && !big) {
-    bool small = true;
-    for (int m = 0; m < kMaps; ++m) small = small && bound[m] <= kWaveSmallTier[m];
-    if (!small) atomicAdd(P.counters + C_SMALL_TAIL_BAD, 1u);
-  }
-  if (is_long) { if (big) atomicAdd(P.counters + C_N_BIG, 1u); }
-  else { atomicAdd(P.counters + C_N_LANE, 1u); atomicAdd(P.counters + C_TIER0 + tier, 1u); }
-  if (src.flags & CRR_WF_FLAG_NEW_RUN) atomicAdd(P.counters + C_NEW_RUN, 1u);
-
-  i32* wi = P.wf_info;
-  const u64 nw = in.n_wf;
-  wi[WI_COUNT * nw + w] = (i32)n; wi[WI_EMPTY_AT * nw + w] = empty_at;
-  wi[WI_ACT * nw + w] = n_act; wi[WI_TIMER * nw + w] = n_timer; wi[WI_CHILD * nw + w] = n_child;
-  wi[WI_RC * nw + w] = n_rc; wi[WI_SIG * nw + w] = n_sig; wi[WI_VH * nw + w] = vh; wi[WI_RP * nw + w] = rp_cap;
-  // + RefreshTasks' search-attributes task (CRR_WF_FLAG_REFRESH_TASKS: its other tasks fit the replay's bound)
-  wi[WI_TASKS * nw + w] = tasks + ((src.flags & CRR_WF_FLAG_REFRESH_TASKS) ? 1 : 0); wi[WI_STARTED * nw + w] = n_started; wi[WI_TIER * nw + w] = tier;
-  wi[WI_LONG * nw + w] = is_long; wi[WI_BIG * nw + w] = big;
-  // device order (flatten.interleave): lanes by (tier, -length, index), then the long tail by (big, -length, index)
-  const u64 cls = is_long ? (u64)big : (u64)tier;
-  const u64 len = n < 0x1FFFFFFFu ? n : 0x1FFFFFFFu;
-  P.sort_in[w] = ((u64)is_long << 63) | (cls << 60) | ((0x1FFFFFFFull - len) << 31) | (u64)w;
-  // the branch tokens' bytes (NewHistoryBranchTokenByBranchID) + the final token
-  P.arena_off[w] = 24ull + src.run_id_len + src.branch_id_len + (src.final_token_len != 0xFFFFFFFFu ? src.final_token_len : 0);
+  WfSummary S;
+  for (int m = 0; m < kMaps; ++m) S.bound[m] = bound[m];
+  S.n = (i32)n; S.empty_at = empty_at; S.n_act = n_act; S.n_timer = n_timer; S.n_child = n_child; S.n_rc = n_rc;
+  S.n_sig = n_sig; S.vh = vh; S.rp_cap = rp_cap; S.tasks = tasks; S.n_started = n_started; S.compact_ok = compact_ok;
+  i32 info[kWfInfo];
+  u64 sort_key, arena;
+  const u32 cnt = wf_finish(in, P, w, src, S, info, sort_key, arena);
+  for (int k = 0; k < 16; ++k)
+    if ((cnt >> k) & 1u) atomicAdd(P.counters + k, 1u);
+  for (int k = 0; k < kWfInfo; ++k) P.wf_info[k * (u64)in.n_wf + w] = info[k];
+  P.sort_in[w] = sort_key;
+  P.arena_off[w] = arena;
 }
 
 // ---- 7: geometry -------------------------------------------------------------------------------------------
@@ -1576,9 +1924,9 @@ struct Dst {
 };
 
 // one event (or pad) slot; side records follow their events (_interleave_side)
-__device__ __forceinline__ void put_slot(const crr_blob_batch& in, const Plan& P, const Dst& D, u64 dst, u32 p,
-                                         u32 w, i64 k, bool real, u64 side_act_base, u64 side_start_base, u64 side_stride,
-                                         u32 lane) {
+// x0: the workflow's first canonical slot (P.off at its first blob)
+__device__ __forceinline__ void put_slot(const Plan& P, const Dst& D, u64 dst, u64 x0, i64 k, bool real,
+                                         u64 side_act_base, u64 side_start_base, u64 side_stride, u32 lane) {
   u8* et = const_cast<u8*>(D.ev.etype);
   i64* id = const_cast<i64*>(D.ev.event_id);
   i64* ver = const_cast<i64*>(D.ev.version);
@@ -1592,8 +1940,7 @@ __device__ __forceinline__ void put_slot(const crr_blob_batch& in, const Plan& P
     id[dst] = 0; ver[dst] = 0; ts[dst] = 0; task[dst] = 0; ref[dst] = 0; key[dst] = 0; aux[dst] = 0;
     return;
   }
-  const u64 NB = P.n_blobs + 1;
-  const u64 x = P.off[0 * NB + in.wf[w].blob_begin] + (u64)k;
+  const u64 x = x0 + (u64)k;
   const u8 e = P.etype[x];
   const u32 t = e & CRR_ETYPE_MASK;
   i32 a = P.aux[x];
@@ -1624,8 +1971,9 @@ __global__ void layout_groups_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lan
   const bool have = p < n_lane;
   const u32 w = have ? P.perm[p] : 0;
   const i64 cnt = have ? P.wf_info[WI_COUNT * (u64)P.n_wf + w] : 0;
+  const u64 x0 = have ? P.off[in.wf[w].blob_begin] : 0;
   for (u64 k = threadIdx.x / 64; k < glen; k += blockDim.x / 64)
-    put_slot(in, P, D, base + k * 64 + lane, p, w, (i64)k, have && (i64)k < cnt, abase, sbase, 64, lane);
+    put_slot(P, D, base + k * 64 + lane, x0, (i64)k, have && (i64)k < cnt, abase, sbase, 64, lane);
 }
 
 __global__ void layout_tail_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u32 n_groups, u32 n_tail) {
@@ -1640,7 +1988,8 @@ __global__ void layout_tail_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane,
   const u64 abase = lane_act + P.tpre[(u64)GV_ACT_SIDE * (n_tail + 1) + i];
   const u64 sbase = lane_start + P.tpre[(u64)GV_START_SIDE * (n_tail + 1) + i];
   const i64 cnt = P.wf_info[WI_COUNT * (u64)P.n_wf + w];
-  for (i64 k = threadIdx.x; k < cnt; k += blockDim.x) put_slot(in, P, D, base + k, p, w, k, true, abase, sbase, 1, 0);
+  const u64 x0 = P.off[in.wf[w].blob_begin];
+  for (i64 k = threadIdx.x; k < cnt; k += blockDim.x) put_slot(P, D, base + k, x0, k, true, abase, sbase, 1, 0);
 }
 
 // descriptors (device order) and branch tokens (canonical order)
@@ -1761,6 +2110,7 @@ Carved carve(void* scratch, uint32_t n_blobs, uint32_t n_wf, uint64_t max_events
   P.reset_ids = (u32*)take(4 * E);
   // per-workflow hash tables: a workflow of n events and r reset points uses <= 4n + 4r + 64 words
   P.table = (u64*)take(8 * (8 * E + 64 * NW));
+  P.dom_refs = reinterpret_cast<KeyRef*>(P.table);   // 32 * E <= 64 * E bytes
   P.wf_info = (i32*)take(4 * kWfInfo * NW);
   P.sort_in = (u64*)take(8 * NW);
   P.sort_out = (u64*)take(8 * NW);
@@ -1834,49 +2184,50 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   }
   P.dom_cap = dom_cap;
   hipError_t e;
-  if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
-  if ((e = hipMemsetAsync(P.counters, 0, 4 * 16, s)) != hipSuccess) return (int)e;
   if (dom_cap) {
     if ((e = hipMemsetAsync(P.dom_table, 0, 4 * (size_t)dom_cap, s)) != hipSuccess) return (int)e;
     hipLaunchKernelGGL(domains_build_kernel, dim3((in->n_domains + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in,
                        P.dom_table, dom_cap);
   }
   const unsigned gb = (nb + kBlock - 1) / kBlock, gw = (nw + kBlock - 1) / kBlock;
-  // A: event counts, the decode, reset points, the per-workflow pass, the device order
-  if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
+  // A: event counts, the decode, reset points, the per-workflow pass, the device order.  A header count
+  // that was wrong (hand-made blobs) shows in `flags` at the readback below (every pass after the decode
+  // skips the plan meanwhile): then all of A again, the counts from walking every blob.
+  u32 n_lane = 0, flags = 0;
+  u64 err = 0, n_events = 0, n_resets = 0;
   for (int full = 0; full < 2; ++full) {
+    if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemsetAsync(P.counters, 0, 4 * 16, s)) != hipSuccess) return (int)e;
+    if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
     if (nb) hipLaunchKernelGGL(blob_head_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P, full);
     multi_scan<u32>(P.cnt, nb, nb, 1, P.tile, P.off, NB, s);
-    if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
+    if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, *in, P);
     if (nb) hipLaunchKernelGGL(blob_decode_general_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
-    if (full) break;
-    // a header count that was wrong (hand-made blobs): count by walking every blob, then decode again
-    u32 flags = 0;
+    if (nb && dom_cap) hipLaunchKernelGGL(domain_resolve_kernel, dim3(2048), dim3(kBlock), 0, s, *in, P);
+    multi_scan<u32>(P.cnt + nb, nb, nb, 1, P.tile, P.off + NB, NB, s);   // previous reset points per blob
+    if (nb) hipLaunchKernelGGL(reset_refs_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
+    if (nw) {
+      const u32 blocks = (nw + kWfWaveBlock / 64 - 1) / (kWfWaveBlock / 64);
+      hipLaunchKernelGGL(wf_pass_wave_kernel, dim3(blocks < 2048 ? blocks : 2048), dim3(kWfWaveBlock), 0, s, *in, P);
+      hipLaunchKernelGGL(wf_pass_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P);
+    }
+    multi_scan<u64>(P.arena_off, nw, nw, 1, P.tile, P.arena_off, (u64)nw + 1, s);
+    if (nw) {
+      size_t tmp = P.sort_tmp_bytes;
+      if ((e = hipcub::DeviceRadixSort::SortKeys(P.sort_tmp, tmp, P.sort_in, P.sort_out, (int)nw, 0, 64, s)) != hipSuccess)
+        return (int)e;
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    // the lane / tail split sizes the geometry launches
+    if ((e = hipMemcpyAsync(&n_lane, P.counters + C_N_LANE, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemcpyAsync(&err, P.err, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemcpyAsync(&n_events, P.off + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
+    if ((e = hipMemcpyAsync(&n_resets, P.off + NB + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
     if ((e = hipMemcpyAsync(&flags, P.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
     if (!flags) break;
-    if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
-    if ((e = hipMemsetAsync(P.err, 0xff, 8, s)) != hipSuccess) return (int)e;
   }
-  multi_scan<u32>(P.cnt + nb, nb, nb, 1, P.tile, P.off + NB, NB, s);   // previous reset points per blob
-  if (nb) hipLaunchKernelGGL(reset_refs_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
-  if (nw) hipLaunchKernelGGL(wf_pass_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P);
-  multi_scan<u64>(P.arena_off, nw, nw, 1, P.tile, P.arena_off, (u64)nw + 1, s);
-  if (nw) {
-    size_t tmp = P.sort_tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortKeys(P.sort_tmp, tmp, P.sort_in, P.sort_out, (int)nw, 0, 64, s)) != hipSuccess)
-      return (int)e;
-  }
-  if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-  // the lane / tail split sizes the geometry launches
-  u32 n_lane = 0;
-  u64 err = 0, n_events = 0, n_resets = 0;
-  if ((e = hipMemcpyAsync(&n_lane, P.counters + C_N_LANE, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
-  if ((e = hipMemcpyAsync(&err, P.err, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
-  if ((e = hipMemcpyAsync(&n_events, P.off + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
-  if ((e = hipMemcpyAsync(&n_resets, P.off + NB + nb, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return (int)e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
   const bool failed = err != ~0ull || n_lane > nw || n_events > max_events || n_resets > max_events;
   const u32 n_groups = failed ? 0 : (n_lane + 63) / 64, n_tail = failed ? 0 : nw - n_lane;
   // B: geometry and the summary (after a failed decode only the error and the counts)
@@ -1919,7 +2270,8 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
   // side records no event references stay zero, like flatten's zero-filled arrays
   if ((e = hipMemsetAsync(D.act, 0, S->n_act_side * sizeof(crr_activity_side), s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(D.start, 0, S->n_start_side * sizeof(crr_start_side), s)) != hipSuccess) return (int)e;
-  if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups);
+  // 16 wavefronts per group of 64 lanes: a wavefront writes one slot row of the group per step
+  if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(1024), 0, s, *in, P, D, n_lane, n_groups);
   if (n_tail) hipLaunchKernelGGL(layout_tail_kernel, dim3(n_tail), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups, n_tail);
   if (nw) hipLaunchKernelGGL(layout_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P, D, n_lane,
                              n_groups, n_tail);

@@ -35,6 +35,7 @@ def main():
     p.add_argument("root")
     p.add_argument("--events", default=None, help="json: kernel name -> events per launch")
     p.add_argument("--min-waves", type=float, default=64)
+    p.add_argument("--kernels", default="replay,widen,compact", help="comma-separated name fragments to report")
     a = p.parse_args()
     data = load(a.root)
     ev = json.load(open(a.events)) if a.events else {}
@@ -44,7 +45,7 @@ def main():
     print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
     for k, c in sorted(data.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
         waves = c.get("SQ_WAVES", 0)
-        if waves < a.min_waves or "replay" not in k and "widen" not in k and "compact" not in k:
+        if waves < a.min_waves or not any(f in k for f in a.kernels.split(",")):
             continue
         w = max(waves, 1)
         wait = c.get("SQ_WAIT_ANY", 0) / max(c.get("SQ_WAVE_CYCLES", 1), 1)

@@ -153,8 +153,9 @@ __device__ __attribute__((noinline)) Cursor skip_nested(const u8* b, u64 p, u64 
 // state (reader, event) in scratch memory.
 constexpr int kDeferGeneral = -90;
 constexpr u32 kDeferMark = 0xFFFFFFFFu;   // cnt[1][blob] of a deferred blob, until the general pass
-// L: the window loads come from an LDS copy of the bytes [base, ...) (blob_decode_kernel stages each
-// wavefront's blobs there with coalesced loads), positions stay offsets into `bytes`.
+// L: reads come from an LDS copy of the bytes [base, ...) (blob_decode_kernel stages each wavefront's
+// blobs there with coalesced loads), 8 unaligned bytes per ds_read_b64 and no register window; positions
+// stay offsets into `bytes`.
 typedef const u8 __attribute__((address_space(3))) lds_u8;
 typedef const v4u __attribute__((address_space(3))) lds_v4u;
 template <bool G, bool L = false>
@@ -185,6 +186,15 @@ struct RdT {
   }
   // bytes q .. q+7 in memory order (little-endian u64)
   __device__ __forceinline__ u64 peek8(u64 q) {
+    if constexpr (L) {   // LDS serves unaligned 8-byte reads (ds_read_b64): no window to carry
+      u64 v;
+      __builtin_memcpy(&v, (const void*)(lb + (u32)(q - base)), 8);
+      return v;
+    } else if constexpr (!G) {   // the fast pass's rare blob larger than the LDS window: unaligned loads
+      u64 v;
+      __builtin_memcpy(&v, b + q, 8);
+      return v;
+    }
     const u64 a = q & ~15ull;
     if (a != wb) {
       if (a == wb + 16) {
@@ -1306,32 +1316,39 @@ __global__ void scan_tile_sums_kernel(u64* tile_sums, u32 n_tiles) {
     __syncthreads();
   }
 }
-// out[k][j] = exclusive prefix of in[k][0..j), j <= m (out has m + 1 entries per array)
+// out[k][j] = exclusive prefix of in[k][0..j), j <= m (out has m + 1 entries per array).  A thread per 4
+// consecutive values: its sum, a wave scan of the sums, the waves' totals through LDS.
 template <class T>
-__global__ void scan_apply_kernel(const T* in, u64 in_stride, u32 m, const u64* tile_sums, u32 n_tiles, u64* out,
-                                  u64 out_stride) {
-  __shared__ u64 buf[kTile];
+__global__ __launch_bounds__(kBlock) void scan_apply_kernel(const T* in, u64 in_stride, u32 m, const u64* tile_sums,
+                                                            u32 n_tiles, u64* out, u64 out_stride) {
+  constexpr int kPer = kTile / kBlock;
+  __shared__ u64 wsum[kBlock / 64];
   const u32 tile = blockIdx.x, k = blockIdx.y;
-  for (u32 i = threadIdx.x; i < kTile; i += kBlock) {
-    const u64 j = (u64)tile * kTile + i;
-    buf[i] = j < m ? (u64)in[k * in_stride + j] : 0;
+  const u32 tid = threadIdx.x, lane = tid & 63, wv = tid / 64;
+  const u64 j0 = (u64)tile * kTile + (u64)tid * kPer;
+  u64 v[kPer];
+  u64 loc = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    v[q] = j0 + q < m ? (u64)in[k * in_stride + j0 + q] : 0;
+    loc += v[q];
   }
+  u64 inc = loc;
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const u64 o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {   // serial over the tile: 1024 adds, cheap next to the walks
-    u64 s = tile_sums[(u64)k * n_tiles + tile];
-    for (int i = 0; i < kTile; ++i) {
-      const u64 v = buf[i];
-      buf[i] = s;
-      s += v;
-    }
-    const u64 j_end = (u64)tile * kTile + kTile;
-    if (j_end >= m && (u64)tile * kTile <= m) out[k * out_stride + m] = s;  // the total
+  u64 s = tile_sums[(u64)k * n_tiles + tile] + inc - loc;
+  for (u32 w = 0; w < wv; ++w) s += wsum[w];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (j0 + q < m) out[k * out_stride + j0 + q] = s;
+    s += v[q];
   }
-  __syncthreads();
-  for (u32 i = threadIdx.x; i < kTile; i += kBlock) {
-    const u64 j = (u64)tile * kTile + i;
-    if (j < m) out[k * out_stride + j] = buf[i];
-  }
+  // the total, by the thread holding value m - 1 (values past m are 0); m == 0: tile 0's first thread
+  if ((m > 0 && j0 <= m - 1 && m - 1 < j0 + kPer) || (m == 0 && tile == 0 && tid == 0)) out[k * out_stride + m] = s;
 }
 
 template <class T>
@@ -1594,21 +1611,32 @@ __global__ __launch_bounds__(kWfWaveBlock) void wf_pass_wave_kernel(crr_blob_bat
     const bool dtc_named = t == CRR_EV_DECISION_TASK_COMPLETED && key != 0;
     const u64 ins_val = m == 1 ? (u64)key : (u64)id;        // an insert's value
     const u64 del_val = m == 1 ? (u64)key : (u64)ref;       // what a delete looks up
+    // deletes: an insert of the same map and value anywhere; an earlier delete of the same map and ref
     bool inserted = false, deleted_before = false, rp_dup = false;
-    for (u64 mm = __ballot(m >= 0 || dtc_named); mm; mm &= mm - 1) {
-      const int j = __builtin_ctzll(mm);
-      const int mj = (int)bcast_u32((u32)m, j), dj = (int)bcast_u32((u32)dir, j);
-      const u64 ij = bcast_u64(ins_val, j), rj = bcast_u64(del_val, j);
-      const u32 kj = bcast_u32(key, j), tj = bcast_u32(t, j);
-      if (dir < 0 && mj == m) {
-        if (dj > 0 && ij == del_val) inserted = true;
-        if (m != 1 && dj < 0 && (u32)j < lane && rj == del_val) deleted_before = true;
+    if (__ballot(dir < 0)) {
+      for (u64 mm = __ballot(dir > 0); mm; mm &= mm - 1) {
+        const int j = __builtin_ctzll(mm);
+        const int mj = (int)bcast_u32((u32)m, j);
+        const u64 ij = bcast_u64(ins_val, j);
+        if (dir < 0 && mj == m && ij == del_val) inserted = true;
       }
-      if (dtc_named && tj == CRR_EV_DECISION_TASK_COMPLETED && (u32)j < lane && kj == key) rp_dup = true;
+      for (u64 mm = __ballot(dir < 0 && m != 1); mm; mm &= mm - 1) {
+        const int j = __builtin_ctzll(mm);
+        const int mj = (int)bcast_u32((u32)m, j);
+        const u64 rj = bcast_u64(del_val, j);
+        if (dir < 0 && m != 1 && mj == m && (u32)j < lane && rj == del_val) deleted_before = true;
+      }
+    }
+    // reset points: a DecisionTaskCompleted key not seen before
+    for (u64 mm = __ballot(dtc_named); mm; mm &= mm - 1) {
+      const int j = __builtin_ctzll(mm);
+      if (dtc_named && (u32)j < lane && bcast_u32(key, j) == key) rp_dup = true;
     }
     const bool valid = dir > 0 || (dir < 0 && (m == 1 ? inserted : inserted && ref < id && !deleted_before));
     WfSummary S;
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 5; ++k) {   // a map without valid deletes: its insert count, no scan
+      const u64 dels = __ballot(m == k && valid && dir < 0);
+      if (!dels) { S.bound[k] = __popcll(__ballot(m == k && dir > 0)); continue; }
       const i32 run = wave_incl_sum(m == k && valid ? dir : 0, lane);
       const i32 hi = wave_max(run);
       S.bound[k] = hi > 0 ? hi : 0;
@@ -2047,15 +2075,25 @@ __global__ void layout_wf_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u
   u64 q = 0;
   auto put = [&](u32 v) { o[q++] = (u8)v; };
   auto be32 = [&](u32 v) { put(v >> 24); put(v >> 16); put(v >> 8); put(v); };
+  auto copy = [&](u64 off, u32 len) {   // 8 bytes per unaligned load / store, the tail bytewise
+    const u8* src = in.strings + off;
+    u32 i = 0;
+    for (; i + 8 <= len; i += 8) {
+      u64 v;
+      __builtin_memcpy(&v, src + i, 8);
+      __builtin_memcpy(o + q + i, &v, 8);
+    }
+    for (; i < len; ++i) o[q + i] = src[i];
+    q += len;
+  };
   put(0x59);
   put(11); put(0); put(10); be32(s.run_id_len);
-  for (u32 i = 0; i < s.run_id_len; ++i) put(in.strings[s.run_id_off + i]);
+  copy(s.run_id_off, s.run_id_len);
   put(11); put(0); put(20); be32(s.branch_id_len);
-  for (u32 i = 0; i < s.branch_id_len; ++i) put(in.strings[s.branch_id_off + i]);
+  copy(s.branch_id_off, s.branch_id_len);
   put(15); put(0); put(30); put(12); be32(0);
   put(0);
-  if (s.final_token_len != 0xFFFFFFFFu)
-    for (u32 i = 0; i < s.final_token_len; ++i) put(in.strings[s.final_token_off + i]);
+  if (s.final_token_len != 0xFFFFFFFFu) copy(s.final_token_off, s.final_token_len);
 }
 
 }  // namespace crr_ingest

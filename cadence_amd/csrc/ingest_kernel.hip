@@ -777,9 +777,34 @@ __device__ u32 count_events(Rd& r) {
 // the list header's: 0x59, 0x0F 0x00 0x0A, 0x0C, be32 n (bounded by the bytes after it: a corrupt
 // count must not size the scratch; the decode finds the truncation).  Any other shape, or FULL (the
 // recount after a header was wrong), walks the blob.
+// blob_head_quick_kernel takes the canonical headers with two unaligned loads and leaves kHeadWalk for
+// blob_head_kernel, which walks the rest (every blob when FULL).
+constexpr u32 kHeadWalk = 0xFFFFFFFFu;
+__global__ __launch_bounds__(kBlock) void blob_head_quick_kernel(crr_blob_batch in, Plan P) {
+  const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bi >= in.n_blobs) return;
+  const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
+  u32 n = 0;
+  if (b1 > b0) {
+    u64 h = 0;
+    u32 c = 0;
+    __builtin_memcpy(&h, in.bytes + b0, 8);   // readable: 32 bytes past the last blob
+    __builtin_memcpy(&c, in.bytes + b0 + 5, 4);
+    if ((h & 0xFFFFFFFFFFull) == 0x0C0A000F59ull && b1 - b0 >= 9) {
+      const i64 cn = (i32)__builtin_bswap32(c);
+      const i64 room = (i64)(b1 - b0 - 9);
+      n = cn < 0 ? 0u : (u32)(cn < room ? cn : room);
+    } else {
+      n = kHeadWalk;
+    }
+  }
+  P.cnt[bi] = n;
+}
+
 __global__ void blob_head_kernel(crr_blob_batch in, Plan P, int full) {
   const u32 bi = blockIdx.x * blockDim.x + threadIdx.x;
   if (bi >= in.n_blobs) return;
+  if (!full && P.cnt[bi] != kHeadWalk) return;   // blob_head_quick_kernel's
   const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
   u32 n = 0;
   if (b1 > b0) {
@@ -1170,7 +1195,10 @@ __device__ __forceinline__ void decode_blob_fast(const crr_blob_batch& in, const
 // LDS, so a walk's window loads are LDS round trips instead of a chain of dependent HBM reads.  A
 // window holding only some of the blobs serves those; the rest are staged again from the first one left.
 // A blob larger than the window alone is walked from HBM.
-constexpr u32 kStageBytes = 20 * 1024;   // 8 wavefronts per CU (the walk's registers allow 2 per SIMD)
+#ifndef CRR_INGEST_STAGE_KB
+#define CRR_INGEST_STAGE_KB 13
+#endif
+constexpr u32 kStageBytes = CRR_INGEST_STAGE_KB * 1024;   // 13 KB: 12 wavefronts per CU (measured best: 10 / 16 / 20 KB slower)
 __global__ __launch_bounds__(64) void blob_decode_kernel(crr_blob_batch in, Plan P) {
   __shared__ __attribute__((aligned(16))) u8 stage[kStageBytes];
   const u32 lane = threadIdx.x;
@@ -2238,6 +2266,7 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
     if ((e = hipMemsetAsync(P.flags, 0, 4, s)) != hipSuccess) return (int)e;
     if ((e = hipMemsetAsync(P.counters, 0, 4 * 16, s)) != hipSuccess) return (int)e;
     if (nw) hipLaunchKernelGGL(blob_wf_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P.blob_wf, P.err);
+    if (nb && !full) hipLaunchKernelGGL(blob_head_quick_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P);
     if (nb) hipLaunchKernelGGL(blob_head_kernel, dim3(gb), dim3(kBlock), 0, s, *in, P, full);
     multi_scan<u32>(P.cnt, nb, nb, 1, P.tile, P.off, NB, s);
     if (nb) hipLaunchKernelGGL(blob_decode_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, *in, P);

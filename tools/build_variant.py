@@ -3,7 +3,8 @@ one box (tools/prof_kernel.py / tools/prof_longtail.py --lib).
 
     python tools/build_variant.py NAME [--src=FILE] -DCRR_WAVE_FIELDS=0 [...]   ->  tools/variants/NAME.so
 
-Only replay_kernel.hip is recompiled; the other objects come from build/ (__graft_entry__.build()).
+Only replay_kernel.hip (or the --src= file, e.g. ingest_kernel.hip) is recompiled; the other objects come
+from build/ (__graft_entry__.build()).
 """
 import os
 import subprocess
@@ -27,7 +28,7 @@ def main():
     subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-I", os.path.join(ROOT, "cadence_amd", "csrc"), "-c", src, "-o", obj],
                    check=True)
     others = [os.path.join(ROOT, "build", os.path.basename(s) + ".o") for s in ge.HIP_SOURCES
-              if not s.endswith("replay_kernel.hip")]
+              if os.path.basename(s) != os.path.basename(src)]
     out = os.path.join(outdir, name + ".so")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", obj, *others, "-o", out], check=True)
     os.remove(obj)

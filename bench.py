@@ -315,7 +315,8 @@ def passive_replication(ctx, batch, one_shot):
            "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
            "events_per_gpu": pr.n_events, "tasks_per_gpu": v["split_workflows"],
            "vs_one_shot": v,
-           "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP)}
+           "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP,
+                                config_traffic("passive_replication", pr.batch.n_wf, pr.n_events))}
     del pr
     return out
 
@@ -362,7 +363,8 @@ def config5(ctx, n_wf, shard):
                        "events_per_gpu": batch.n_events, "workflows_per_gpu": batch.n_wf,
                        "workflows_ok": int(digest[1]),
                        "vh_items_per_workflow": float(res.exec["n_vh_items"][res.exec["status"] == 0].mean()),
-                       "roofline": roofline(synth.algorithmic_bytes(batch, res), float(np.mean(ms)), FAST_GROUP),
+                       "roofline": roofline(synth.algorithmic_bytes(batch, res), float(np.mean(ms)), FAST_GROUP,
+                                            config_traffic("config5_rebuild", batch.n_wf, batch.n_events)),
                        "setup_s": setup}}
     if ctx.rank == 0:
         from oracle import oracle
@@ -462,7 +464,7 @@ def ndc_line(ctx, nb):
                                                     ((got["status"] == 0) & (got["action"] == abi.NDC_DUPLICATE)).sum(),
                                                     (got["status"] == abi.Status.NDC_RETRY_TASK).sum(),
                                                     ((got["status"] != 0) & (got["status"] != abi.Status.NDC_RETRY_TASK)).sum()))},
-            "roofline": roofline(alg, k_ms, "crr::ndc_prepare_kernel")}
+            "roofline": roofline(alg, k_ms, "crr::ndc_prepare_kernel", config_traffic("config5_ndc_prepare", n, n))}
     if ctx.rank == 0:
         m = min(n, 200_000)
         sub = ndc.NdcBatch(tasks=nb.tasks[:m], branches=nb.branches, items=nb.items, n_out_items=nb.n_out_items)
@@ -509,7 +511,8 @@ def checksum_line(ctx, db, batch, res):
     return {"workload": "Load verify: the mutable-state checksum recomputed from the replayed rows of every workflow",
             "value": tot * args.config_steps / wall, "unit": "workflows verified/s",
             "matches_replay_checksums": bool((got[ok] == ex["checksum"][ok]).all()), "verified": int(ok.sum()),
-            "roofline": roofline(alg, k_ms, "crr::checksum_kernel")}
+            "roofline": roofline(alg, k_ms, "crr::checksum_kernel",
+                                 config_traffic("config5_checksum_verify", batch.n_wf, batch.n_events))}
 
 
 # ---- persisted blobs -> rows (rank 0, N = 1) ---------------------------------------------------------------------

@@ -28,12 +28,13 @@ def main():
     import numpy as np
     import torch
     from cadence_amd import synth_native
+    from cadence_amd import dist as cdist
     from cadence_amd.engine import ReplayEngine
     from cadence_amd.flatten import interleave
     from cadence_amd.replication import PassiveReplication
 
     t0 = time.time()
-    batch = interleave(synth_native.mixed(a.wf), long_threshold=256)
+    batch = interleave(synth_native.mixed(a.wf, shard=(cdist.NUM_SHARDS, 1, 0)), long_threshold=256)   # bench.py's N=1 shard
     eng = ReplayEngine(0)
     db = eng.upload(batch)
     eng.launch(db)
@@ -63,7 +64,7 @@ def main():
         phases["waves"] = int(buf[5])
     v = pr.verify(one_shot)
     med = float(np.median(ms[1:]))
-    print(json.dumps({"hbm_rows": a.hbm_rows, "workflows": a.wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
+    print(json.dumps({"hbm_rows": a.hbm_rows, "workflows": pr.batch.n_wf, "events": int(pr.n_events), "kernel_ms": ms[1:], "median_ms": med,
                       "events_per_s": pr.n_events / (med * 1e-3), "verify": v, "setup_s": setup_s, "phase_clocks_per_wave": phases}), flush=True)
 
 

@@ -19,13 +19,15 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_kernel(root):
-    """{counter: {kernel: median over dispatches}} for the replay kernels."""
+def per_kernel(root, prefixes=("replay_",), exclude=()):
+    """{counter: {kernel: median over dispatches}} for the kernels whose names start with `prefixes` (and
+    contain none of `exclude`)."""
     acc = collections.defaultdict(float)
     for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("crr::", "").strip()
-            if not k.startswith("replay_"):
+            k = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+                 .replace("crr::", "").strip())
+            if not k.startswith(tuple(prefixes)) or any(x in k for x in exclude):
                 continue
             acc[(r["Counter_Name"], k, f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -41,8 +43,11 @@ def main():
     p.add_argument("--workflows", type=int, required=True)
     p.add_argument("--events", type=int, required=True)
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "traffic_configs.json"))
+    p.add_argument("--kernels", default="replay_", help="comma-separated kernel-name prefixes of the launch group")
+    p.add_argument("--exclude", action="append", default=[], help="a name fragment to leave out (repeatable; e.g. "
+                                                                  "the fresh instantiations a resume probe also dispatches)")
     a = p.parse_args()
-    d = per_kernel(a.root)
+    d = per_kernel(a.root, a.kernels.split(","), a.exclude)
     fetch = {k: 2.0 * v * 1024 for k, v in d.get("FETCH_SIZE", {}).items()}   # KB -> bytes, x2 (gfx950)
     write = {k: v * 1024 for k, v in d.get("WRITE_SIZE", {}).items()}
     if not fetch or not write:

@@ -3947,9 +3947,11 @@ using CompactTier3 = CTier<12, 8, 6, 4, 4, 8, 64>;
 // instead of per-lane gathers from kCrcGlobal through the L1: an 8-KB table gather touches many lines per
 // instruction, and with few events per workflow (a resume) the checksum is a large part of its work
 // (passive replication on the config-3 shard: 1.02 -> 0.91 ms per step with the resume instantiations'
-// tables in LDS, A/B on one box; their occupancy is register-limited, so the 8 KB costs no waves)
+// tables in LDS, A/B on one box; their occupancy is register-limited, so the 8 KB costs no waves).  Tier 3's
+// resume kernel (one wave per SIMD, few workflows) does better on the constant-memory tables: 0.885 ->
+// 0.85 ms with tiers 1-2 only (round 4, A/B)
 #ifndef CRR_COMPACT_LDS_CRC_MASK  // bit k: tier k+1's resume instantiation (bit 3+k: its fresh one)
-#define CRR_COMPACT_LDS_CRC_MASK 7
+#define CRR_COMPACT_LDS_CRC_MASK 3
 #endif
 template <int TIER_NO, bool RESUME>
 struct CompactLdsCrc {

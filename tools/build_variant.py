@@ -23,7 +23,9 @@ def main():
     outdir = os.path.join(ROOT, "tools", "variants")
     os.makedirs(outdir, exist_ok=True)
     obj = os.path.join(outdir, name + ".o")
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-mllvm", "-amdgpu-sched-strategy=max-ilp",
+    sched = os.environ.get("CRR_VARIANT_SCHED", "max-ilp")   # "default": the compiler's own scheduler
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+             *([] if sched == "default" else ["-mllvm", "-amdgpu-sched-strategy=" + sched]),
              "-I", os.path.join(ROOT, "include"), *defs]
     subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-I", os.path.join(ROOT, "cadence_amd", "csrc"), "-c", src, "-o", obj],
                    check=True)

@@ -8,18 +8,19 @@
 //   cadence_amd/flatten.py                live_set_bounds, tier_classes, interleave, _interleave_side
 //
 // Pipeline (crr_ingest_plan, then crr_ingest_layout once the caller has sized its buffers):
-//   1 blob_head_kernel     lane per blob: the event count from the History list header (a full walk
-//                          only for a blob not in thriftrw's canonical shape); blob -> workflow map
+//   1 blob_head_quick_kernel / blob_head_kernel   lane per blob: the event count from the History list
+//                          header (a full walk only for a blob not in thriftrw's canonical shape)
 //   2 scan                 exclusive prefixes: every blob's slice of the canonical (stride-1,
 //                          workflow-order) scratch columns
-//   3 blob_decode_kernel   lane per blob, the one full thrift walk: columns, side records and key-string
-//                          references (with their hashes) at the events' own slots; domain names
-//                          resolved against a device hash set; previous reset points counted
+//   3 blob_decode_kernel   a wavefront per 64 blobs staged in LDS, a lane per blob walking it: columns,
+//                          side records and key-string references (hashes, 16-byte heads) at the events'
+//                          own slots; previous reset points counted; domain_resolve_kernel then looks the
+//                          domain names up in the device hash set, a lane per event
 //   4 reset_refs_kernel    the previous reset points' strings at their canonical reset_keys positions
-//   5 wf_pass_kernel       lane per workflow: interning (per-workflow open-addressed table over the
-//                          string hashes, exact byte compares), side-record ordinals, capacities, VH
-//                          items, tasks, live-set bounds (valid deletes through a second table), tier
-//                          class, sort key
+//   5 wf_pass_wave_kernel  a wavefront per workflow (<= 64 events): interning by first occurrence, side-record
+//                          ordinals, capacities, VH items, tasks, live-set bounds by pairwise lane compares,
+//                          tier class, sort key; wf_pass_kernel, a lane per workflow with per-workflow
+//                          hash tables, takes the longer ones and those with previous reset points
 //   6 radix sort (hipCUB)  device order = (long, tier | big, -length, index)
 //   7 geometry             per-group maxima (one wavefront per group), prefixes over groups and the
 //                          tail, tier boundaries, the summary
@@ -28,9 +29,9 @@
 // A blob whose walk finds more events than its header announced (hand-made blobs: a second events
 // list) sends the plan back to a full counting walk of every blob before decoding.
 //
-// Parsing is integer / byte work: lanes walk their own blob through a 32-byte register window (aligned
-// dwordx4 loads, one per 16 bytes of a sequential walk) and take each field header / integer with one
-// funnel-shift extraction instead of a load per byte; no MFMA, no LDS staging.
+// Parsing is integer / byte work: in the fast pass a lane walks its blob in LDS, each field header /
+// integer one unaligned 8-byte ds_read; the general pass (and the header walks) read through a 32-byte
+// register window over HBM (aligned dwordx4 loads, a funnel-shift extraction per value).  No MFMA.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 

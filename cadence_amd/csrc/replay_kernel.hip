@@ -3757,6 +3757,9 @@ __device__ __forceinline__ i64 wf_stride(const crr_inputs& in, u32 w) {
 }
 
 // LDS arena of a block: the lane-per-workflow [slot][lane] tables or 4 per-wave row arenas.
+#ifndef CRR_SMALL_CRC  // the lane kernels' CRC tables: 0 built in LDS per block, 1 copied into LDS, 2 none
+#define CRR_SMALL_CRC 0
+#endif
 template <class TIER> struct WaveTier;
 template <> struct WaveTier<SmallTier> { using Arena = WaveArena<40, 32, 16, 8, 8, 24>; };
 template <> struct WaveTier<LargeTier> { using Arena = WaveArena<64, 48, 24, 16, 16, 32>; };
@@ -3772,8 +3775,22 @@ template <class TIER, bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
+#if CRR_SMALL_CRC == 2
+  const u32* crc_tables = kCrcGlobal.v;  // gathers through the L1
+#else
   __shared__ u32 crc_tables[8 * 256];
+#if CRR_SMALL_CRC == 1
+  {  // a copy of the constant-memory tables
+    const uint4* src = reinterpret_cast<const uint4*>(kCrcGlobal.v);
+    uint4* dst = reinterpret_cast<uint4*>(crc_tables);
+#pragma unroll
+    for (int i = 0; i < 8 * 256 / 4 / kBlock; ++i) dst[i * kBlock + threadIdx.x] = src[i * kBlock + threadIdx.x];
+    __syncthreads();
+  }
+#else
   build_crc_tables<kBlock>(crc_tables);
+#endif
+#endif
   __shared__ BlockArena<TIER> arena;
   const u32 n_lane = WAVE_TAIL ? lane_count(in) : in.n_wf;
   const u32 tail_end = WAVE_TAIL ? tail_count_end(in) : in.n_wf;  // [tail_end, n_wf): replay_big_kernel

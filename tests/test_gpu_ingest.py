@@ -72,6 +72,24 @@ def test_device_ingest_matches_host_path(eng, gen):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("gen", ["chains_59", "chains_65", "mixed_64"])
+def test_device_ingest_wave_pass_boundaries(eng, gen):
+    """Workflows either side of the wavefront-per-workflow pass's limit (64 events): 59- and 65-event
+    activity chains, mixed histories around 64 events -- the two per-workflow kernels must agree with the
+    host path byte for byte."""
+    if gen == "chains_59":
+        b = synth.activity_chain(2000, 9, synth.SEED_C2, with_keys=True, wf_ids=np.arange(2000))
+    elif gen == "chains_65":
+        b = synth.activity_chain(2000, 10, synth.SEED_C2, with_keys=True, wf_ids=np.arange(2000))
+    else:
+        b = synth_native.mixed(4000, mean_len=64)
+    bs = encode_batch(b)
+    _canon, want = _host_path(bs)
+    ing, out = _ingest(eng, bs)
+    _assert_same_inputs(ing.to_host_batch(out), want)
+
+
+@pytest.mark.gpu
 def test_device_ingest_python_histories_with_prev_reset_points(eng):
     """Python-generated histories: previous auto-reset points, unknown domains, empty batches, CAN."""
     hs = synth_mixed.mixed_histories(800, 23, multi_version=True, invalid_rate=0.3, can_rate=0.5)

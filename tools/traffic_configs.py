@@ -23,7 +23,7 @@ def per_kernel(root, prefixes=("replay_",), exclude=()):
     """{counter: {kernel: median over dispatches}} for the kernels whose names start with `prefixes` (and
     contain none of `exclude`)."""
     acc = collections.defaultdict(float)
-    for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
             k = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                  .replace("crr::", "").strip())

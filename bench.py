@@ -317,6 +317,11 @@ def passive_replication(ctx, batch, one_shot):
            "vs_one_shot": v,
            "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP,
                                 config_traffic("passive_replication", pr.batch.n_wf, pr.n_events))}
+    if ctx.rank == 0:   # every split workflow, the Load-unstable ones included: the oracle given the same split
+        from oracle import oracle
+        t0 = time.perf_counter()
+        out["vs_oracle"] = pr.verify_oracle(oracle.replay, host_cpus())
+        out["vs_oracle"]["oracle_s"] = time.perf_counter() - t0
     del pr
     return out
 

@@ -119,6 +119,8 @@ class PassiveReplication:
     snapshot: Dict[str, object] = None
     n_events: int = 0                     # events applied per step
     hbm_rows: bool = False                # continue every lane workflow over its HBM rows (A/B only)
+    pre_wf: np.ndarray = None             # the prefix replay's descriptors
+    suffix: HistoryBatch = None           # the new events (the step's inputs, host copy)
 
     def setup(self):
         eng, torch, b = self.eng, self.eng.torch, self.batch
@@ -132,7 +134,9 @@ class PassiveReplication:
         eng.launch(db)
         torch.cuda.synchronize(eng.dev)
         self.prefix = eng.download(db)
+        self.pre_wf = pre
         sb = suffix_batch(b, cut, self.split, suf)
+        self.suffix = sb
         self.n_events = sb.n_events
         dn = eng.upload(sb)
         dn.c_out = db.c_out                        # apply onto the loaded rows in place
@@ -164,6 +168,33 @@ class PassiveReplication:
     def step(self, stream=None):
         self.eng.launch(self.db_new, stream)
 
+    def verify_oracle(self, replay_fn, threads: int) -> Dict[str, int]:
+        """The last step's rows against the oracle given the same split (``replay_fn`` = oracle.replay: the
+        suffix batch with the prefix replay's rows as its loaded states, mutableStateBuilder.Load then
+        ApplyEvents) -- every split workflow whose prefix replayed OK, the Load-unstable ones included.
+        Returns the counts compared and the mismatching fields."""
+        b = self.batch
+        ok_dev = self.prefix.exec["status"] == 0
+        mask_c = np.zeros(b.n_wf, bool)
+        if b.perm is None:
+            mask_c[:] = ok_dev
+        else:
+            mask_c[b.perm] = ok_dev
+        loaded = self.prefix.to_loaded(dataclasses.replace(b, wf=self.pre_wf), mask=mask_c)
+        if b.perm is not None:
+            loaded = loaded.permuted(b.perm)
+        kd = self.suffix.key_dict if self.suffix.key_dict is not None else key_dict_from_events(b)
+        ref = replay_fn(dataclasses.replace(self.suffix, init=loaded, key_dict=kd), threads)
+        res = self.eng.download(self.db)
+        sel = ok_dev & self.split
+        bad = _compare_rows(b, res, ref, sel)
+        c = np.clip(self.prefix.exec["n_activity"].astype(np.int64), 0, b.wf["act_cap"].astype(np.int64))
+        live_pre = gather_live(b, self.prefix)
+        unstable = np.zeros(b.n_wf, bool)
+        np.logical_or.at(unstable, np.repeat(np.arange(b.n_wf), c)[(live_pre["act"]["flags"] & abi.ROW_MAPPED) == 0], True)
+        return {"compared_workflows": int(sel.sum()), "load_unstable_compared": int((sel & unstable).sum()),
+                "mismatches": bad}
+
     def verify(self, one_shot: ReplayResult) -> Dict[str, int]:
         """Compare the last step's rows with the one-shot replay of the whole histories (same layout):
         every field of the exec row but the per-call counters, and every live row, for the split
@@ -178,30 +209,60 @@ class PassiveReplication:
         unstable = np.zeros(b.n_wf, bool)
         np.logical_or.at(unstable, wf[(live_pre["act"]["flags"] & abi.ROW_MAPPED) == 0], True)
         sel = ok & ~unstable
-        bad = 0
-        for f in abi.EXEC_ROW.names:
-            if f in ("reserved", "inconsistencies", "n_tasks"):
-                continue
-            bad += int(((res.exec[f] != one_shot.exec[f]) & sel).sum())
-        la, lb = gather_live(b, res), gather_live(b, one_shot)
-        for t, (name, _dt, _b, cap_f, n_f) in enumerate(abi.TABLES):
-            if name == "tasks":
-                continue
-            cap = b.wf[cap_f].astype(np.int64)     # gather_live's clamp
-            ca = np.clip(res.exec[n_f].astype(np.int64), 0, cap)
-            cb = np.clip(one_shot.exec[n_f].astype(np.int64), 0, cap)
-            keep_a = np.repeat(sel, ca)
-            keep_b = np.repeat(sel, cb)
-            ra, rb = la[name][keep_a], lb[name][keep_b]
-            if ra.shape != rb.shape:
-                bad += 1
-                continue
-            for fld in ra.dtype.names:
-                if fld == "reserved":
-                    continue
-                x, y = ra[fld], rb[fld]
-                if fld == "flags":   # Load recomputes the ActivityID mapping bit; the persisted flags must agree
-                    x, y = x & ~np.uint32(abi.ROW_MAPPED), y & ~np.uint32(abi.ROW_MAPPED)
-                bad += int((x != y).sum())
+        bad = _compare_rows(b, res, one_shot, sel, exact_flags=False, skip=("inconsistencies",))
         return {"compared_workflows": int(sel.sum()), "split_workflows": int(self.split.sum()),
                 "resumed_ok": int((res.exec["status"] == 0).sum()), "mismatches": bad}
+
+
+def key_dict_from_events(b: HistoryBatch):
+    """Per-workflow key id -> string tables (flatten.key_dict_from_interners' format, batch order) from the
+    events' own key strings: a workflow's ids are interned over its history, so every id its rows hold
+    names a string some event of the history carries."""
+    cnt = b.wf["ev_count"].astype(np.int64)
+    st = b.wf_strides()
+    wf_idx = np.repeat(np.arange(b.n_wf), cnt)
+    step = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    x = b.wf["ev_begin"].astype(np.int64)[wf_idx] + step * st[wf_idx]
+    key = b.cols["key"][x].astype(np.int64)
+    count = np.zeros(b.n_wf, np.int64)
+    np.maximum.at(count, wf_idx, key + 1)
+    count = np.maximum(count, 1)
+    begin = np.cumsum(count) - count
+    off = np.zeros(int(count.sum()), np.uint32)
+    ln = np.zeros(int(count.sum()), np.uint32)
+    has = key > 0
+    slot = begin[wf_idx[has]] + key[has]
+    off[slot] = b.key_off[x[has]]
+    ln[slot] = b.key_len[x[has]]
+    return begin.astype(np.uint32), count.astype(np.uint32), off, ln, b.key_arena
+
+
+def _compare_rows(b: HistoryBatch, res: ReplayResult, want: ReplayResult, sel: np.ndarray, exact_flags=True,
+                  skip=()) -> int:
+    """Mismatching exec fields and live-row fields of the workflows in ``sel`` (device order; both results
+    in ``b``'s layout).  exact_flags=False: a row's ActivityID-mapping bit is not compared (Load recomputes
+    it; the one-shot replay never reloaded)."""
+    bad = 0
+    for f in abi.EXEC_ROW.names:
+        if f in ("reserved", "n_tasks") or f in skip:
+            continue
+        bad += int(((res.exec[f] != want.exec[f]) & sel).sum())
+    la, lb = gather_live(b, res), gather_live(b, want)
+    for name, _dt, _b, cap_f, n_f in abi.TABLES:
+        if name == "tasks":
+            continue
+        cap = b.wf[cap_f].astype(np.int64)     # gather_live's clamp
+        ca = np.clip(res.exec[n_f].astype(np.int64), 0, cap)
+        cb = np.clip(want.exec[n_f].astype(np.int64), 0, cap)
+        ra, rb = la[name][np.repeat(sel, ca)], lb[name][np.repeat(sel, cb)]
+        if ra.shape != rb.shape:
+            bad += 1
+            continue
+        for fld in ra.dtype.names:
+            if fld == "reserved":
+                continue
+            x, y = ra[fld], rb[fld]
+            if fld == "flags" and not exact_flags:
+                x, y = x & ~np.uint32(abi.ROW_MAPPED), y & ~np.uint32(abi.ROW_MAPPED)
+            bad += int((x != y).sum())
+    return bad

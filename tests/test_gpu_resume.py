@@ -97,3 +97,7 @@ def test_passive_replication_in_place_matches_one_shot(native):
     v = pr.verify(one)
     assert v["mismatches"] == 0, v
     assert v["compared_workflows"] > 0.5 * v["split_workflows"] > 0, v   # the rest: failed or not Load-stable
+    # every split workflow, the Load-unstable ones too, against the oracle given the same split
+    vo = pr.verify_oracle(_oracle().replay, 0)
+    assert vo["mismatches"] == 0, vo
+    assert vo["compared_workflows"] >= v["compared_workflows"], vo

@@ -322,6 +322,10 @@ def passive_replication(ctx, batch, one_shot):
         t0 = time.perf_counter()
         out["vs_oracle"] = pr.verify_oracle(oracle.replay, host_cpus())
         out["vs_oracle"]["oracle_s"] = time.perf_counter() - t0
+        # the loaded states themselves: the whole-shard prefix replay against the oracle
+        t0 = time.perf_counter()
+        out["vs_oracle"]["prefix"] = pr.verify_prefix_oracle(oracle.replay, host_cpus())
+        out["vs_oracle"]["prefix"]["oracle_s"] = time.perf_counter() - t0
     del pr
     return out
 

@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1

@@ -3630,11 +3630,12 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       if (L.vh_last_id != want_id || L.vh_last_ver != want_ver) FAIL(CRR_ERR_REBUILD_LAST_ITEM, n_ev);
     }
     if (wf_flags & CRR_WF_FLAG_REFRESH_TASKS) {  // Rebuild's RefreshTasks (state_rebuilder.go:181-186)
-      T.refresh(L, G);  // the state effects (the timers re-created: a task each, emitted from the rows below)
       L.n_tasks = 0;    // CloseTransactionAsSnapshot drops the replay's tasks
-      if constexpr (EMIT) {
-        if (K.on) CHECK_N(refresh_tasks_head(in, L, G, K, src, n_ev, now_ns, retention_days));
-      }
+      // with or without emission: its Go errors and the DecisionTimeout write-back are state effects (only
+      // K.add is compiled out of the non-EMIT instantiations).  Before the timer refresh, as in Go
+      // (mutable_state_task_refresher.go:77-170): a failing head leaves the timer task statuses as replayed.
+      CHECK_N(refresh_tasks_head(in, L, G, K, src, n_ev, now_ns, retention_days));
+      T.refresh(L, G);  // the state effects (the timers re-created: a task each, emitted from the rows below)
     }
   }
 done_events:

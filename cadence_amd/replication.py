@@ -195,6 +195,16 @@ class PassiveReplication:
         return {"compared_workflows": int(sel.sum()), "load_unstable_compared": int((sel & unstable).sum()),
                 "mismatches": bad}
 
+    def verify_prefix_oracle(self, replay_fn, threads: int) -> Dict[str, int]:
+        """The prefix replay (the loaded states every step starts from) against the oracle over the same
+        descriptors -- every workflow, every exec field and live row -- so that ``verify_oracle`` (which
+        hands the oracle the device's prefix rows as its loaded states) does not rest on the device alone."""
+        b = dataclasses.replace(self.batch, wf=self.pre_wf)
+        ref = replay_fn(b, threads)
+        bad = _compare_rows(b, self.prefix, ref, np.ones(b.n_wf, bool))
+        return {"compared_workflows": int(b.n_wf), "events": int(self.pre_wf["ev_count"].astype(np.int64).sum()),
+                "mismatches": bad}
+
     def verify(self, one_shot: ReplayResult) -> Dict[str, int]:
         """Compare the last step's rows with the one-shot replay of the whole histories (same layout):
         every field of the exec row but the per-call counters, and every live row, for the split

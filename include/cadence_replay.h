@@ -44,7 +44,9 @@
 extern "C" {
 #endif
 
-#define CRR_ABI_VERSION 4
+/* 5: status codes 17-18, CRR_IN_HAS_RESUME / CRR_IN_ADVANCED_VISIBILITY, crr_start_side.refresh_jitter,
+ *    RefreshTasks' own task rows (task_cap), RefreshTasks' state effects without CRR_IN_EMIT_TASKS too */
+#define CRR_ABI_VERSION 5
 
 /* ---- constants restated from the reference ------------------------------------------------ */
 /* common/constants.go:30-58 */
@@ -248,16 +250,20 @@ typedef struct crr_workflow {
     int32_t  act_cap, timer_cap, child_cap, rc_cap, sig_cap, vh_cap, rp_cap;
     int32_t  flags;             /* CRR_WF_FLAG_* */
     int64_t  task_base;         /* emitted-task rows (CRR_IN_EMIT_TASKS): task_base + slot * stride */
-    int32_t  task_cap;
+    int32_t  task_cap;          /* rows at task_base for the tasks the replay generates; with
+                                   CRR_WF_FLAG_REFRESH_TASKS they hold RefreshTasks' tasks instead, which can be one
+                                   more (the search-attributes task, CRR_IN_ADVANCED_VISIBILITY): size it as the
+                                   replay's upper bound + 1 (flatten.py).  Too few: CRR_ERR_CAPACITY */
     int32_t  retention_days;    /* domainEntry.GetRetentionDays (DeleteHistoryEventTask, task_generator.go:238-255) */
 } crr_workflow;
 
 #define CRR_WF_FLAG_NEW_RUN 1
 /* After the replay (and the rebuild last-item check), Rebuild's RefreshTasks (state_rebuilder.go:183-186
- * -> mutable_state_task_refresher.go:77-496).  State effects: every pending activity's TimerTaskStatus and
- * user timer's TaskStatus cleared, then CreateNextActivityTimer / CreateNextUserTimer; a started decision
- * with Attempt > 1 gets getNextDecisionTimeout's DecisionTimeout (the jitter injected as
- * crr_start_side.refresh_jitter).  With CRR_IN_EMIT_TASKS the replay's own tasks are dropped
+ * -> mutable_state_task_refresher.go:77-496).  State effects, with or without CRR_IN_EMIT_TASKS: the Go
+ * errors below, then every pending activity's TimerTaskStatus and user timer's TaskStatus cleared and
+ * CreateNextActivityTimer / CreateNextUserTimer; a started decision with Attempt > 1 gets
+ * getNextDecisionTimeout's DecisionTimeout (the jitter injected as crr_start_side.refresh_jitter; a replay
+ * leaves every started decision at Attempt 0, mutable_state_decision_task_manager.go:207-223).  With CRR_IN_EMIT_TASKS the replay's own tasks are dropped
  * (CloseTransactionAsSnapshot) and the task rows hold RefreshTasks' tasks, in its order:
  *   workflow timeout (startTime = now_ns) [+ delayed decision], close tasks or record-started, the
  *   decision's schedule / start task, each pending not-started activity's transfer task, the activity

@@ -98,6 +98,61 @@ def test_passive_replication_in_place_matches_one_shot(native):
     assert v["mismatches"] == 0, v
     assert v["compared_workflows"] > 0.5 * v["split_workflows"] > 0, v   # the rest: failed or not Load-stable
     # every split workflow, the Load-unstable ones too, against the oracle given the same split
+    vp = pr.verify_prefix_oracle(_oracle().replay, 0)     # the loaded states themselves
+    assert vp["mismatches"] == 0 and vp["compared_workflows"] == b.n_wf, vp
     vo = pr.verify_oracle(_oracle().replay, 0)
     assert vo["mismatches"] == 0, vo
     assert vo["compared_workflows"] >= v["compared_workflows"], vo
+
+
+def test_inconsistent_loaded_states_route_to_retry_or_capacity(engine):
+    """Loaded states the compact tiers cannot continue in LDS (rows out of ID order)
+    go to the general path before HBM changes and end equal to the oracle given the same rows; a state
+    with more loaded rows than its slot capacity fails CRR_ERR_CAPACITY at step 0 without writing a row
+    (the rest of the batch unchanged).  Neither may write outside the workflow's slots."""
+    from cadence_amd import abi
+    hs = synth_mixed.mixed_histories(4000, 64, multi_version=True)
+    pre, suf, mask = split_histories(hs, 8, last_only=True)
+    pre_b = interleave(flatten(pre, known_domains=KNOWN))
+    loaded = loaded_from(pre_b, engine.replay(pre_b), mask)
+    swapped = []
+    for name in ("act", "timer", "child"):
+        c = loaded.counts(name)
+        off = np.cumsum(c) - c
+        for w in np.nonzero(c >= 2)[0][:150]:   # slots 0 and 1 exchanged: rows no longer in ID order
+            o = int(off[w])
+            r = loaded.rows[name]
+            r[[o, o + 1]] = r[[o + 1, o]]
+            swapped.append(int(w))
+    assert len(swapped) > 200
+    suf_b = interleave(flatten(suf, known_domains=KNOWN, loaded=loaded))
+    got = engine.replay(suf_b)
+    want = _oracle().replay(suf_b, 0)
+    d = diff_results(suf_b, got, suf_b, want)
+    assert not d, "\n".join(d)
+    # more loaded activities than act_cap for a few resumed workflows (the exec row's count, as uploaded)
+    db = engine.upload(suf_b)
+    ex = db.tensors["exec"][:suf_b.n_wf * abi.EXEC_ROW.itemsize].cpu().numpy().view(abi.EXEC_ROW).copy()
+    resumed = np.nonzero((suf_b.wf["flags"] & abi.WF_FLAG_RESUME) != 0)[0]
+    bad = resumed[:: max(1, resumed.size // 40)][:40]
+    ex["n_activity"][bad] = suf_b.wf["act_cap"][bad] + 3
+    db.tensors["exec"][:ex.nbytes].copy_(engine.torch.from_numpy(ex.view(np.uint8)))
+    engine.launch(db)
+    r2 = engine.download(db)
+    assert (r2.exec["status"][bad] == abi.Status.CAPACITY).all()
+    assert (r2.exec["fail_step"][bad] == ex["src_next"][bad]).all()
+    assert (r2.exec["n_activity"][bad] == 0).all()
+    keep = np.ones(suf_b.n_wf, bool)
+    keep[bad] = False
+    for f in ("status", "checksum", "next_event_id", "n_activity", "n_timer", "n_vh_items"):
+        assert (r2.exec[f][keep] == got.exec[f][keep]).all(), f
+    for name, _dt, *_ in abi.TABLES:   # only the bad workflows' own slots may differ
+        if name == "tasks":
+            continue
+        same = r2.tables[name] == got.tables[name]
+        own = np.zeros(same.shape[0], bool)
+        base_f, cap_f = {t[0]: (t[2], t[3]) for t in abi.TABLES}[name]
+        for w in bad:
+            idx = int(suf_b.wf[base_f][w]) + np.arange(int(suf_b.wf[cap_f][w])) * int(suf_b.wf_strides()[w])
+            own[idx[idx < own.size]] = True
+        assert same[~own].all(), name

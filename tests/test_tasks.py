@@ -199,6 +199,70 @@ def test_refresh_missing_start_or_completion_event():
     assert r.exec["status"][0] == abi.Status.MISSING_COMPLETION_EVENT
 
 
+def _refresh_state_effect_histories():
+    """Rebuilds whose RefreshTasks fails, with task emission on or off alike: a bad delayed-decision
+    initiator (mutable_state_task_generator.go:269-277; the start event's own task generation already
+    fails on it) and a missing start event
+    (mutable_state_builder.go:1131-1157) with a live activity whose timer task status a failing head
+    leaves as replayed (the timer refresh comes after it, mutable_state_task_refresher.go:278-336), and a
+    completion event outside the completion batch (:1085-1128).  And two
+    started decisions scheduled with Attempt 3 / 6: getNextDecisionTimeout's DecisionTimeout write-back
+    (:352-388, :1051-1064) needs a started decision with Attempt > 1, which a replay cannot leave --
+    ReplicateDecisionTaskStartedEvent is called with a nil decision and sets Attempt = 0
+    (mutable_state_decision_task_manager.go:207-223) -- and RefreshTasks on a resumed state fails at
+    GetStartEvent (the start event is not in the call), so the write-back is unreachable on this path."""
+    act = dict(activity_id="a", schedule_to_start_timeout_seconds=30, schedule_to_close_timeout_seconds=60,
+               start_to_close_timeout_seconds=20)
+    hs = [
+        [[_start(), ev(ET.DecisionTaskScheduled, 2, start_to_close_timeout_seconds=10, attempt=3)],
+         [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)]],
+        [[_start(), ev(ET.DecisionTaskScheduled, 2, start_to_close_timeout_seconds=7, attempt=6)],
+         [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)]],
+        [[_start(first_decision_task_backoff_seconds=30, initiator=abi.INITIATOR_DECIDER),
+          ev(ET.ActivityTaskScheduled, 2, **act)]],
+        [[ev(ET.DecisionTaskScheduled, 2), ev(ET.ActivityTaskScheduled, 3, **act)]],
+        [[_start(), ev(ET.DecisionTaskScheduled, 2)], [ev(ET.DecisionTaskStarted, 3, scheduled_event_id=2)],
+         [ev(ET.DecisionTaskCompleted, 4, started_event_id=3), ev(ET.WorkflowExecutionCompleted, 5)],
+         [ev(ET.WorkflowExecutionSignaled, 6)]],
+    ]
+    return [WorkflowHistory(batches=b, refresh_tasks=True, now_ns=REB_NOW, retention_days=3,
+                            refresh_jitter=5 * SEC + 123 + 7 * i) for i, b in enumerate(hs)]
+
+
+def test_refresh_state_effects_do_not_depend_on_emission():
+    # the bad initiator already fails the replay at the start event's own GenerateDelayedDecisionTasks
+    want_status = [0, 0, abi.Status.BAD_INITIATOR, abi.Status.MISSING_START_EVENT, abi.Status.MISSING_COMPLETION_EVENT]
+    res, bs = {}, {}
+    for emit in (False, True):
+        b = bs[emit] = flatten(_refresh_state_effect_histories(), known_domains=KNOWN)
+        b.emit_tasks = emit
+        res[emit] = oracle.replay(b, 1)
+        assert [int(s) for s in res[emit].exec["status"]] == want_status
+    for f in ("decision_timeout", "decision_attempt", "status", "fail_step", "checksum", "flags"):
+        assert (res[False].exec[f] == res[True].exec[f]).all(), f
+    # the started decisions' Attempt is 0 after the replay, so DecisionTimeout stays the scheduled one
+    assert [int(x) for x in res[False].exec["decision_attempt"][:2]] == [0, 0]
+    assert [int(x) for x in res[False].exec["decision_timeout"][:2]] == [10, 7]
+    # a failing head leaves the activity's timer task status as the replay's epilogue set it
+    for w in (3,):
+        assert int(res[False].live_rows(bs[False], w)["act"]["timer_task_status"][0]) != 0
+
+
+@pytest.mark.gpu
+def test_device_refresh_state_effects_match_oracle():
+    from cadence_amd.engine import ReplayEngine
+    eng = ReplayEngine(0)
+    for emit in (False, True):
+        b = flatten(_refresh_state_effect_histories() * 40, known_domains=KNOWN)
+        b.emit_tasks = emit
+        want = oracle.replay(b, 1)
+        for layout in (interleave(b), interleave(b, long_threshold=0), b):
+            layout.emit_tasks = emit
+            got = eng.replay(layout)
+            d = diff_results(layout, got, b, want)
+            assert not d, f"emit={emit}: " + "\n".join(d)
+
+
 def _mixed():
     hs = synth_mixed.mixed_histories(3000, 61, multi_version=True, invalid_rate=0.2, can_rate=0.4)
     for i, h in enumerate(hs):

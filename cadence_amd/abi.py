@@ -295,11 +295,18 @@ class CInputs(ctypes.Structure):
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("compact_begin", ctypes.c_uint32),
                 ("compact2_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
-                ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32)]
+                ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32), ("digest_keys", ctypes.c_void_p)]
 
 
 class COutputs(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES] + [("scratch",)]]
+    _fields_ = [(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES] + [("scratch",), ("digest",)]]
+
+
+# crr_replay's fused digest (crr_outputs.digest): stripes of partial sums (cadence_replay.h)
+DIGEST_FIELDS = 7
+DIGEST_STRIPES = 8
+DIGEST_STRIDE = 16
+DIGEST_WORDS = DIGEST_STRIPES * DIGEST_STRIDE
 
 
 SCRATCH_EXTRA_WORDS = 64
@@ -313,4 +320,6 @@ def check_layout(lib):
         got = lib.crr_sizeof(i)
         if got != dt.itemsize:
             raise RuntimeError(f"ABI layout mismatch for struct #{i}: C {got} vs numpy {dt.itemsize}")
-    assert ctypes.sizeof(CInputs) == 8 * 8 + 5 * 8 + 40
+    for i, st in ((13, CInputs), (14, COutputs)):
+        if lib.crr_sizeof(i) != ctypes.sizeof(st):
+            raise RuntimeError(f"ABI layout mismatch for {st.__name__}: C {lib.crr_sizeof(i)} vs ctypes {ctypes.sizeof(st)}")

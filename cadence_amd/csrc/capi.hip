@@ -199,6 +199,7 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if (!out->act || !out->timer || !out->child || !out->rc || !out->sig || !out->vh || !out->rp) return false;
   if ((in->flags & CRR_IN_EMIT_TASKS) && !out->tasks) return false;
   if (in->stride == 64 && !out->scratch) return false;
+  if (out->digest && !in->digest_keys) return false;
   if (in->flags & CRR_IN_WAVE_TAIL) {
     if (in->stride != 64 || in->wave_begin > in->n_wf) return false;
   }
@@ -241,6 +242,8 @@ size_t crr_sizeof(int which) {
     case 10: return sizeof(crr_ndc_task);
     case 11: return sizeof(crr_ndc_result);
     case 12: return sizeof(crr_task_row);
+    case 13: return sizeof(crr_inputs);
+    case 14: return sizeof(crr_outputs);
     default: return 0;
   }
 }
@@ -282,6 +285,9 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
   const unsigned n_lane = (in->flags & CRR_IN_WAVE_TAIL) ? in->wave_begin : in->n_wf;
   d->valid[0] = d->valid[1] = d->valid[2] = false;
+  // the kernels add every workflow's contribution as it is finalised (crr_outputs.digest)
+  if (out->digest && hipMemsetAsync(out->digest, 0, CRR_DIGEST_WORDS * sizeof(int64_t), s) != hipSuccess)
+    return (int)hipGetLastError();
   for (int phase = 0; phase < 2; ++phase) {
     if (phase == 0 && !(in->flags & CRR_IN_HAS_NEW_RUN)) continue;
     if (timed) (void)hipEventRecord(d->ev[2 * phase], s);

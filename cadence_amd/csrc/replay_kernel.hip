@@ -3189,12 +3189,45 @@ __device__ unsigned long long g_phase_prof[8];
 #else
 #define CRR_PHASE(k) do {} while (0)
 #endif
+// ---- the job's digest, folded into the replay (crr_outputs.digest) -------------------
+// Each finalised workflow adds its terms (cadence_replay.h) to its lane's Digest; the kernel, once every
+// lane of the wavefront is back on one path, sums the wavefront's lanes (xor-shuffle tree) and lane 0 adds
+// the 7 sums to the block's stripe with 64-bit atomics (8 stripes, one 128-byte line each, so a 1M-workflow
+// launch's ~110k atomics spread over 56 lines).  Off (NULL) unless a caller asks for it.
+struct Digest {
+  i64 v[CRR_DIGEST_FIELDS] = {0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void add(const crr_exec_row& R, i32 n_ev, u64 key) {
+    const bool ok = R.status == CRR_OK;
+    const u64 crc = (u64)(u32)R.checksum;
+    const u64 fw = ((u64)(u32)R.status << 32) | (u64)(u32)R.fail_step;
+    v[0] += ok ? (i64)n_ev : 0;
+    v[1] += ok ? 1 : 0;
+    v[2] += ok ? 0 : 1;
+    v[3] += ok ? (i64)crc : 0;
+    v[4] = (i64)((u64)v[4] + (ok ? (key ^ crc) : 0ull));
+    v[5] += (i64)R.inconsistencies;
+    v[6] = (i64)((u64)v[6] + (ok ? 0ull : (key ^ fw)));
+  }
+};
+// every lane of the wavefront active (a kernel's last statement, after its per-workflow work returned)
+__device__ __forceinline__ void digest_flush(const crr_outputs& out, const Digest& D) {
+  if (!out.digest) return;
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(out.digest + (blockIdx.x % CRR_DIGEST_STRIPES) * CRR_DIGEST_STRIDE);
+#pragma unroll
+  for (int k = 0; k < CRR_DIGEST_FIELDS; ++k) {
+    u64 x = (u64)D.v[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += (u64)__shfl_xor((long long)x, off, 64);
+    if ((threadIdx.x & 63) == 0 && x != 0) atomicAdd(dst + k, x);
+  }
+}
+
 // pre_x: the workflow's exec row already read by the caller (a kernel that expects loaded states issues it
-// with the descriptor, one round trip earlier), else nullptr
+// with the descriptor, one round trip earlier), else nullptr.  dg: the lane's digest terms (nullptr: none).
 template <bool EMIT, class P, class SRC>
 __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outputs& out, u32 w, const crr_workflow* wfp,
                                             const Geo& G, P& T, SRC& src, const u32* crc_tables,
-                                            const crr_exec_row* pre_x = nullptr) {
+                                            const crr_exec_row* pre_x = nullptr, Digest* dg = nullptr) {
 #if CRR_PHASE_PROF
   u64 ph[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -3720,6 +3753,9 @@ done_events:
   if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len, true, L.vh_last_id, L.vh_last_ver);
   CRR_PHASE(5);
   out.exec[w] = R;
+  // the digest's terms: one lane per workflow (the wave path's lanes all hold the same result)
+  if (dg && out.digest && (!std::is_same<SRC, WaveSource>::value || (threadIdx.x & 63) == 0))
+    dg->add(R, n_ev, in.digest_keys[w]);
 #if CRR_PHASE_PROF
   if constexpr (!std::is_same<SRC, WaveSource>::value) {
     if ((wfp->flags & CRR_WF_FLAG_RESUME) && (threadIdx.x & 63) == 0 && ph[1] != 0) {
@@ -3773,7 +3809,8 @@ union BlockArena {
 // Fast path (stride 64): blocks [0, wave_blocks) replay the long-history tail one workflow per
 // wavefront (dispatched first, they run longest), the remaining blocks replay lane per workflow.
 template <class TIER, bool WAVE_TAIL, bool EMIT, bool LANES = false>
-__device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
+__device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi,
+                                           Digest& D) {
   static_assert(sizeof(typename WaveTier<TIER>::Arena) * kWavesPerBlock <= sizeof(LdsArena<TIER>),
                 "per-wave arenas must fit in the lane arena");
 #if CRR_SMALL_CRC == 2
@@ -3809,7 +3846,7 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     T.init();
 
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
-    replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
+    replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
     return;
   }
   const u32 w = lo + (blockIdx.x - wave_blocks) * kBlock + threadIdx.x;  // lanes [lo, hi); launched with kBlock
@@ -3829,18 +3866,22 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
   LdsTables<TIER, LANES> T;
   T.init(&arena.lane, &in, ev_begin);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
 }
 template <bool WAVE_TAIL, bool EMIT, bool LANES = false>
 #ifndef CRR_SMALL_WAVES_PER_EU
 #define CRR_SMALL_WAVES_PER_EU 3
 #endif
 __global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_lds<SmallTier, WAVE_TAIL, EMIT, LANES>(in, out, phase, lo, hi);
+  Digest D;
+  replay_lds<SmallTier, WAVE_TAIL, EMIT, LANES>(in, out, phase, lo, hi, D);
+  digest_flush(out, D);
 }
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi);
+  Digest D;
+  replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi, D);
+  digest_flush(out, D);
 }
 template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_lds_small_kernel<false, false, true>(crr_inputs, crr_outputs, int, u32, u32);
@@ -3865,6 +3906,7 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
   }
   build_crc_tables(crc_tables);
   const u32 stride = gridDim.x * blockDim.x;
+  Digest D;
   for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += stride) {
     const u32 w = retry_only ? out.scratch[kScratchHeader + i] : i;
     const crr_workflow* wfp = in.wf + w;
@@ -3874,8 +3916,9 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
     load_geo(G, wfp, out, st);
     GlobalTables T;
     LaneSource S(in.ev, wfp->ev_begin, st, wfp->ev_count, (in.flags & CRR_IN_EMIT_TASKS) != 0);
-    replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+    replay_body<true>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
   }
+  digest_flush(out, D);
 }
 
 // Retry pass over the workflows the fast path handed back (one launch, 64 threads per block,
@@ -3891,7 +3934,7 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
 template <class ST, bool EMIT = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
-                                                 WaveTables<ST>& T, const u32* crc_tables) {
+                                                 WaveTables<ST>& T, const u32* crc_tables, Digest& D) {
   const crr_workflow* wfp = in.wf + w;
   if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   const i64 st = wf_stride(in, w);
@@ -3901,10 +3944,10 @@ __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body<EMIT, WaveTables<ST>, WaveSource>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<EMIT, WaveTables<ST>, WaveSource>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
 }
 __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
-                                                 LdsArena<HugeTier>* arena, const u32* crc_tables) {
+                                                 LdsArena<HugeTier>* arena, const u32* crc_tables, Digest& D) {
   const crr_workflow* wfp = in.wf + w;
   if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   Geo G;
@@ -3914,11 +3957,11 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
   T.list = -1;
   T.init(arena, &in, wfp->ev_begin);
   LaneSource S(in.ev, wfp->ev_begin, 64, wfp->ev_count, tasks);
-  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
   if (T.retried) {
     GlobalTables H;
     LaneSource S2(in.ev, wfp->ev_begin, 64, wfp->ev_count, tasks);
-    replay_body<true>(in, out, w, wfp, G, H, S2, crc_tables);
+    replay_body<true>(in, out, w, wfp, G, H, S2, crc_tables, nullptr, &D);
   }
 }
 // Wide segment (CRR_IN_TIERED [hbm_begin, lanes)): lane workflows whose live sets the host expects to
@@ -3928,10 +3971,8 @@ __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr
 #ifndef CRR_WIDE_WAVES_PER_EU
 #define CRR_WIDE_WAVES_PER_EU 2
 #endif
-__global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase,
-                                                                                    u32 lo, u32 hi) {
-  __shared__ u32 crc_tables[8 * 256];
-  build_crc_tables<kBlock>(crc_tables);
+__device__ __forceinline__ void replay_wide(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi,
+                                            const u32* crc_tables, Digest& D) {
   const u32 w = lo + blockIdx.x * kBlock + threadIdx.x;
   if (w >= hi) return;
   const crr_workflow* wfp = in.wf + w;
@@ -3949,7 +3990,15 @@ __global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_ker
   }
   GlobalTables T;
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, (in.flags & CRR_IN_EMIT_TASKS) != 0);
-  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables);
+  replay_body<true>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
+}
+__global__ void __launch_bounds__(kBlock, CRR_WIDE_WAVES_PER_EU) replay_wide_kernel(crr_inputs in, crr_outputs out, int phase,
+                                                                                    u32 lo, u32 hi) {
+  __shared__ u32 crc_tables[8 * 256];
+  build_crc_tables<kBlock>(crc_tables);
+  Digest D;
+  replay_wide(in, out, phase, lo, hi, crc_tables, D);
+  digest_flush(out, D);
 }
 // Compact LDS tiers (CRR_IN_TIERED segments [compact_begin, compact2_begin), [compact2_begin,
 // wide_begin) and [wide_begin, hbm_begin)): lane per workflow, 64 lanes per block; slot counts per map
@@ -3976,7 +4025,8 @@ struct CompactLdsCrc {
   static constexpr bool value = ((CRR_COMPACT_LDS_CRC_MASK >> ((TIER_NO - 1) + (RESUME ? 0 : 3))) & 1) != 0;
 };
 template <class TIER, bool EMIT, bool RESUME, int TIER_NO>
-__device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi) {
+__device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi,
+                                               Digest& D) {
   __shared__ CompactArena<TIER> arena;
   const u32* crc_tables = kCrcGlobal.v;
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
@@ -4011,7 +4061,7 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   T.init(&arena, &in, ev_begin, ev_count0);
   LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
   replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables,
-                                                             RESUME ? &X0 : nullptr);
+                                                             RESUME ? &X0 : nullptr, &D);
 }
 // register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
 // limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
@@ -4027,11 +4077,15 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
 #endif
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, RESUME ? CRR_COMPACT1_RESUME_WAVES_PER_EU : CRR_COMPACT1_WAVES_PER_EU) replay_compact1_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier1, EMIT, RESUME, 1>(in, out, phase, lo, hi);
+  Digest D;
+  replay_compact<CompactTier1, EMIT, RESUME, 1>(in, out, phase, lo, hi, D);
+  digest_flush(out, D);
 }
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_COMPACT2_WAVES_PER_EU) replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier2, EMIT, RESUME, 2>(in, out, phase, lo, hi);
+  Digest D;
+  replay_compact<CompactTier2, EMIT, RESUME, 2>(in, out, phase, lo, hi, D);
+  digest_flush(out, D);
 }
 template __global__ void replay_compact1_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact1_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
@@ -4046,7 +4100,9 @@ template __global__ void replay_compact2_kernel<true, true>(crr_inputs, crr_outp
 // few hundred wavefronts, so what matters is its per-event latency (LDS, not the HBM rows' round trips)
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, 1) replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
-  replay_compact<CompactTier3, EMIT, RESUME, 3>(in, out, phase, lo, hi);
+  Digest D;
+  replay_compact<CompactTier3, EMIT, RESUME, 3>(in, out, phase, lo, hi, D);
+  digest_flush(out, D);
 }
 template __global__ void replay_compact3_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_compact3_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
@@ -4063,11 +4119,13 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
   build_crc_tables(crc_tables);
   WaveTables<LdsRows<BigArena, -1>> T;
   T.S.M = &arena;
-  replay_wave_item(in, out, phase, w, T, crc_tables);
+  Digest D;
+  replay_wave_item(in, out, phase, w, T, crc_tables, D);
   if (T.retried) {
     WaveTables<HbmRows> H;
-    replay_wave_item(in, out, phase, w, H, crc_tables);
+    replay_wave_item(in, out, phase, w, H, crc_tables, D);
   }
+  digest_flush(out, D);
 }
 // Long-history tail of a CRR_IN_TIERED batch ([wave_begin, big_begin), longest first): one wavefront
 // per workflow over a 12-KB LDS row arena; a workflow that outgrows it (or resumes a loaded state) is
@@ -4086,11 +4144,13 @@ __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(
   if (w >= hi) return;
   WaveTables<LdsRows<WaveTier<LargeTier>::Arena, -1>> T;
   T.S.M = &arena;
-  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables);
+  Digest D;
+  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables, D);
   if (T.retried) {
     WaveTables<HbmRows> H;
-    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables);
+    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables, D);
   }
+  digest_flush(out, D);
 }
 template __global__ void replay_tail_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_tail_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
@@ -4107,15 +4167,16 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   const u32 n1 = min(__hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
   if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
   build_crc_tables(crc_tables);
+  Digest D;
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
     if (w >= in.n_wf) continue;
     WaveTables<LdsRows<BigArena, -1>> T;
     T.S.M = &arena.wave;
-    replay_wave_item(in, out, phase, w, T, crc_tables);
+    replay_wave_item(in, out, phase, w, T, crc_tables, D);
     if (T.retried) {
       WaveTables<HbmRows> H;
-      replay_wave_item(in, out, phase, w, H, crc_tables);
+      replay_wave_item(in, out, phase, w, H, crc_tables, D);
     }
   }
   __syncthreads();  // the lane arena reuses the wave arena's LDS
@@ -4127,8 +4188,9 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   for (u32 base = start * chunk; base < n0; base += gridDim.x * chunk) {
     const u32 i = base + threadIdx.x;
     const u32 w = (threadIdx.x < chunk && i < n0) ? out.scratch[retry_slot(in, 0, i)] : in.n_wf;
-    if (w < in.n_wf) replay_lane_item(in, out, phase, w, &arena.lane, crc_tables);
+    if (w < in.n_wf) replay_lane_item(in, out, phase, w, &arena.lane, crc_tables, D);
   }
+  digest_flush(out, D);
   // every block has read both counts: the last one to finish resets them for the next launch
   if (threadIdx.x == 0) {
     __threadfence();

@@ -160,6 +160,24 @@ class ReplayEngine:
         co.scratch = T["scratch"].data_ptr()
         return DeviceBatch(batch, T, ci, co, self.device)
 
+    # -- the fused digest (crr_outputs.digest) -------------------------------------------------------
+    def enable_digest(self, db: DeviceBatch, keys: np.ndarray):
+        """Every later crr_replay of ``db`` also writes its digest (dist.DIGEST_FIELDS, as stripes of partial
+        sums) into ``db.tensors["digest"]``; ``keys``: each device position's identity key (dist.device_keys)."""
+        torch = self.torch
+        k = np.ascontiguousarray(np.asarray(keys, np.int64)[: db.n_wf])
+        if k.size != db.n_wf:
+            raise ValueError("one digest key per workflow")
+        db.tensors["digest_keys"] = torch.from_numpy(k.copy()).to(self.dev)
+        db.tensors["digest"] = torch.zeros(abi.DIGEST_WORDS, dtype=torch.int64, device=self.dev)
+        db.c_in.digest_keys = db.tensors["digest_keys"].data_ptr()
+        db.c_out.digest = db.tensors["digest"].data_ptr()
+
+    def read_digest(self, db: DeviceBatch) -> np.ndarray:
+        """The last launch's digest, int64[7] (its stripes summed, mod 2^64)."""
+        self.torch.cuda.synchronize(self.dev)
+        return fold_digest(db.tensors["digest"].cpu().numpy())
+
     # -- launch ------------------------------------------------------------------------------------
     def launch(self, db: DeviceBatch, stream=None):
         """Enqueue crr_replay on ``stream`` (torch stream; default: current stream)."""
@@ -276,6 +294,13 @@ class ReplayEngine:
         db = self.upload(batch)
         self.launch(db)
         return self.download(db)
+
+
+def fold_digest(raw: np.ndarray) -> np.ndarray:
+    """crr_outputs.digest (CRR_DIGEST_WORDS int64: stripes of partial sums) -> the digest, int64[7]."""
+    st = np.asarray(raw, np.int64).reshape(abi.DIGEST_STRIPES, abi.DIGEST_STRIDE)[:, :abi.DIGEST_FIELDS]
+    with np.errstate(over="ignore"):
+        return st.sum(axis=0, dtype=np.int64)
 
 
 COMPACT_TABLES = [t[0] for t in abi.TABLES]   # crr_compact_out.rows order

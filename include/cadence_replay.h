@@ -45,7 +45,8 @@ extern "C" {
 #endif
 
 /* 5: status codes 17-18, CRR_IN_HAS_RESUME / CRR_IN_ADVANCED_VISIBILITY, crr_start_side.refresh_jitter,
- *    RefreshTasks' own task rows (task_cap), RefreshTasks' state effects without CRR_IN_EMIT_TASKS too */
+ *    RefreshTasks' own task rows (task_cap), RefreshTasks' state effects without CRR_IN_EMIT_TASKS too,
+ *    the fused digest (crr_inputs.digest_keys, crr_outputs.digest), crr_sizeof(13 / 14) */
 #define CRR_ABI_VERSION 5
 
 /* ---- constants restated from the reference ------------------------------------------------ */
@@ -321,6 +322,10 @@ typedef struct crr_inputs {
                                               the fast kernels' per-wave arenas (replayed concurrently
                                               with the 57-KB arena); n_wf: none */
     uint32_t                 hbm_begin;
+    /* The job's digest (the one collective of a multi-GPU run), folded into the replay launch:
+       per workflow the identity key the digest binds its result to (e.g. a hash of the workflow ID), in batch
+       order; NULL (with crr_outputs.digest NULL): no digest. */
+    const uint64_t*          digest_keys;
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
@@ -481,7 +486,21 @@ typedef struct crr_outputs {
     crr_task_row*        tasks;     /* CRR_IN_EMIT_TASKS only (else may be NULL) */
     uint32_t*            scratch;   /* engine scratch: >= 2 * n_wf + 64 words, zero-filled before the
                                        first call that uses it; every call leaves its counters zeroed */
+    int64_t*             digest;    /* NULL, or CRR_DIGEST_WORDS int64 (device): this call's digest, below */
 } crr_outputs;
+
+/* crr_replay's digest (crr_outputs.digest, with crr_inputs.digest_keys): CRR_DIGEST_STRIPES partial sums of
+ * CRR_DIGEST_FIELDS int64 fields, stripe k at digest[k * CRR_DIGEST_STRIDE]; the digest is the field-wise
+ * sum over the stripes, every sum wrapping mod 2^64 (so an all-reduce SUM of the whole buffer across ranks,
+ * summed over stripes afterwards, is the job's digest).  crr_replay zeroes the buffer first.  Per workflow
+ * with key k, ok = (status == CRR_OK):
+ *   0 ok ? ev_count : 0      1 ok      2 !ok      3 ok ? checksum : 0      4 ok ? k ^ checksum : 0
+ *   5 inconsistencies        6 ok ? 0 : k ^ ((uint64)(uint32)status << 32 | (uint32)fail_step)
+ * (cadence_amd/dist.py digest_numpy is the host restatement). */
+#define CRR_DIGEST_FIELDS  7
+#define CRR_DIGEST_STRIPES 8
+#define CRR_DIGEST_STRIDE  16    /* int64 per stripe: one 128-byte line each */
+#define CRR_DIGEST_WORDS   (CRR_DIGEST_STRIPES * CRR_DIGEST_STRIDE)
 
 /* ---- NDC branch decisions ------------------------------------------------------
  * branchManagerImpl.prepareVersionHistory (service/history/ndc/branch_manager.go:87-149) for a batch
@@ -572,7 +591,7 @@ int crr_release(void);
 int crr_abi_version(void);
 size_t crr_sizeof(int which);   /* 0 workflow, 1 exec row, 2 activity, 3 timer, 4 child, 5 initiated,
                                    6 vh item, 7 reset point, 8 activity side, 9 start side,
-                                   10 ndc task, 11 ndc result, 12 task row */
+                                   10 ndc task, 11 ndc result, 12 task row, 13 crr_inputs, 14 crr_outputs */
 
 /* Host-side CRC32-IEEE (hash/crc32.ChecksumIEEE) used by the shim's standalone verify. */
 uint32_t crr_crc32_ieee(const uint8_t* data, size_t len);

@@ -152,3 +152,65 @@ def test_device_digest_counts_resumed_events(eng):
     assert d_dev[0] == int(wf["ev_count"][ok].sum()) and 0 < d_dev[0] <= pr.n_events
     # NextEventID - 1 would count the loaded prefix too
     assert d_dev[0] < int((res.exec["next_event_id"][ok] - 1).sum())
+
+
+@pytest.mark.gpu
+def test_fused_digest_equals_host_digest_every_path(eng):
+    """The digest folded into the replay launch (crr_outputs.digest) == dist.digest_numpy of the rows, on
+    every kernel that finalises workflows: the tier segments and the retry pass (mixed, interleaved), the
+    wavefront tail and big kernels (long histories), the canonical-layout global kernel, task emission,
+    and a passive-replication step (loaded states).  Keys bind results to identities: exchanging two OK
+    workflows' keys changes it."""
+    from cadence_amd import dist
+    from cadence_amd.replication import PassiveReplication
+    from cadence_amd.engine import fold_digest
+    mixed = _mixed(3000, 11, mean_len=60, invalid_rate=0.1, can_rate=0.3)
+    long = flatten(synth_mixed.long_tail_histories(60, 12, max_len=4000, run_cap=1500, multi_version=True, caps=None),
+                   known_domains=KNOWN)
+    cases = [("mixed", interleave(mixed)), ("lanes", interleave(mixed, long_threshold=None)), ("canonical", mixed),
+             ("long", interleave(long))]
+    emit = interleave(mixed)
+    emit.emit_tasks = True
+    cases.append(("emit", emit))
+    for name, b in cases:
+        db = eng.upload(b)
+        keys = dist.device_keys(b)
+        eng.enable_digest(db, keys)
+        eng.launch(db)
+        got = eng.read_digest(db)
+        res = eng.download(db)
+        want = dist.digest_numpy(res.exec, b.wf["ev_count"], keys)
+        assert (got == want).all(), (name, got, want)
+        assert got[1] + got[2] == b.n_wf, name
+        eng.launch(db)   # the buffer is zeroed by each call: a second launch gives the same digest
+        assert (eng.read_digest(db) == want).all(), name
+    # identity binding through the keys the kernel reads
+    b = cases[0][1]
+    db = eng.upload(b)
+    keys = dist.device_keys(b)
+    eng.enable_digest(db, keys)
+    eng.launch(db)
+    d0 = eng.read_digest(db)
+    ex = eng.download(db).exec
+    ok = np.nonzero((ex["status"] == 0))[0]
+    i = int(ok[0])
+    j = int(ok[np.nonzero(ex["checksum"][ok] != ex["checksum"][i])[0][0]])
+    k2 = keys.copy()
+    k2[[i, j]] = k2[[j, i]]
+    eng.enable_digest(db, k2)
+    eng.launch(db)
+    d1 = eng.read_digest(db)
+    assert (d1[:4] == d0[:4]).all() and d1[4] != d0[4]
+    # passive replication: the resumed step's digest counts this call's events
+    pb = interleave(_mixed(1500, 9, mean_len=40))
+    pr = PassiveReplication(eng, pb)
+    pr.setup()
+    keys = dist.device_keys(pr.batch)
+    eng.enable_digest(pr.db_new, keys)
+    pr.restore()
+    pr.step()
+    got = eng.read_digest(pr.db_new)
+    res = eng.download(pr.db)
+    wf = pr.db_new.tensors["wf"][: pb.n_wf * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
+    assert (got == dist.digest_numpy(res.exec, wf["ev_count"], keys)).all()
+    assert fold_digest(pr.db_new.tensors["digest"].cpu().numpy())[0] == got[0]

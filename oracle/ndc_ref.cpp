@@ -254,7 +254,9 @@ extern "C" int oracle_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* resu
       }
       results[k] = r;
     };
-    // prepareVersionHistory (branch_manager.go:87-149)
+    // prepareVersionHistory (branch_manager.go:87-149); a VersionHistories always holds a branch
+    // (NewVersionHistories), so an empty one is invalid input
+    if (t.branch_count == 0) { finish(CRR_ERR_NDC_BAD_INDEX); continue; }
     int idx = 0;
     Item lca{0, 0};
     int e = local.find_lca_index_and_item(incoming, &idx, &lca);

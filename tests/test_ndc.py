@@ -4,6 +4,7 @@ CPU: the oracle restatement pinned to the reference's own expectations (versionH
 branch_manager_test.go).  GPU: crr_ndc_prepare against the oracle on random version histories, every
 result field and the new branch's items bit-exact.
 """
+import dataclasses
 import random
 
 import numpy as np
@@ -165,3 +166,41 @@ def test_device_matches_oracle_on_random_tasks():
         assert bad.size == 0, f"{f}: {bad.size} tasks differ, first {bad[:1]}: {got[f][bad[:1]]} vs {want[f][bad[:1]]}"
     for k in range(len(b.tasks)):
         assert new_branch_items(b, got, got_out, k) == new_branch_items(b, want, want_out, k)
+
+
+def _check_device(eng, b):
+    want, want_out = oracle.ndc_prepare(b)
+    got, got_out = prepare_on_device(eng, b)
+    for f in abi.NDC_RESULT.names:
+        bad = np.nonzero(got[f] != want[f])[0]
+        assert bad.size == 0, f"{f}: {bad.size} tasks differ, first {bad[:1]}: {got[f][bad[:1]]} vs {want[f][bad[:1]]}"
+    for k in range(len(b.tasks)):
+        assert new_branch_items(b, got, got_out, k) == new_branch_items(b, want, want_out, k)
+    return got
+
+
+def test_empty_version_histories_are_invalid():
+    r, _ = one(NdcTask([], 0, [(10, 0)], 11, 0))
+    assert r["status"] == Status.NDC_BAD_INDEX and r["action"] == abi.NDC_DUPLICATE
+
+
+@pytest.mark.gpu
+def test_device_staged_and_unstaged_layouts():
+    """The kernel stages each wavefront's span of branch descriptors and items in LDS when it fits
+    (ndc.pack's contiguous layout) and reads HBM otherwise: tasks shuffled in memory (every wavefront's
+    span is the whole batch), long version histories (spans past the stage), and tasks without any
+    branch (invalid) give the oracle's results either way."""
+    from cadence_amd.engine import ReplayEngine
+    eng = ReplayEngine(0)
+    tasks = random_tasks(6000, 21)
+    tasks[5] = NdcTask([], 0, [(10, 0)], 11, 0)
+    b = pack(tasks)
+    _check_device(eng, b)
+    perm = np.random.default_rng(3).permutation(len(b.tasks))
+    _check_device(eng, dataclasses.replace(b, tasks=b.tasks[perm].copy()))
+    longh = []
+    for t in random_tasks(640, 22):   # every task's histories stretched to ~40 items: 64 tasks >> 768 items
+        ext = lambda br: [(e + 1000 * i, v + 10000 * i) for i in range(8) for (e, v) in br][:40] if br else br  # noqa: E731
+        longh.append(NdcTask([ext(x) for x in t.local], t.current_index, ext(t.incoming), t.first_event_id + 7000,
+                             t.first_event_version))
+    _check_device(eng, pack(longh))

@@ -9,7 +9,8 @@ import json
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KINDS = {1: "read u8/lane", 4: "read u32/lane", 8: "read u64/lane", 108: "write u64/lane"}
+KINDS = {1: "read u8/lane", 4: "read u32/lane", 8: "read u64/lane", 108: "write u64/lane",
+         1014: "gather u64 per 112-B row/lane", 1026: "gather u64 per 208-B row/lane", 1002: "gather u64 per 16-B row/lane"}
 
 
 def main():

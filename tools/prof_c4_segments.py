@@ -27,6 +27,8 @@ def main():
     p.add_argument("--lib", default=None)
     p.add_argument("--threshold", type=int, default=256)
     p.add_argument("--only", default="all,tail,big,c1,c2,c3,small,lanes")
+    p.add_argument("--top", type=int, default=0, help="runs 'tailtop': only the N longest tail workflows")
+    p.add_argument("--wave-prof", action="store_true", help="read crr_wave_prof (tools/wave_prof.py builds)")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -48,18 +50,25 @@ def main():
     print(json.dumps({"tiers": list(b.tiers), "wave_begin": n_lane, "n_wf": b.n_wf, "segments": info}), flush=True)
     eng.lib.crr_segment_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
     wf0 = b.wf.copy()
+    seg["tailtop"] = seg["tail"]
     for what in a.only.split(","):
         wf = wf0.copy()
         if what != "all":
             keep = np.zeros(b.n_wf, bool)
-            lo, hi = seg[what]
-            keep[lo:hi] = True
+            if what == "tailtop":
+                lo, hi = seg["tail"]
+                keep[lo + np.argsort(-cnt[lo:hi], kind="stable")[:a.top]] = True
+            else:
+                lo, hi = seg[what]
+                keep[lo:hi] = True
             keep |= (wf0["flags"] & abi.WF_FLAG_NEW_RUN) != 0   # phase 0 unchanged
             wf["ev_count"] = np.where(keep, wf0["ev_count"], 0)
             wf["empty_batch_at"] = np.where(keep, wf0["empty_batch_at"], -1)
         db = eng.upload(b)
         db.tensors["wf"][:wf.nbytes].copy_(torch.from_numpy(wf.view(np.uint8)))
         eng.lib.crr_segment_timing(1)
+        wp = getattr(eng.lib, "crr_wave_prof", None) if a.wave_prof else None
+        wbuf = np.zeros(16, np.uint64)
         ms, segs = [], []
         for r in range(a.reps + 1):
             db.tensors["scratch"].zero_()
@@ -68,6 +77,9 @@ def main():
             k = eng.last_kernel_ms()
             buf = (ctypes.c_float * 7)()
             got = eng.lib.crr_segment_ms(ctypes.addressof(buf), 7)
+            if wp is not None:
+                wp.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                wp(wbuf.ctypes.data, 1)   # read and reset: the last rep's split is kept
             if r:
                 ms.append(k[2])
                 segs.append(list(buf) if got == 7 else None)
@@ -76,7 +88,17 @@ def main():
         sm = None
         if all(s is not None for s in segs):
             sm = {n: round(float(np.median([s[i] for s in segs])), 4) for i, n in enumerate(SIDE)}
-        print(json.dumps({"run": what, "group_ms": ms, "median_ms": med, "segment_finish_ms": sm}), flush=True)
+        line = {"run": what, "group_ms": ms, "median_ms": med, "segment_finish_ms": sm}
+        if wp is not None:
+            w = [int(x) for x in wbuf]
+            cyc = {n: w[i] for i, n in enumerate(("chunk_total", "pre_walk", "walk", "map_op_visits", "other_visits",
+                                                 "epilogues", "post_walk"))}
+            cnts = {n: w[8 + i] for i, n in enumerate(("chunks", "map_ops", "other_visits", "epilogues", "replays"))}
+            line["wave_prof"] = {"cycles": cyc, "counts": cnts,
+                                 "per_chunk": {k: v / max(cnts["chunks"], 1) for k, v in cyc.items()},
+                                 "per_map_op": cyc["map_op_visits"] / max(cnts["map_ops"], 1),
+                                 "per_epilogue": cyc["epilogues"] / max(cnts["epilogues"], 1)}
+        print(json.dumps(line), flush=True)
         del db
         torch.cuda.empty_cache()
 

@@ -17,6 +17,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+MOPS = ("none", "act_insert", "act_start", "act_delete", "act_cancel", "timer_start", "timer_delete", "child_insert",
+        "child_start", "child_delete", "rc_insert", "rc_delete", "sig_insert", "sig_delete")
 SIDE = ("large", "wide_c3", "big", "c1", "c2", "tail", "caller(small)")
 
 
@@ -68,7 +70,7 @@ def main():
         db.tensors["wf"][:wf.nbytes].copy_(torch.from_numpy(wf.view(np.uint8)))
         eng.lib.crr_segment_timing(1)
         wp = getattr(eng.lib, "crr_wave_prof", None) if a.wave_prof else None
-        wbuf = np.zeros(16, np.uint64)
+        wbuf = np.zeros(48, np.uint64)
         ms, segs = [], []
         for r in range(a.reps + 1):
             db.tensors["scratch"].zero_()
@@ -97,7 +99,9 @@ def main():
             line["wave_prof"] = {"cycles": cyc, "counts": cnts,
                                  "per_chunk": {k: v / max(cnts["chunks"], 1) for k, v in cyc.items()},
                                  "per_map_op": cyc["map_op_visits"] / max(cnts["map_ops"], 1),
-                                 "per_epilogue": cyc["epilogues"] / max(cnts["epilogues"], 1)}
+                                 "per_epilogue": cyc["epilogues"] / max(cnts["epilogues"], 1),
+                                 "per_op": {n: {"count": w[32 + i], "cycles_each": w[16 + i] / max(w[32 + i], 1)}
+                                            for i, n in enumerate(MOPS) if w[32 + i]}}
         print(json.dumps(line), flush=True)
         del db
         torch.cuda.empty_cache()

@@ -11,6 +11,7 @@ Buckets (cycles summed over every wavefront-path replay, then counts):
   0 chunk loop total  1 before the walk (VH prologue, lane-parallel passes)  2 walk total  3 map-op visits
   4 other visits (reset points, events of slow chunks)  5 batch epilogues  6 after the walk
   8 chunks  9 map-op visits  10 other visits  11 epilogues  12 replays
+  16 + op: cycles of the visits of map operation op (MOP_*), 32 + op: their count
 """
 import os
 import subprocess
@@ -24,7 +25,7 @@ PATCHES = [
     # the accumulators, declared with the other per-replay state
     ("  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n",
      "  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n"
-     "  u64 wp_[16] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0};\n"),
+     "  u64 wp_[48] = {};\n"),
     ("    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {\n      if (c0) src.advance(c0 >> 6);\n",
      "    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {\n      const u64 wt0_ = __builtin_readcyclecounter();\n"
      "      if (c0) src.advance(c0 >> 6);\n"),
@@ -39,6 +40,9 @@ PATCHES = [
      "          if (!fast) {",
      "        const u64 wv1_ = __builtin_readcyclecounter();\n"
      "        if (isop_) { wp_[3] += wv1_ - wv0_; wp_[9] += 1; } else { wp_[4] += wv1_ - wv0_; wp_[10] += 1; }\n"
+     "        { const u32 t_ = et & CRR_ETYPE_MASK; const u32 op_ = (u32)((t_ < 16 ? mop_word(0) : t_ < 32 ? mop_word(1) :"
+     " mop_word(2)) >> (4 * (t_ & 15))) & 15u;\n"
+     "          if (isop_) { wp_[16 + op_] += wv1_ - wv0_; wp_[32 + op_] += 1; } }\n"
      "        if (et & CRR_ETYPE_BATCH_LAST) {\n          T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks\n"
      "          { const u64 wv2_ = __builtin_readcyclecounter(); wp_[5] += wv2_ - wv1_; wp_[11] += 1; }\n"
      "          if (!fast) {"),
@@ -53,14 +57,14 @@ PATCHES = [
      "  out.exec[w] = R;\n"
      "  if constexpr (" + WAVE + ") {\n"
      "    if ((threadIdx.x & 63) == 0 && wp_[8]) { wp_[12] = 1;\n"
-     "      for (int q_ = 0; q_ < 16; ++q_) atomicAdd(&g_wave_prof[q_], (unsigned long long)wp_[q_]); }\n"
+     "      for (int q_ = 0; q_ < 48; ++q_) atomicAdd(&g_wave_prof[q_], (unsigned long long)wp_[q_]); }\n"
      "  }\n"),
     # the device array and its reader
     ("// ---- the job's digest, folded into the replay",
-     "__device__ unsigned long long g_wave_prof[16];\n"
+     "__device__ unsigned long long g_wave_prof[48];\n"
      "extern \"C\" int crr_wave_prof(unsigned long long* host, int reset) {\n"
      "  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_prof), sizeof(g_wave_prof)) != hipSuccess) return -1;\n"
-     "  if (reset) { unsigned long long z[16] = {}; if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z)) != hipSuccess) return -1; }\n"
+     "  if (reset) { unsigned long long z[48] = {}; if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z)) != hipSuccess) return -1; }\n"
      "  return 0;\n}\n"
      "// ---- the job's digest, folded into the replay"),
 ]

@@ -2058,12 +2058,17 @@ struct WaveTables {
     else return __builtin_amdgcn_readlane(v, j & 63);
   }
 
-  // first slot j < hw with pred(row j) (uniform), -1 if none
+  // first slot j < hw with pred(row j) (uniform), -1 if none.  The bound is made scalar (the compiler
+  // cannot tell that the high-water marks are wave-uniform: a loop over a VGPR bound is compiled as a
+  // divergent loop, exec masks saved and merged around every load) and every lane reads a row of the
+  // block (a lane past hw reads the block's first): the predicate's loads go out together, branch-free.
   template <class Row, class F>
   __device__ __forceinline__ i32 find(Row row, i32 hw, F pred) const {
-    for (i32 b = 0; b < hw; b += 64) {
+    const i32 n = uniform32(hw);
+    for (i32 b = 0; b < n; b += 64) {
       const i32 j = b + lane;
-      const u64 m = __builtin_amdgcn_ballot_w64(j < hw && pred(row(j)));
+      const bool hit = pred(row(j < n ? j : b));
+      const u64 m = __builtin_amdgcn_ballot_w64((j < n) & hit);
       if (m) return b + (i32)__builtin_ctzll(m);
     }
     return -1;
@@ -2086,20 +2091,24 @@ struct WaveTables {
   __device__ __forceinline__ auto S_() const { return [this](i32 j) -> crr_initiated_row& { return S.sig(j); }; }
   __device__ __forceinline__ auto P_() const { return [this](i32 j) -> crr_reset_point_row& { return S.rp(j); }; }
 
+  // predicates with both fields read (bitwise &): a short-circuit && puts the second load behind a branch
+  // and its own wait
   __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
-    return find(A_(), hw_act, [&](const crr_activity_row& r) { return (r.flags & CRR_ROW_LIVE) && r.schedule_id == sched; });
+    return find(A_(), hw_act, [&](const crr_activity_row& r) {
+      return ((r.flags & CRR_ROW_LIVE) != 0) & (r.schedule_id == sched);
+    });
   }
   __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
     return find(A_(), hw_act, [&](const crr_activity_row& r) {
-      return (r.flags & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED) && r.key == key;
+      return ((r.flags & (CRR_ROW_LIVE | CRR_ROW_MAPPED)) == (CRR_ROW_LIVE | CRR_ROW_MAPPED)) & (r.key == key);
     });
   }
   __device__ __forceinline__ i32 find_timer(u32 key) const {
-    return find(T_(), hw_timer, [&](const crr_timer_row& r) { return (r.flags & CRR_ROW_LIVE) && r.key == key; });
+    return find(T_(), hw_timer, [&](const crr_timer_row& r) { return ((r.flags & CRR_ROW_LIVE) != 0) & (r.key == key); });
   }
   template <class Row>
   __device__ __forceinline__ i32 find_initiated(Row row, i32 hw, i64 id) const {
-    return find(row, hw, [&](const auto& r) { return (r.flags & CRR_ROW_LIVE) && r.initiated_id == id; });
+    return find(row, hw, [&](const auto& r) { return ((r.flags & CRR_ROW_LIVE) != 0) & (r.initiated_id == id); });
   }
 
   // LdsRows: each activity's earliest timer candidate (timer_sequence.go:269-381 over its own timeouts),
@@ -2318,13 +2327,17 @@ struct WaveTables {
   __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
     if (L.n_act > 0 && dirty_act) {
       BestTimer B;
-      for (i32 j = lane; j < hw_act; j += 64) {
+      const i32 hwa = uniform32(hw_act);
+      for (i32 j = lane; j < hwa; j += 64) {
         const crr_activity_row& r = S.act(j);
-        if (!(r.flags & CRR_ROW_LIVE)) continue;
-        if constexpr (ST::kLds) {
+        if constexpr (ST::kLds) {  // the row's flags and ID and its cached candidate, read together
+          const u32 fl = r.flags;
+          const i64 sid = r.schedule_id;
           const i64 w = S.M->ids[ST::A + j];
-          if (w & 1) B.offer(S.M->ids[j], r.schedule_id, (i32)((w >> 8) & 0xff), j, ((w >> 16) & 1) != 0);
+          const i64 ct = S.M->ids[j];
+          if ((fl & CRR_ROW_LIVE) && (w & 1)) B.offer(ct, sid, (i32)((w >> 8) & 0xff), j, ((w >> 16) & 1) != 0);
         } else {
+          if (!(r.flags & CRR_ROW_LIVE)) continue;
           activity_candidates(B, j, r.schedule_id, r.scheduled_time, r.started_id != CRR_EMPTY_EVENT_ID, r.started_time,
                               max(r.started_time, r.last_heartbeat_time),
                               r.schedule_to_start, r.schedule_to_close, r.start_to_close, r.heartbeat,
@@ -2345,10 +2358,13 @@ struct WaveTables {
     dirty_act = false;
     if (L.n_timer > 0 && dirty_timer) {
       BestTimer B;
-      for (i32 j = lane; j < hw_timer; j += 64) {
+      const i32 hwt = uniform32(hw_timer);
+      for (i32 j = lane; j < hwt; j += 64) {
         const crr_timer_row& r = S.timer(j);
-        if (!(r.flags & CRR_ROW_LIVE)) continue;
-        B.offer(r.expiry_time, r.started_id, 0, j, r.task_status == CRR_TIMER_TASK_STATUS_CREATED);
+        const u32 fl = r.flags;
+        const i64 ex = r.expiry_time, sid = r.started_id;
+        const i32 ts = r.task_status;
+        if (fl & CRR_ROW_LIVE) B.offer(ex, sid, 0, j, ts == CRR_TIMER_TASK_STATUS_CREATED);
       }
       wave_min(B);
       if (B.have && !B.created && own(B.j)) S.timer(B.j).task_status = CRR_TIMER_TASK_STATUS_CREATED;

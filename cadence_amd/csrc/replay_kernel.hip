@@ -2579,10 +2579,12 @@ struct LaneSource {
 // its lane only where they use it (WaveEv): a MarkerRecorded reads nothing, a DecisionTaskCompleted
 // two fields, instead of every event broadcasting all seven.
 //   CRR_WAVE_FIELDS 0: __shfl (LDS crossbar) into VGPRs; 1: v_readlane into SGPRs; 2: v_readlane then a
-//   VGPR copy.  Config 4 (alternating A/B on one box): 13.4 / 13.9 / 13.9 ms, against 15.7 ms for the
-//   per-event prologue with every field broadcast.
+//   VGPR copy.  Round 3 (config 4, alternating A/B on one box): 13.4 / 13.9 / 13.9 ms, against 15.7 ms for the
+//   per-event prologue with every field broadcast.  Round 5, once the slot searches and the chunk bounds were
+//   scalar: 1 is the fastest (config 4 6.05 -> 5.61 ms, the 256 longest runs alone 4.55 -> 4.24 ms; 2: no
+//   gain): with the fields scalar the transitions' branches are scalar branches, not exec-masked regions.
 #ifndef CRR_WAVE_FIELDS
-#define CRR_WAVE_FIELDS 0
+#define CRR_WAVE_FIELDS 1
 #endif
 struct WaveSource {
   const crr_events& E;
@@ -2590,7 +2592,7 @@ struct WaveSource {
   i32 n, lane;
   Ev cur, nxt;  // per lane: event c * 64 + lane of the current / next chunk
   __device__ __forceinline__ WaveSource(const crr_events& e, i64 b, i64 stride, i32 count)
-      : E(e), begin(b), st(stride), n(count) {
+      : E(e), begin(b), st(stride), n(uniform32(count)) {
     lane = (i32)(threadIdx.x & 63);
   }
   __device__ __forceinline__ Ev load_chunk(i32 c) const {
@@ -3351,6 +3353,8 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
   }
 
   if constexpr (std::is_same<SRC, WaveSource>::value) {
+    // every lane holds the same workflow: its state in scalar registers from here on (a loaded state's
+    // fields come from per-lane loads, which the compiler would otherwise take as divergent)
     // Wavefront per workflow, a 64-event chunk at a time (lane l: event c0 + l).  The prologue of
     // :98-129 for every event of the chunk runs lane-parallel: each lane checks its (ID, version)
     // against its predecessor's (lane 0 against the state carried in), the version-history items it
@@ -3361,10 +3365,14 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     // lane 0 of the first chunk, against the loaded state).
     const i32 lane = src.lane;
     const u64 below = lane == 0 ? 0ull : (~0ull >> (64 - lane));  // lanes < this one
-    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {
+    // the event count read into a scalar register: loaded per lane, the compiler would take it -- and every
+    // chunk bound, failure point and visit mask derived from it -- as divergent, and compile the chunk loop
+    // and the walk as exec-masked loops
+    const i32 n_wave = uniform32(n_ev);
+    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {
       if (c0) src.advance(c0 >> 6);
       const Ev& C = src.cur;
-      const i32 cnt = n_ev - c0 < 64 ? n_ev - c0 : 64;
+      const i32 cnt = n_wave - c0 < 64 ? n_wave - c0 : 64;
       const bool valid = lane < cnt;
       i64 pid = __shfl_up((long long)C.id_, 1, 64), pver = __shfl_up((long long)C.ver_, 1, 64);
       if (lane == 0) { pid = L.vh_last_id; pver = L.vh_last_ver; }

@@ -26,8 +26,8 @@ PATCHES = [
     ("  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n",
      "  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n"
      "  u64 wp_[48] = {};\n"),
-    ("    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {\n      if (c0) src.advance(c0 >> 6);\n",
-     "    for (i32 c0 = 0; c0 < n_ev; c0 += 64) {\n      const u64 wt0_ = __builtin_readcyclecounter();\n"
+    ("    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {\n      if (c0) src.advance(c0 >> 6);\n",
+     "    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {\n      const u64 wt0_ = __builtin_readcyclecounter();\n"
      "      if (c0) src.advance(c0 >> 6);\n"),
     ("      i32 wfail = -1;\n      int wrc = CRR_OK;\n      while (vm) {\n",
      "      i32 wfail = -1;\n      int wrc = CRR_OK;\n      const u64 wt1_ = __builtin_readcyclecounter();\n"

@@ -31,8 +31,9 @@ __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checks
 namespace {
 
 constexpr int kBlock = 256;
-// side streams with the higher priority: 1 compact tier 3, 3 compact tier 1, 4 compact tier 2
-constexpr unsigned kSegPrioMask = 0x1A;
+// side streams with the higher priority: 1 compact tier 3, 2 the big long-tail kernel, 3 compact tier 1,
+// 4 compact tier 2
+constexpr unsigned kSegPrioMask = 0x1E;
 constexpr int kWideBlock = 256;  // replay_wide_kernel's block
 constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
 
@@ -350,13 +351,14 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           (void)hipEventRecord(ss->fork, s);
           for (hipStream_t x : ss->side) (void)hipStreamWaitEvent(x, ss->fork, 0);
         }
+        // Launch order: the big long-tail kernel first (its 65-KB blocks fit only beside few tail wavefronts),
+        // then the lane segments, the tail last.  The tail's thousands of 13-KB wavefronts fill every CU's LDS
+        // as soon as they are dispatched, and a kernel queued behind them on another stream then waits for
+        // tail wavefronts to finish (config 4: the big kernel finishing at 9.2 ms instead of ~5 when the tail
+        // won the race); the lane segments are short, and the tail wavefronts they delay are its shortest.
         if (run_big)  // the longest histories first
           hipLaunchKernelGGL(crr::replay_big_kernel, dim3(in->n_wf - tail_end), dim3(64), 0, s_big, *in, *out, phase,
                              tail_end, in->n_wf);
-        if (run_tail) {  // the long-history tail, one wavefront each
-          if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
-          else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
-        }
         // a compact tier's launch: <EMIT, RESUME> instantiations
 #define CRR_LAUNCH_COMPACT(K, lo_, hi_, strm)                                                                     \
         do {                                                                                                       \
@@ -377,6 +379,10 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         // the 1-slot segment of a multi-segment (mixed) batch takes the divergent dispatch; a one-class
         // batch (config 2) replays in lockstep and keeps the plain switch
         launch_fast(s, true, false, 0, lb, fork);
+        if (run_tail) {  // the long-history tail, one wavefront each
+          if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+        }
         if (fork) {
           if (seg) {
             for (int i = 0; i < kSide; ++i) (void)hipEventRecord(d->seg_end[i], ss->side[i]);

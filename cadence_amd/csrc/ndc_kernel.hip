@@ -23,8 +23,16 @@ using u32 = uint32_t;
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr u32 kStageItems = 768;      // per wavefront: 12 KB of items
-constexpr u32 kStageBranches = 256;   // per wavefront: 2 KB of branch descriptors
+#ifndef CRR_NDC_STAGE_ITEMS
+#define CRR_NDC_STAGE_ITEMS 512
+#endif
+#ifndef CRR_NDC_STAGE_BRANCHES
+#define CRR_NDC_STAGE_BRANCHES 256
+#endif
+// per wavefront: 8 KB of items, 2 KB of branch descriptors (40 KB per block, 4 blocks per CU).  Measured
+// on config 5's 1M tasks (tools/prof_ndc.py): 768 items 0.132 ms, 512 items 0.118 ms, unstaged 0.144 ms
+constexpr u32 kStageItems = CRR_NDC_STAGE_ITEMS;
+constexpr u32 kStageBranches = CRR_NDC_STAGE_BRANCHES;
 
 struct Item {
   i64 e, v;

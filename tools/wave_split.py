@@ -40,6 +40,18 @@ PATCHES = {
                   "    i64 ct = add_seconds(in->ev.timestamp[six], sa.schedule_to_close);",
                   "    crr_activity_side sa{}; sa.schedule_to_close = 20; sa.start_to_close = 10; (void)six;\n"
                   "    i64 ct = add_seconds(ev.ts(), sa.schedule_to_close);")],
+    # round 5 (config 3 traffic attribution): the compact tiers' ActivityTaskStarted without its re-read of the
+    # scheduled event (aux -> side record, timestamp) ...
+    "noreread2": [("      const i64 six = ix(ss);\n      const crr_activity_side sa = in->act_side[in->ev.aux[six]];\n"
+                   "      sched_t = in->ev.timestamp[six]; s2c = sa.schedule_to_close; st2c = sa.start_to_close; hb = sa.heartbeat;",
+                   "      (void)ss;\n      sched_t = ev.ts(); s2c = 20; st2c = 10; hb = 0;")],
+    # ... and finalize building a new activity row without re-reading its scheduled / started events
+    "nofinread": [("      const crr_activity_side as = in->act_side[in->ev.aux[ix(ss)]];\n      crr_activity_row r;",
+                   "      crr_activity_side as{}; as.schedule_to_start = 1; as.schedule_to_close = 2; as.start_to_close = 3;\n"
+                   "      crr_activity_row r;"),
+                  ("      r.scheduled_time = ev_ts(ss);\n", "      r.scheduled_time = (i64)ss;\n"),
+                  ("      r.started_time = started ? ev_ts(st) : CRR_ZERO_TIME;\n",
+                   "      r.started_time = started ? (i64)st : CRR_ZERO_TIME;\n")],
     # passive replication in the compact tiers (CompactTables<TIER, true>), tools/prof_replication.py --lib:
     # the whole step without the checksum
     "rnocrc": [("  const bool want_crc = L.status == CRR_OK;", "  const bool want_crc = false;")],

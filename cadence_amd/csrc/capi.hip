@@ -21,9 +21,10 @@ __global__ void replay_compact2_kernel(crr_inputs in, crr_outputs out, int phase
 template <bool EMIT, bool RESUME>
 __global__ void replay_compact3_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_big_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
-template <bool EMIT>
+template <bool EMIT, bool RESUME>
 __global__ void replay_tail_kernel(crr_inputs in, crr_outputs out, int phase, uint32_t lo, uint32_t hi);
 __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, int retry_only);
+__global__ void tail_gate_kernel(const uint32_t* scratch, uint32_t need);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
 }
@@ -215,10 +216,11 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   return true;
 }
 
-// Every crr_replay leaves the retry-list counters (scratch[0..2]) zeroed; an error return after the
-// fast kernels were enqueued must reset them itself (the retry pass that would have is not launched).
+// Every crr_replay leaves the retry-list counters and the big segment's gate (scratch[0..3]) zeroed; an
+// error return after the fast kernels were enqueued must reset them itself (the retry pass that would have
+// is not launched).
 int fail_reset(const crr_outputs* out, hipStream_t s, hipError_t err) {
-  if (out->scratch) (void)hipMemsetAsync(out->scratch, 0, 3 * sizeof(uint32_t), s);
+  if (out->scratch) (void)hipMemsetAsync(out->scratch, 0, 4 * sizeof(uint32_t), s);
   return (int)err;
 }
 
@@ -380,8 +382,14 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
         // batch (config 2) replays in lockstep and keeps the plain switch
         launch_fast(s, true, false, 0, lb, fork);
         if (run_tail) {  // the long-history tail, one wavefront each
-          if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
-          else hipLaunchKernelGGL((crr::replay_tail_kernel<false>), dim3(tail_end - n_lane), dim3(64), 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          // behind the big segment's blocks (tail_gate_kernel): they cannot start once tail wavefronts hold the LDS
+          if (run_big && fork)
+            hipLaunchKernelGGL(crr::tail_gate_kernel, dim3(1), dim3(64), 0, s_tail, out->scratch, in->n_wf - tail_end);
+          const dim3 g_(tail_end - n_lane), b_(64);
+          if (emit && resume) hipLaunchKernelGGL((crr::replay_tail_kernel<true, true>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          else if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true, false>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          else if (resume) hipLaunchKernelGGL((crr::replay_tail_kernel<false, true>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
+          else hipLaunchKernelGGL((crr::replay_tail_kernel<false, false>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
         }
         if (fork) {
           if (seg) {

@@ -60,6 +60,7 @@ constexpr i64 kSecond = 1000000000LL;
 constexpr int kBlock = 256;
 constexpr int CRR_INTERNAL_RETRY = 200;  // LDS slots exhausted: replay again with GlobalTables
 constexpr u32 kScratchHeader = 64;       // scratch[0], [1] = retry list counts; lists follow the header
+constexpr u32 kScratchGate = 3;          // scratch[3]: big-segment blocks resident (tail_gate_kernel)
 // Retry lists: list 0 (fast path -> big-arena wavefront pass) at scratch[64 + k], list 1 (big arena ->
 // HBM-row wavefront pass) at scratch[64 + n_wf + k]; scratch holds >= 2 * n_wf + 64 words.
 __device__ __forceinline__ u32 retry_slot(const crr_inputs& in, int list, u32 k) {
@@ -2606,11 +2607,11 @@ struct WaveSource {
   __device__ __forceinline__ i64 task_id(i32 step) const { return E.task_id[begin + (i64)step * st]; }
   __device__ __forceinline__ void start() {
     if (n > 0) cur = load_chunk(0);
-    if (n > 64) nxt = load_chunk(1);
   }
-  // chunk c (>= 1) becomes the current one
-  __device__ __forceinline__ void advance(i32 c) {
-    cur = nxt;
+  // the next chunk becomes the current one
+  __device__ __forceinline__ void rotate() { cur = nxt; }
+  // chunk c + 1's loads, issued while chunk c is processed
+  __device__ __forceinline__ void issue_next(i32 c) {
     if ((c + 1) * 64 < n) nxt = load_chunk(c + 1);
   }
 };
@@ -2633,11 +2634,28 @@ __device__ __forceinline__ i64 lane_i64(i64 v, i32 l) {
   const u32 lo = lane_u32((u32)(u64)v, l), hi = lane_u32((u32)((u64)v >> 32), l);
   return (i64)(((u64)hi << 32) | lo);
 }
+// ActivityTaskScheduled's side record (the fields the transitions read), gathered lane-parallel for the
+// whole chunk before the walk: the walk's insert reads it out of its lane instead of waiting on a
+// dependent HBM load per insert
+struct SidePf {
+  i32 s2s, s2c, st2c, hb, retry, dom;
+};
 // event l of the current chunk, each field read out of lane l where a transition uses it
 struct WaveEv {
   const Ev& C;
   i32 l;
   u32 et;
+  const SidePf* sp;
+  __device__ __forceinline__ crr_activity_side act_side(const crr_inputs&) const {
+    crr_activity_side a{};
+    a.schedule_to_start = (i32)lane_u32((u32)sp->s2s, l);
+    a.schedule_to_close = (i32)lane_u32((u32)sp->s2c, l);
+    a.start_to_close = (i32)lane_u32((u32)sp->st2c, l);
+    a.heartbeat = (i32)lane_u32((u32)sp->hb, l);
+    a.has_retry_policy = (i32)lane_u32((u32)sp->retry, l);
+    a.domain_status = (i32)lane_u32((u32)sp->dom, l);
+    return a;
+  }
   __device__ __forceinline__ i64 id() const { return lane_i64(C.id_, l); }
   __device__ __forceinline__ i64 ver() const { return lane_i64(C.ver_, l); }
   __device__ __forceinline__ i64 ts() const { return lane_i64(C.ts_, l); }
@@ -2803,6 +2821,16 @@ __device__ __forceinline__ int map_op_and_after(Lane& L, const Geo& G, P& T, con
 
 // One event of ApplyEvents' dispatch (state_builder.go:131-631); returns the Go error's status
 // code (CRR_OK: applied).  `t` is a scalar when the caller found it wave-uniform.
+// ActivityTaskScheduled's side record: from HBM, or from the chunk's prefetch (WaveEv::act_side)
+template <class EV, class = void>
+struct HasActSide { static constexpr bool value = false; };
+template <class EV>
+struct HasActSide<EV, decltype((void)&EV::act_side)> { static constexpr bool value = true; };
+template <class EV>
+__device__ __forceinline__ crr_activity_side act_side_of(const crr_inputs& in, const EV& ev) {
+  if constexpr (HasActSide<EV>::value) return ev.act_side(in);
+  else return in.act_side[ev.aux()];
+}
 template <class P, class EV>
 __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outputs& out, Lane& L, const Geo& G, P& T,
                                            const EV& ev, const i32 s, const i32 t, const i64 batch_first_id,
@@ -2894,7 +2922,7 @@ __device__ __forceinline__ int apply_event(const crr_inputs& in, const crr_outpu
           K.add(L, G, CRR_TASK_DECISION, 0, L.decision_version, 0, L.decision_schedule_id, 0, L.start_src);
         break;
       case CRR_EV_ACTIVITY_TASK_SCHEDULED: {  // :283-295 -> mutable_state_builder.go:2142-2197
-        as = in.act_side[ev.aux()];
+        as = act_side_of(in, ev);
         if (as.domain_status == CRR_DOMAIN_UNKNOWN) FAIL(CRR_ERR_DOMAIN_NOT_FOUND, s);
         op = MOP_ACT_INSERT;  // then GenerateActivityTransferTasks (below)
         break;
@@ -3370,7 +3398,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
     // and the walk as exec-masked loops
     const i32 n_wave = uniform32(n_ev);
     for (i32 c0 = 0; c0 < n_wave; c0 += 64) {
-      if (c0) src.advance(c0 >> 6);
+      if (c0) src.rotate();
       const Ev& C = src.cur;
       const i32 cnt = n_wave - c0 < 64 ? n_wave - c0 : 64;
       const bool valid = lane < cnt;
@@ -3407,6 +3435,16 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
       } while (0)
       const u32 tl = C.et & CRR_ETYPE_MASK;
       const bool live = valid && lane < lim;
+      // the chunk's side records in flight during the lane-parallel passes below (A/B, config 4: the 256
+      // longest runs 4.22-4.27 -> 4.15-4.21 ms together with the tail kernel's HBM-row copy removed; slower
+      // beside it: the register pressure of both)
+      SidePf SP{0, 0, 0, 0, 0, 0};
+      if (valid && tl == CRR_EV_ACTIVITY_TASK_SCHEDULED) {
+        const crr_activity_side* a = in.act_side + (u32)C.aux_;
+        const int4 w0 = reinterpret_cast<const int4*>(a)[0], w1 = reinterpret_cast<const int4*>(a)[1];
+        SP = SidePf{w0.x, w0.y, w0.z, w0.w, w1.x, w1.z};  // has_retry_policy, domain_status
+      }
+      src.issue_next(c0 >> 6);  // after them: a wait on a side record does not wait on the next chunk
       auto le = [](i32 k) -> u64 { return k < 0 ? 0ull : k >= 63 ? ~0ull : (2ull << k) - 1; };  // lanes <= k
       auto last_in = [](u64 m) -> i32 { return m ? 63 - (i32)__builtin_clzll(m) : -1; };
       // A chunk without the rare types (start, closes, continue-as-new, unknown) on a created or running
@@ -3473,7 +3511,7 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
         const i32 j = (i32)__builtin_ctzll(vm);
         vm &= vm - 1;
         const i32 s = c0 + j;
-        const WaveEv ev{C, j, (u32)__builtin_amdgcn_readlane(C.et, j)};
+        const WaveEv ev{C, j, (u32)__builtin_amdgcn_readlane(C.et, j), &SP};
         const u32 et = ev.et;
         i64 bfid = batch_first_id;
         if (!fast) {
@@ -4048,9 +4086,19 @@ template <int TIER_NO, bool RESUME>
 struct CompactLdsCrc {
   static constexpr bool value = ((CRR_COMPACT_LDS_CRC_MASK >> ((TIER_NO - 1) + (RESUME ? 0 : 3))) & 1) != 0;
 };
+// Wave priority (s_setprio) of the small segments whose lanes run long serial histories next to the
+// long-tail wavefronts (config 4: compact tiers 2 / 3 hold ~200 workflows of up to 243 events, three
+// wavefronts each, and share their SIMDs with tail wavefronts: 0.94 ms alone, 4.5-4.8 ms in the group)
+#ifndef CRR_PRIO_C23
+#define CRR_PRIO_C23 0
+#endif
+#ifndef CRR_PRIO_BIG
+#define CRR_PRIO_BIG 0
+#endif
 template <class TIER, bool EMIT, bool RESUME, int TIER_NO>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi,
                                                Digest& D) {
+  if constexpr (TIER_NO >= 2 && CRR_PRIO_C23 > 0) __builtin_amdgcn_s_setprio(CRR_PRIO_C23);
   __shared__ CompactArena<TIER> arena;
   const u32* crc_tables = kCrcGlobal.v;
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
@@ -4138,8 +4186,11 @@ template __global__ void replay_compact3_kernel<true, true>(crr_inputs, crr_outp
 __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   __shared__ u32 crc_tables[8 * 256];
   __shared__ BigArena arena;
+  // resident: counted in before anything else (tail_gate_kernel holds the tail back until every block is)
+  if (threadIdx.x == 0) atomicAdd(out.scratch + kScratchGate, 1u);
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
+  if constexpr (CRR_PRIO_BIG > 0) __builtin_amdgcn_s_setprio(CRR_PRIO_BIG);
   build_crc_tables(crc_tables);
   WaveTables<LdsRows<BigArena, -1>> T;
   T.S.M = &arena;
@@ -4159,25 +4210,47 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
 #ifndef CRR_TAIL_WAVES_PER_EU
 #define CRR_TAIL_WAVES_PER_EU 3
 #endif
-template <bool EMIT>
+// RESUME (a batch holding loaded states, CRR_IN_HAS_RESUME): a workflow the LDS arena cannot hold -- it
+// outgrew it, or resumes a loaded state -- is replayed again over its HBM rows in the same wavefront.
+// Otherwise such a workflow (the host's bounds route the ones expected to outgrow to the big segment) goes
+// to the retry pass's wave list: without the HBM-row instantiation in the kernel the tail needs 87
+// VGPRs instead of 168 with 141 VGPRs of scratch spills, and fewer scalar spills (236 vs 302).
+// The big segment's blocks need 65 KB of LDS each; once the tail's thousands of 13-KB wavefronts hold the
+// CUs, a big block queued behind them waits for tail wavefronts to finish (config 4: the group at 9.4 ms
+// instead of 5.6 in about one launch in ten, whichever hardware queue won the dispatch race).  The tail's
+// stream therefore runs this one-wavefront gate first: it returns once every big block has counted itself
+// in (or after ~10 ms, a bound every wave reaches).  The counter is reset by the retry pass.
+__global__ void __launch_bounds__(64) tail_gate_kernel(const u32* scratch, u32 need) {
+  if (threadIdx.x != 0) return;
+  const u32* counter = scratch + kScratchGate;
+  for (u32 i = 0; i < (1u << 16); ++i) {  // ~10 ms at most (a poll is ~140 ns)
+    if (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(crr_inputs in, crr_outputs out, int phase,
                                                                              u32 lo, u32 hi) {
   const u32* crc_tables = kCrcGlobal.v;
   __shared__ WaveTier<LargeTier>::Arena arena;
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
-  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, -1>> T;
+  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, RESUME ? -1 : 1>> T;
   T.S.M = &arena;
   Digest D;
   replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables, D);
-  if (T.retried) {
-    WaveTables<HbmRows> H;
-    replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables, D);
+  if constexpr (RESUME) {
+    if (T.retried) {
+      WaveTables<HbmRows> H;
+      replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables, D);
+    }
   }
   digest_flush(out, D);
 }
-template __global__ void replay_tail_kernel<false>(crr_inputs, crr_outputs, int, u32, u32);
-template __global__ void replay_tail_kernel<true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_tail_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_tail_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_tail_kernel<false, true>(crr_inputs, crr_outputs, int, u32, u32);
+template __global__ void replay_tail_kernel<true, true>(crr_inputs, crr_outputs, int, u32, u32);
 union RetryArena {
   LdsArena<HugeTier> lane;
   BigArena wave;
@@ -4223,6 +4296,7 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
       __hip_atomic_store(out.scratch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(out.scratch + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(out.scratch + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out.scratch + kScratchGate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

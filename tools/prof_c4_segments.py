@@ -70,7 +70,7 @@ def main():
         db.tensors["wf"][:wf.nbytes].copy_(torch.from_numpy(wf.view(np.uint8)))
         eng.lib.crr_segment_timing(1)
         wp = getattr(eng.lib, "crr_wave_prof", None) if a.wave_prof else None
-        wbuf = np.zeros(48, np.uint64)
+        wbuf = np.zeros(64, np.uint64)
         ms, segs = [], []
         for r in range(a.reps + 1):
             db.tensors["scratch"].zero_()
@@ -101,7 +101,14 @@ def main():
                                  "per_map_op": cyc["map_op_visits"] / max(cnts["map_ops"], 1),
                                  "per_epilogue": cyc["epilogues"] / max(cnts["epilogues"], 1),
                                  "per_op": {n: {"count": w[32 + i], "cycles_each": w[16 + i] / max(w[32 + i], 1)}
-                                            for i, n in enumerate(MOPS) if w[32 + i]}}
+                                            for i, n in enumerate(MOPS) if w[32 + i]},
+                                 "wave_tables": {"act_epilogue": {"count": w[56], "cand_loads": w[48] / max(w[56], 1),
+                                                                  "wave_min": w[49] / max(w[56], 1),
+                                                                  "update": w[50] / max(w[56], 1)},
+                                                 "timer_epilogue": {"count": w[57], "cycles_each": w[51] / max(w[57], 1)},
+                                                 "act_insert": {"find_mapped": w[52] / max(w[33], 1),
+                                                                "take": w[53] / max(w[33], 1),
+                                                                "write": w[54] / max(w[33], 1)}}}
         print(json.dumps(line), flush=True)
         del db
         torch.cuda.empty_cache()

@@ -12,6 +12,9 @@ Buckets (cycles summed over every wavefront-path replay, then counts):
   4 other visits (reset points, events of slow chunks)  5 batch epilogues  6 after the walk
   8 chunks  9 map-op visits  10 other visits  11 epilogues  12 replays
   16 + op: cycles of the visits of map operation op (MOP_*), 32 + op: their count
+  48..55 (WaveTables sub-buckets): activity epilogue candidate loads, its wave minimum, its update; the
+  timer epilogue; act_insert's ActivityID lookup, its free-slot search, its row write; 56 / 57: activity /
+  timer epilogue count
 """
 import os
 import subprocess
@@ -26,9 +29,9 @@ PATCHES = [
     ("  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n",
      "  i64 batch_first_id = 0;\n  i32 last_task_step = -1;\n"
      "  u64 wp_[48] = {};\n"),
-    ("    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {\n      if (c0) src.advance(c0 >> 6);\n",
+    ("    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {\n      if (c0) src.rotate();\n",
      "    for (i32 c0 = 0; c0 < n_wave; c0 += 64) {\n      const u64 wt0_ = __builtin_readcyclecounter();\n"
-     "      if (c0) src.advance(c0 >> 6);\n"),
+     "      if (c0) src.rotate();\n"),
     ("      i32 wfail = -1;\n      int wrc = CRR_OK;\n      while (vm) {\n",
      "      i32 wfail = -1;\n      int wrc = CRR_OK;\n      const u64 wt1_ = __builtin_readcyclecounter();\n"
      "      wp_[1] += wt1_ - wt0_; wp_[8] += 1;\n      while (vm) {\n"),
@@ -52,19 +55,46 @@ PATCHES = [
     ("      if (wfail >= 0) {  // the failing event's prologue has run\n        WAVE_VH_AFTER(wfail);",
      "      { const u64 wt3_ = __builtin_readcyclecounter(); wp_[6] += wt3_ - wt2_; wp_[0] += wt3_ - wt0_; }\n"
      "      if (wfail >= 0) {  // the failing event's prologue has run\n        WAVE_VH_AFTER(wfail);"),
+    # WaveTables sub-buckets (wpx_): epilogue halves and act_insert's parts
+    ("  bool dirty_act = false, dirty_timer = false;\n\n  __device__ __forceinline__ void init() { lane = (i32)(threadIdx.x & 63); }",
+     "  bool dirty_act = false, dirty_timer = false;\n  u64 wpx_[16] = {};\n\n  __device__ __forceinline__ void init() { lane = (i32)(threadIdx.x & 63); }"),
+    ("    if (L.n_act > 0 && dirty_act) {\n      BestTimer B;\n      const i32 hwa = uniform32(hw_act);",
+     "    if (L.n_act > 0 && dirty_act) {\n      const u64 e0_ = __builtin_readcyclecounter();\n      BestTimer B;\n      const i32 hwa = uniform32(hw_act);"),
+    ("      wave_min(B);\n      i32 attempt = 0;",
+     "      const u64 e1_ = __builtin_readcyclecounter(); wpx_[0] += e1_ - e0_;\n      wave_min(B);\n"
+     "      const u64 e2_ = __builtin_readcyclecounter(); wpx_[1] += e2_ - e1_; wpx_[8] += 1;\n      i32 attempt = 0;"),
+    ("      if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, (i32)bcast(B.j, (u32)attempt), -1);\n    }",
+     "      if (B.have && !B.created) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, B.y, L.current_version, B.t, B.e, (i32)bcast(B.j, (u32)attempt), -1);\n"
+     "      wpx_[2] += __builtin_readcyclecounter() - e2_;\n    }"),
+    ("    if (L.n_timer > 0 && dirty_timer) {\n      BestTimer B;\n      const i32 hwt = uniform32(hw_timer);",
+     "    const u64 et0_ = __builtin_readcyclecounter();\n    const bool tdo_ = L.n_timer > 0 && dirty_timer;\n"
+     "    if (L.n_timer > 0 && dirty_timer) {\n      BestTimer B;\n      const i32 hwt = uniform32(hw_timer);"),
+    ("    dirty_timer = false;\n  }\n  __device__ __forceinline__ bool task_writer() const { return lane == 0; }",
+     "    if (tdo_) { wpx_[3] += __builtin_readcyclecounter() - et0_; wpx_[9] += 1; }\n"
+     "    dirty_timer = false;\n  }\n  __device__ __forceinline__ bool task_writer() const { return lane == 0; }"),
+    ("    const i32 m = find_act_mapped(row.key);\n    const i32 j = take(A_(), hw_act, ST::A, G.act_cap);\n    if (j < 0) return -j;",
+     "    const u64 i0_ = __builtin_readcyclecounter();\n    const i32 m = find_act_mapped(row.key);\n"
+     "    const u64 i1_ = __builtin_readcyclecounter(); wpx_[4] += i1_ - i0_;\n"
+     "    const i32 j = take(A_(), hw_act, ST::A, G.act_cap);\n"
+     "    const u64 i2_ = __builtin_readcyclecounter(); wpx_[5] += i2_ - i1_;\n    if (j < 0) return -j;"),
+    ("    act_cand_store(j, row);\n    ++L.n_act;\n    dirty_act = true;\n    return CRR_OK;",
+     "    act_cand_store(j, row);\n    ++L.n_act;\n    dirty_act = true;\n    wpx_[6] += __builtin_readcyclecounter() - i2_;\n    return CRR_OK;"),
     # flush at the end of the replay (lane 0 of a wavefront-path replay)
     ("  out.exec[w] = R;\n",
      "  out.exec[w] = R;\n"
      "  if constexpr (" + WAVE + ") {\n"
      "    if ((threadIdx.x & 63) == 0 && wp_[8]) { wp_[12] = 1;\n"
-     "      for (int q_ = 0; q_ < 48; ++q_) atomicAdd(&g_wave_prof[q_], (unsigned long long)wp_[q_]); }\n"
+     "      for (int q_ = 0; q_ < 48; ++q_) atomicAdd(&g_wave_prof[q_], (unsigned long long)wp_[q_]);\n"
+     "      if constexpr (WaveWpx<P>::value) for (int q_ = 0; q_ < 16; ++q_) atomicAdd(&g_wave_prof[48 + q_], (unsigned long long)T.wpx_[q_]); }\n"
      "  }\n"),
     # the device array and its reader
     ("// ---- the job's digest, folded into the replay",
-     "__device__ unsigned long long g_wave_prof[48];\n"
+     "__device__ unsigned long long g_wave_prof[64];\n"
+     "template <class P, class = void> struct WaveWpx { static constexpr bool value = false; };\n"
+     "template <class P> struct WaveWpx<P, decltype((void)&P::wpx_)> { static constexpr bool value = true; };\n"
      "extern \"C\" int crr_wave_prof(unsigned long long* host, int reset) {\n"
      "  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_prof), sizeof(g_wave_prof)) != hipSuccess) return -1;\n"
-     "  if (reset) { unsigned long long z[48] = {}; if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z)) != hipSuccess) return -1; }\n"
+     "  if (reset) { unsigned long long z[64] = {}; if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z)) != hipSuccess) return -1; }\n"
      "  return 0;\n}\n"
      "// ---- the job's digest, folded into the replay"),
 ]

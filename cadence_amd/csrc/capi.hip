@@ -329,10 +329,11 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
       if (in->flags & CRR_IN_TIERED) {
         // segments by expected live-set size: 1 entry per map | 2 | compact tiers 1-3 | more (HBM rows)
         auto clampb = [&](uint32_t b, uint32_t lo) { return b < lo ? lo : (b < n_lane ? b : n_lane); };
-        // loaded states (CRR_IN_HAS_RESUME) continue in the compact tiers' arenas (the 1- and 2-slot tiers
-        // rebuild rows from this call's events only): their segments join compact tier 1, which holds both
+        // loaded states (CRR_IN_HAS_RESUME) continue in the compact tiers' arenas; the host places them there
+        // (flatten.resumed_bounds), so the 1- and 2-slot segments keep their fast kernels for the batch's fresh
+        // workflows (a loaded state found in one goes to the general path: speed only)
         const bool resume = (in->flags & CRR_IN_HAS_RESUME) != 0;
-        const uint32_t lb = resume ? 0u : clampb(in->large_begin, 0), cb = resume ? 0u : clampb(in->compact_begin, lb);
+        const uint32_t lb = clampb(in->large_begin, 0), cb = clampb(in->compact_begin, lb);
         const uint32_t c2 = clampb(in->compact2_begin, cb), wb = clampb(in->wide_begin, c2);
         const uint32_t hb = clampb(in->hbm_begin, wb);
         const bool run_small = lb > 0, run_large = cb > lb, run_tail = tail && tail_end > n_lane;

@@ -3255,15 +3255,44 @@ struct Digest {
     v[6] = (i64)((u64)v[6] + (ok ? 0ull : (key ^ fw)));
   }
 };
+// The digest's pointers, read from the kernel arguments where they are used: held from the kernel's start
+// they take four of the replay loop's scalar registers (config 2's kernel: 31 scalar spills and 2 vector
+// ones instead of 10 and none; the digest on cost its kernel ~2 %).  Every kernel that folds a digest takes
+// (crr_inputs in, crr_outputs out, ...) first; the kernel-argument segment lays them out in that order at
+// their natural alignment.
+constexpr size_t kKernargOut = (sizeof(crr_inputs) + alignof(crr_outputs) - 1) / alignof(crr_outputs) * alignof(crr_outputs);
+// (a volatile read of the constant segment: a scalar load at the point of use, not merged with the kernel
+// start's)
+typedef const __attribute__((address_space(4))) char* kernarg_ptr;
+template <class T>
+__device__ __forceinline__ T kernarg_late(size_t off) {
+  kernarg_ptr ka = (kernarg_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+  return *reinterpret_cast<const volatile __attribute__((address_space(4))) T*>(ka + off);
+}
+__device__ __forceinline__ int64_t* digest_ptr() { return kernarg_late<int64_t*>(kKernargOut + offsetof(crr_outputs, digest)); }
+__device__ __forceinline__ const uint64_t* digest_keys_ptr() {
+  return kernarg_late<const uint64_t*>(offsetof(crr_inputs, digest_keys));
+}
 // every lane of the wavefront active (a kernel's last statement, after its per-workflow work returned)
-__device__ __forceinline__ void digest_flush(const crr_outputs& out, const Digest& D) {
-  if (!out.digest) return;
-  unsigned long long* dst = reinterpret_cast<unsigned long long*>(out.digest + (blockIdx.x % CRR_DIGEST_STRIPES) * CRR_DIGEST_STRIDE);
+__device__ __forceinline__ void digest_flush(const crr_outputs&, const Digest& D) {
+  int64_t* const digest = digest_ptr();
+  if (!digest) return;
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(digest + (blockIdx.x % CRR_DIGEST_STRIPES) * CRR_DIGEST_STRIDE);
+  // (a field zero in every lane -- the failure terms of an all-OK wavefront -- is skipped; one whose lanes all
+  // hold less than 2^26 is summed in 32 bits: one crossbar shuffle per level instead of two)
 #pragma unroll
   for (int k = 0; k < CRR_DIGEST_FIELDS; ++k) {
     u64 x = (u64)D.v[k];
+    if (__builtin_amdgcn_ballot_w64(x != 0) == 0) continue;
+    if (__builtin_amdgcn_ballot_w64(x >= (1ull << 26)) == 0) {
+      u32 y = (u32)x;
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) x += (u64)__shfl_xor((long long)x, off, 64);
+      for (int off = 32; off >= 1; off >>= 1) y += (u32)__shfl_xor((int)y, off, 64);
+      x = y;
+    } else {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) x += (u64)__shfl_xor((long long)x, off, 64);
+    }
     if ((threadIdx.x & 63) == 0 && x != 0) atomicAdd(dst + k, x);
   }
 }
@@ -3751,6 +3780,10 @@ done_events:
   bool want_crc = L.status == CRR_OK;
   TokenWords TW;
   TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
+  // the workflow's digest key with them: read before the loop it would be held across it (registers the
+  // loop spills for), read at the add its round trip would end every wavefront
+  u64 dkey = 0;
+  if (dg && digest_ptr()) dkey = digest_keys_ptr()[w];
   // the wave path's items were written by the lanes of their events; the checksum reads them all
   if constexpr (std::is_same<SRC, WaveSource>::value) wave_sync_global();
   if (L.vh_n > 0) {
@@ -3816,8 +3849,8 @@ done_events:
   CRR_PHASE(5);
   out.exec[w] = R;
   // the digest's terms: one lane per workflow (the wave path's lanes all hold the same result)
-  if (dg && out.digest && (!std::is_same<SRC, WaveSource>::value || (threadIdx.x & 63) == 0))
-    dg->add(R, n_ev, in.digest_keys[w]);
+  if (dg && digest_ptr() && (!std::is_same<SRC, WaveSource>::value || (threadIdx.x & 63) == 0))
+    dg->add(R, n_ev, dkey);
 #if CRR_PHASE_PROF
   if constexpr (!std::is_same<SRC, WaveSource>::value) {
     if ((wfp->flags & CRR_WF_FLAG_RESUME) && (threadIdx.x & 63) == 0 && ph[1] != 0) {
@@ -4135,10 +4168,11 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables,
                                                              RESUME ? &X0 : nullptr, &D);
 }
-// register budgets (waves per SIMD): tier 1's 14-KB blocks fit 11 per CU, so 3 waves/SIMD is the LDS
-// limit too; tier 2's 28-KB blocks fit 5 (LDS-limited below 2)
+// register budgets (waves per SIMD): tier 1's 10-KB blocks would fit 15 per CU, but at 3 waves/SIMD (168
+// VGPRs) its loop spills 24 VGPRs (156 B/lane of scratch); at 2 (256 VGPRs) none, and the config-3 shard
+// replays 2.55-2.59 ms against 2.60-2.66 (round 5, alternated A/B on one box); tier 2's 20-KB blocks fit 8
 #ifndef CRR_COMPACT1_WAVES_PER_EU
-#define CRR_COMPACT1_WAVES_PER_EU 3
+#define CRR_COMPACT1_WAVES_PER_EU 2
 #endif
 // the resume instantiation at 2: its loaded-row reads and in-place finalize spill at 168 VGPRs
 #ifndef CRR_COMPACT1_RESUME_WAVES_PER_EU

@@ -601,6 +601,7 @@ COMPACT_MAX_EVENTS = 1023
 # tier classes 0..4; WIDE: HBM rows
 TIER_SLOTS = [SMALL_TIER, LARGE_TIER, COMPACT1_TIER, COMPACT2_TIER, COMPACT3_TIER]
 WIDE = len(TIER_SLOTS)
+COMPACT_FIRST = 2  # TIER_SLOTS index of compact tier 1
 
 
 def _pair_keys(a: np.ndarray, b: np.ndarray) -> np.ndarray:
@@ -690,6 +691,9 @@ WAVE_SMALL_TIER = {"act": 40, "timer": 32, "child": 16, "rc": 8, "sig": 8, "rp":
 WAVE_BIG_CAPS = {"act": 64, "timer": 64, "child": 64, "rc": 64, "sig": 64, "rp": 64}
 
 
+# the event ID each table's rows are keyed by (CompactTables::load's virtual steps)
+LOADED_ID = {"act": "schedule_id", "timer": "started_id", "child": "initiated_id", "rc": "initiated_id",
+             "sig": "initiated_id"}
 LOADED_COUNT = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "rc": "n_rc", "sig": "n_signal",
                 "rp": "n_reset_points"}
 
@@ -697,8 +701,10 @@ LOADED_COUNT = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "rc
 def resumed_bounds(batch: HistoryBatch, bounds: Dict[str, np.ndarray], resumed: np.ndarray):
     """Live-set bounds and tier classes with the loaded states counted in: a resumed workflow's bound is
     its loaded rows plus this batch's growth (deletes of loaded entries not subtracted: an upper bound).
-    The compact tiers also need the whole history's event IDs to fit their 10-bit steps (the loaded
-    entries' IDs sit below NextEventID; CompactTables::load hands anything else to the general path)."""
+    The compact tiers hold a loaded entry as a virtual step below vk = COMPACT_MAX_EVENTS - ev_count
+    (CompactTables::load: its ID must lie in [NextEventID - vk, NextEventID)), so a resumed workflow goes
+    there when its oldest live loaded ID does -- however long the history before it; CompactTables::load
+    still hands anything else to the general path."""
     ex = batch.init.exec if batch.init is not None else None
     out = {}
     for m, v in bounds.items():
@@ -706,11 +712,46 @@ def resumed_bounds(batch: HistoryBatch, bounds: Dict[str, np.ndarray], resumed: 
         out[m] = np.where(resumed, v + add, v)
     tier = tier_classes(batch, out)
     if ex is not None:
-        span = ex["next_event_id"].astype(np.int64) + batch.wf["ev_count"].astype(np.int64)
-        tier = np.where(resumed & (span > COMPACT_MAX_EVENTS), WIDE, tier)
+        nei = ex["next_event_id"].astype(np.int64)
+        vk = COMPACT_MAX_EVENTS - batch.wf["ev_count"].astype(np.int64)
+        oldest = nei.copy()  # no live loaded entry: nothing to place below vk
+        for name, id_f in LOADED_ID.items():
+            rows = batch.init.rows.get(name)
+            c = batch.init.counts(name)
+            if rows is None or not c.sum():
+                continue
+            np.minimum.at(oldest, np.repeat(np.arange(batch.n_wf), c), rows[id_f].astype(np.int64))
+        tier = np.where(resumed & ((vk <= 0) | (nei - oldest > vk)), WIDE, tier)
     else:
         tier = np.where(resumed, WIDE, tier)
+    # the 1- and 2-slot tiers rebuild rows from this call's events only: a resumed workflow they would
+    # hold takes the smallest compact tier that does, so those segments keep their fast kernels for the
+    # batch's fresh workflows (the device hands a loaded state found there to the general path)
+    low = resumed & (tier < COMPACT_FIRST)
+    if low.any():
+        ok = _compact_ok(batch)
+        cls = np.full(batch.n_wf, WIDE, np.int64)
+        for k in range(WIDE - 1, COMPACT_FIRST - 1, -1):
+            fit = ok.copy()
+            for m, cap in TIER_SLOTS[k].items():
+                fit &= out[m] <= cap
+            cls = np.where(fit, k, cls)
+        tier = np.where(low, cls, tier)
     return out, tier
+
+
+def _compact_ok(batch: HistoryBatch) -> np.ndarray:
+    """Workflows the compact encodings can take: <= COMPACT_MAX_EVENTS events, event IDs below 2^32."""
+    cnt = batch.wf["ev_count"].astype(np.int64)
+    ok = cnt <= COMPACT_MAX_EVENTS
+    if batch.n_events:
+        st = batch.wf_strides()
+        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + (
+            np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)) * np.repeat(st, cnt)
+        big_id = np.zeros(batch.n_wf, bool)
+        np.logical_or.at(big_id, np.repeat(np.arange(batch.n_wf), cnt), batch.cols["event_id"][idx] > 0xFFFFFFFF)
+        ok &= ~big_id
+    return ok
 
 
 def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:
@@ -719,15 +760,7 @@ def tier_classes(batch: HistoryBatch, bounds: Optional[Dict[str, np.ndarray]] = 
     below 2^32 (their encodings; the kernel hands anything else to the general path anyway)."""
     b = live_set_bounds(batch) if bounds is None else bounds
     cls = np.full(batch.n_wf, WIDE, np.int64)
-    cnt = batch.wf["ev_count"].astype(np.int64)
-    compact_ok = cnt <= COMPACT_MAX_EVENTS
-    if batch.n_events:
-        st = batch.wf_strides()
-        idx = np.repeat(batch.wf["ev_begin"].astype(np.int64), cnt) + (
-            np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)) * np.repeat(st, cnt)
-        big_id = np.zeros(batch.n_wf, bool)
-        np.logical_or.at(big_id, np.repeat(np.arange(batch.n_wf), cnt), batch.cols["event_id"][idx] > 0xFFFFFFFF)
-        compact_ok &= ~big_id
+    compact_ok = _compact_ok(batch)
     for k in range(WIDE - 1, -1, -1):
         fit = np.ones(batch.n_wf, bool)
         for m, cap in TIER_SLOTS[k].items():

@@ -148,6 +148,10 @@ class PassiveReplication:
             dn.c_in.large_begin = dn.c_in.compact_begin = dn.c_in.compact2_begin = dn.c_in.wide_begin = 0
             dn.c_in.hbm_begin = 0
             dn.c_in.flags &= ~(abi.IN_LDS_SMALL | abi.IN_HAS_RESUME)
+        elif sb.tiers is not None:
+            # every workflow resumes, and the 1- and 2-slot tiers rebuild rows from this call's events only:
+            # their segments join compact tier 1 (whose bounds hold theirs)
+            dn.c_in.large_begin = dn.c_in.compact_begin = 0
         for name, *_ in abi.TABLES:                # only db's outputs are used
             dn.tensors.pop("out_" + name, None)
         dn.tensors.pop("exec", None)

@@ -308,10 +308,11 @@ typedef struct crr_inputs {
          [0, large_begin)               <= 1 pending entry per map             (1-slot LDS tier)
          [large_begin, compact_begin)   <= 2 activities / timers / reset points (2-slot LDS tier)
          [compact_begin, compact2_begin) compact tier 1 (4 / 3 / 2 / 1 / 1 / 4 slots)
-         [compact2_begin, wide_begin)    compact tier 2 (8 / 6 / 3 / 3 / 3 / 8 slots)
-         [wide_begin, hbm_begin)         compact tier 3 (16 / 12 / 8 / 6 / 6 / 10 slots)
-         [hbm_begin, lanes)              more: the workflow's own HBM rows (a loaded state,
-                                         CRR_WF_FLAG_RESUME, stays in its segment with CRR_IN_HAS_RESUME)
+         [compact2_begin, wide_begin)    compact tier 2 (8 / 5 / 3 / 3 / 3 / 8 slots)
+         [wide_begin, hbm_begin)         compact tier 3 (12 / 8 / 6 / 4 / 4 / 8 slots)
+         [hbm_begin, lanes)              more: the workflow's own HBM rows
+       (a loaded state, CRR_WF_FLAG_RESUME, belongs in a compact segment or [hbm_begin, lanes): the 1- and
+       2-slot tiers rebuild rows from this call's events only and hand one to the general path)
        (hbm_begin below wide_begin, e.g. 0, reads as wide_begin: no compact tier 3 segment)
        (activity / timer / child / request-cancel / signal / reset-point slots; flatten.py) */
     uint32_t                 large_begin;
@@ -342,10 +343,10 @@ typedef struct crr_inputs {
 #define CRR_IN_ADVANCED_VISIBILITY 64u /* config.AdvancedVisibilityWritingMode != off: RefreshTasks also emits
                                    the search-attributes task (mutable_state_task_refresher.go:160-167) */
 #define CRR_IN_HAS_RESUME 32u   /* some workflow carries CRR_WF_FLAG_RESUME (CRR_IN_TIERED batches): the
-                                   compact tiers continue loaded states in their LDS arenas, and the 1- and
-                                   2-slot segments [0, compact_begin) join compact tier 1 (which holds
-                                   both).  Without it a loaded state in an LDS segment is replayed by the
-                                   general path over its HBM rows: speed only, never results */
+                                   compact tiers (and the long-tail kernel) run the instantiations that
+                                   continue loaded states.  Without it -- or for a loaded state in the 1- or
+                                   2-slot segments -- the general path replays it over its HBM rows: speed
+                                   only, never results */
 
 /* ---- output rows ---------------------------------------------------------------------------- */
 /* WorkflowExecutionInfo numeric image + engine status (208 B).  "step" / "*_src" values below are

@@ -69,6 +69,27 @@ def test_resume_passive_replication_last_batch(engine):
     assert n > 2500
 
 
+def test_resume_old_histories_in_the_compact_window(engine):
+    """Histories past the compact encodings' 1023 steps whose live loaded entries are recent resume in the
+    compact tiers (the virtual-step window [NextEventID - vk, NextEventID), flatten.resumed_bounds); the
+    rest take the HBM-row segment, or the general path when CompactTables::load finds an entry outside it."""
+    from cadence_amd import abi
+    from cadence_amd import flatten as fl
+    caps = {"act": 3, "timer": 2, "child": 1, "rc": 1, "sig": 1}  # live sets a compact tier holds
+    hs = synth_mixed.long_tail_histories(600, 64, min_len=200, max_len=3000, run_cap=3000, multi_version=True,
+                                         caps=caps)
+    pre, suf, mask = split_histories(hs, 8, last_only=True)
+    pre_b = interleave(flatten(pre, known_domains=KNOWN))
+    loaded = loaded_from(pre_b, engine.replay(pre_b), mask)
+    suf_b = flatten(suf, known_domains=KNOWN, loaded=loaded)
+    resumed = (suf_b.wf["flags"] & abi.WF_FLAG_RESUME) != 0
+    _, tier = fl.resumed_bounds(suf_b, fl.live_set_bounds(suf_b), resumed)
+    old = resumed & (loaded.exec["next_event_id"] > fl.COMPACT_MAX_EVENTS)
+    assert (old & (tier < fl.WIDE)).sum() > 20 and (old & (tier == fl.WIDE)).sum() > 0
+    loaded2, n = _device_split(engine, hs, 8, interleave, last_only=True)
+    assert n > 50   # Load-stable and equal to the one-shot replay (90 on this seed); every workflow equals the oracle
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("native", [False, True])
 def test_passive_replication_in_place_matches_one_shot(native):

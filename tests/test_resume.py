@@ -92,3 +92,44 @@ def test_resume_empty_batch_keeps_loaded_state():
     assert r2["status"] == abi.Status.EMPTY_HISTORY and r2["fail_step"] == 2
     assert r2["current_version"] == abi.EMPTY_VERSION
     assert r2["next_event_id"] == 3 and r2["decision_schedule_id"] == 2
+
+
+def test_resumed_tiering_follows_the_loaded_id_window():
+    """A resumed workflow takes a compact tier when its live loaded IDs fit the virtual-step window
+    [NextEventID - vk, NextEventID), vk = COMPACT_MAX_EVENTS - ev_count (CompactTables::load), however long
+    its history: the same states shifted 5000 event IDs later keep their tiers, and a live entry older than
+    the window sends its workflow to the HBM-row segment."""
+    import dataclasses
+    from cadence_amd import flatten as fl
+    hs = synth_mixed.mixed_histories(300, 54, multi_version=True)
+    pre, suf, mask = split_histories(hs, 4, last_only=True)
+    pre_b = flatten(pre, known_domains=KNOWN)
+    loaded = loaded_from(pre_b, oracle.replay(pre_b, 2), mask)
+    suf_b = flatten(suf, known_domains=KNOWN, loaded=loaded)
+    resumed = (suf_b.wf["flags"] & abi.WF_FLAG_RESUME) != 0
+    bounds = fl.live_set_bounds(suf_b)
+    _, base = fl.resumed_bounds(suf_b, bounds, resumed)
+    with_act = resumed & (loaded.counts("act") > 0)
+    assert with_act.sum() > 20 and (base[with_act] < fl.WIDE).any()
+    # every loaded ID and NextEventID 5000 later: the window moves with them
+    ex = loaded.exec.copy()
+    ex["next_event_id"][loaded.mask] += 5000
+    rows = {n: r.copy() for n, r in loaded.rows.items()}
+    for n, f in fl.LOADED_ID.items():
+        if n in rows and len(rows[n]):
+            rows[n][f] += 5000
+    shifted = dataclasses.replace(suf_b, init=dataclasses.replace(loaded, exec=ex, rows=rows))
+    _, t2 = fl.resumed_bounds(shifted, bounds, resumed)
+    assert (t2 == base).all()
+    # one live activity older than the window
+    c = loaded.counts("act")
+    off = np.cumsum(c) - c
+    w = int(np.nonzero(with_act & (base < fl.WIDE))[0][0])
+    rows2 = {n: r.copy() for n, r in loaded.rows.items()}
+    vk = fl.COMPACT_MAX_EVENTS - int(suf_b.wf["ev_count"][w])
+    rows2["act"]["schedule_id"][off[w]] = int(loaded.exec["next_event_id"][w]) - vk - 1
+    old = dataclasses.replace(suf_b, init=dataclasses.replace(loaded, rows=rows2))
+    _, t3 = fl.resumed_bounds(old, bounds, resumed)
+    assert t3[w] == fl.WIDE
+    t3[w] = base[w]
+    assert (t3 == base).all()

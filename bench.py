@@ -284,7 +284,21 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
            "setup_s": {"generate": t1 - t0, "interleave": t2 - t1}}
     if ctx.rank == 0:
         out["parity_sample"] = parity_sample(ctx, sample_fn, long_threshold)
+        out["parity_full"] = full_parity(ctx, batch, res, canon)
     return out, batch, res, db
+
+
+def full_parity(ctx, batch, res, canon):
+    """The timed replays' own results -- every workflow of the rank's shard, every row -- against the oracle
+    (outside the clock)."""
+    from oracle import oracle
+    from cadence_amd.result import diff_results
+    t0 = time.perf_counter()
+    ref = oracle.replay(canon, host_cpus())
+    dt = time.perf_counter() - t0
+    d = diff_results(batch, res, canon, ref)
+    return {"workflows": canon.n_wf, "events": canon.n_events, "bit_exact": not d, "first_diffs": d[:3],
+            "oracle_s": dt}
 
 
 def parity_sample(ctx, sample_fn, long_threshold):

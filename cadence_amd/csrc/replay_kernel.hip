@@ -3297,6 +3297,41 @@ __device__ __forceinline__ void digest_flush(const crr_outputs&, const Digest& D
   }
 }
 
+// The same over a block of kWavesPerBlock wavefronts (the LDS kernels' 256 threads): the wavefront sums meet
+// in LDS and one wavefront adds the block's -- a quarter of the atomics (measured on config 2's kernel: the
+// digest's atomics ~1 % of it, its reductions ~0.5-1 %, the per-workflow terms ~0.5 %).  Every thread of
+// the block calls it (a kernel's last statement).
+__device__ __forceinline__ void digest_flush_block(const crr_outputs&, const Digest& D) {
+  int64_t* const digest = digest_ptr();
+  if (!digest) return;
+  __shared__ u64 part[kWavesPerBlock][CRR_DIGEST_FIELDS];
+  const u32 wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < CRR_DIGEST_FIELDS; ++k) {
+    u64 x = (u64)D.v[k];
+    if (__builtin_amdgcn_ballot_w64(x != 0) != 0) {
+      if (__builtin_amdgcn_ballot_w64(x >= (1ull << 26)) == 0) {
+        u32 y = (u32)x;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) y += (u32)__shfl_xor((int)y, off, 64);
+        x = y;
+      } else {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x += (u64)__shfl_xor((long long)x, off, 64);
+      }
+    }
+    if (lane == 0) part[wv][k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < CRR_DIGEST_FIELDS) {
+    u64 x = 0;
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; ++i) x += part[i][threadIdx.x];
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(digest + (blockIdx.x % CRR_DIGEST_STRIPES) * CRR_DIGEST_STRIDE);
+    if (x != 0) atomicAdd(dst + threadIdx.x, x);
+  }
+}
+
 // pre_x: the workflow's exec row already read by the caller (a kernel that expects loaded states issues it
 // with the descriptor, one round trip earlier), else nullptr.  dg: the lane's digest terms (nullptr: none).
 template <bool EMIT, class P, class SRC>
@@ -3970,13 +4005,13 @@ template <bool WAVE_TAIL, bool EMIT, bool LANES = false>
 __global__ void __launch_bounds__(kBlock, EMIT ? 2 : CRR_SMALL_WAVES_PER_EU) replay_lds_small_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   Digest D;
   replay_lds<SmallTier, WAVE_TAIL, EMIT, LANES>(in, out, phase, lo, hi, D);
-  digest_flush(out, D);
+  digest_flush_block(out, D);
 }
 template <bool WAVE_TAIL, bool EMIT>
 __global__ void __launch_bounds__(kBlock) replay_lds_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   Digest D;
   replay_lds<LargeTier, WAVE_TAIL, EMIT>(in, out, phase, lo, hi, D);
-  digest_flush(out, D);
+  digest_flush_block(out, D);
 }
 template __global__ void replay_lds_small_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_lds_small_kernel<false, false, true>(crr_inputs, crr_outputs, int, u32, u32);

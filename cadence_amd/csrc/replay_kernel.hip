@@ -4154,19 +4154,9 @@ template <int TIER_NO, bool RESUME>
 struct CompactLdsCrc {
   static constexpr bool value = ((CRR_COMPACT_LDS_CRC_MASK >> ((TIER_NO - 1) + (RESUME ? 0 : 3))) & 1) != 0;
 };
-// Wave priority (s_setprio) of the small segments whose lanes run long serial histories next to the
-// long-tail wavefronts (config 4: compact tiers 2 / 3 hold ~200 workflows of up to 243 events, three
-// wavefronts each, and share their SIMDs with tail wavefronts: 0.94 ms alone, 4.5-4.8 ms in the group)
-#ifndef CRR_PRIO_C23
-#define CRR_PRIO_C23 0
-#endif
-#ifndef CRR_PRIO_BIG
-#define CRR_PRIO_BIG 0
-#endif
 template <class TIER, bool EMIT, bool RESUME, int TIER_NO>
 __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_outputs& out, int phase, u32 lo, u32 hi,
                                                Digest& D) {
-  if constexpr (TIER_NO >= 2 && CRR_PRIO_C23 > 0) __builtin_amdgcn_s_setprio(CRR_PRIO_C23);
   __shared__ CompactArena<TIER> arena;
   const u32* crc_tables = kCrcGlobal.v;
   const u32 w = lo + blockIdx.x * 64u + threadIdx.x;
@@ -4259,7 +4249,6 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
   if (threadIdx.x == 0) atomicAdd(out.scratch + kScratchGate, 1u);
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
-  if constexpr (CRR_PRIO_BIG > 0) __builtin_amdgcn_s_setprio(CRR_PRIO_BIG);
   build_crc_tables(crc_tables);
   WaveTables<LdsRows<BigArena, -1>> T;
   T.S.M = &arena;

@@ -256,11 +256,11 @@ def config_traffic(name, n_wf, n_events):
     return None
 
 
-def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
-    """One non-headline line: generate this rank's shard, time `config_steps` replays, roofline over the
-    launch group, parity of a sample against the oracle (rank 0)."""
+def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256, global_ids=None):
+    """One non-headline line: generate this rank's shard, time `config_steps` replays (each with the fused
+    digest and, N > 1, its RCCL all-reduce: BASELINE config 3's "RCCL checksum reduce"), roofline over the
+    launch group, parity of the timed replays' own rows and of a sample against the oracle (rank 0)."""
     from cadence_amd import synth
-    from cadence_amd import dist as cdist
     from cadence_amd.flatten import interleave
     args, torch, eng = ctx.args, ctx.torch, ctx.eng
     t0 = time.time()
@@ -269,16 +269,19 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
     batch = interleave(canon, long_threshold=long_threshold)
     t2 = time.time()
     db = eng.upload(batch)
-    wall, ms = timed_steps(ctx, db, args.config_steps, 1)
+    keys = digest_keys(ctx, batch, global_ids)
+    eng.enable_digest(db, keys)
+    wall, ms = timed_steps(ctx, db, args.config_steps, 1, per_step=digest_exchange(ctx, db))
     res = eng.download(db)
-    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"], cdist.device_keys(batch))
-    tot_events, tot_wf, tot_ok = ctx.reduce([float(batch.n_events), float(batch.n_wf), float(digest[1])], op="sum")
+    dg = digest_check(ctx, db, res, batch, keys)
+    tot_events, tot_wf = ctx.reduce([float(batch.n_events), float(batch.n_wf)], op="sum")
     grp_ms = float(np.mean(ms))
     out = {"workload": workload, "value": tot_events * args.config_steps / wall, "unit": "events/s",
            "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
-           "workflows_per_gpu": batch.n_wf, "events_per_gpu": batch.n_events, "workflows_ok": int(tot_ok),
+           "workflows_per_gpu": batch.n_wf, "events_per_gpu": batch.n_events, "workflows_ok": dg["digest"][1],
            "workflows_per_s": tot_wf * args.config_steps / wall,
            "tiers": list(batch.tiers) if batch.tiers else None, "wave_tail": batch.n_wf - (batch.wave_begin or batch.n_wf),
+           "digest": dg,
            "roofline": roofline(synth.algorithmic_bytes(batch, res), grp_ms, FAST_GROUP,
                                 config_traffic(name, batch.n_wf, batch.n_events)),
            "setup_s": {"generate": t1 - t0, "interleave": t2 - t1}}
@@ -286,6 +289,44 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256):
         out["parity_sample"] = parity_sample(ctx, sample_fn, long_threshold)
         out["parity_full"] = full_parity(ctx, batch, res, canon)
     return out, batch, res, db
+
+
+def digest_keys(ctx, batch, global_ids=None):
+    """Identity keys of the batch's workflows in device order: the global workflow IDs of this rank's part
+    of the job (the generator's shard split, dist.rank_workflows) when they are known and match the batch,
+    else rank-qualified local indices (still unique across ranks)."""
+    from cadence_amd import dist as cdist
+    if global_ids is None or len(global_ids) != batch.n_wf:
+        global_ids = (np.int64(ctx.rank) << np.int64(40)) + np.arange(batch.n_wf, dtype=np.int64)
+    return cdist.device_keys(batch, global_ids)
+
+
+def digest_exchange(ctx, db):
+    """The step's exchange at N > 1: the one RCCL all-reduce of the fused digest's 1-KB buffer."""
+    if ctx.world == 1:
+        return None
+    from cadence_amd import dist as cdist
+    return lambda: cdist.all_reduce_digest(ctx.torch, ctx.dist, db.tensors["digest"])
+
+
+def digest_check(ctx, db, res, batch, keys):
+    """The last timed step's (all-reduced) device digest against the host restatement of the same rows
+    (dist.digest_numpy per rank, summed over the ranks as int64)."""
+    from cadence_amd import dist as cdist
+    got = ctx.eng.read_digest(db)
+    want = cdist.digest_numpy(res.exec, batch.wf["ev_count"], keys)
+    if ctx.world > 1:
+        torch = ctx.torch
+        t = torch.from_numpy(want.copy())
+        if ctx.backend == "nccl":
+            t = t.to(ctx.eng.dev)
+        ctx.dist.all_reduce(t, op=ctx.dist.ReduceOp.SUM)
+        want = t.cpu().numpy()
+    return {"digest": [int(x) for x in got], "matches_host_digest": bool((got == want).all()),
+            "fields": "events_ok, workflows_ok, workflows_failed, crc_sum, identity_fold, inconsistencies, failed_fold",
+            "reduce": "fused into each timed replay launch" + (f"; one {'RCCL' if ctx.backend == 'nccl' else 'gloo'} "
+                                                                 "all-reduce of its 1-KB buffer per timed step"
+                                                                 if ctx.world > 1 else "")}
 
 
 def full_parity(ctx, batch, res, canon):
@@ -359,7 +400,7 @@ def _resume_bytes(pr):
 
 
 # ---- config 5: NDC / XDC -----------------------------------------------------------------------------------------
-def config5(ctx, n_wf, shard):
+def config5(ctx, n_wf, shard, global_ids=None):
     """BASELINE config 5 on this rank's shards: (a) multi-version mixed histories rebuilt onto a reset
     branch (Rebuild: the target branch token, the last-item check, RefreshTasks) -- failover versions at
     batch boundaries give 1-4 VersionHistory items; (b) crr_ndc_prepare over one replication task per
@@ -374,10 +415,11 @@ def config5(ctx, n_wf, shard):
     batch = interleave(canon)
     db = eng.upload(batch)
     setup = time.time() - t0
-    wall, ms = timed_steps(ctx, db, args.config_steps, 1)
+    keys = digest_keys(ctx, batch, global_ids)
+    eng.enable_digest(db, keys)
+    wall, ms = timed_steps(ctx, db, args.config_steps, 1, per_step=digest_exchange(ctx, db))
     res = eng.download(db)
-    from cadence_amd import dist as cdist
-    digest = cdist.digest_numpy(res.exec, batch.wf["ev_count"], cdist.device_keys(batch))
+    dg = digest_check(ctx, db, res, batch, keys)
     tot_ev, tot_wf = ctx.reduce([float(batch.n_events), float(batch.n_wf)], op="sum")
     out = {"workload": f"config 5: {n_wf} multi-version mixed histories per GPU rebuilt onto reset branches "
                        "(state_rebuilder.go:97-191: target branch token, last-item check, RefreshTasks), failover "
@@ -386,18 +428,14 @@ def config5(ctx, n_wf, shard):
                        "workflows_rebuilt_per_s": tot_wf * args.config_steps / wall,
                        "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
                        "events_per_gpu": batch.n_events, "workflows_per_gpu": batch.n_wf,
-                       "workflows_ok": int(digest[1]),
+                       "workflows_ok": dg["digest"][1], "digest": dg,
                        "vh_items_per_workflow": float(res.exec["n_vh_items"][res.exec["status"] == 0].mean()),
                        "roofline": roofline(synth.algorithmic_bytes(batch, res), float(np.mean(ms)), FAST_GROUP,
                                             config_traffic("config5_rebuild", batch.n_wf, batch.n_events)),
                        "setup_s": setup}}
     if ctx.rank == 0:
-        from oracle import oracle
-        from cadence_amd.result import diff_results
-        sample = as_rebuilds(synth_native.mixed(20_000, multi_version=True, seed=0xCAD00015), 0xCAD00015)
-        b = interleave(sample)
-        d = diff_results(b, eng.replay(b), sample, oracle.replay(sample, host_cpus()))
-        out["rebuild"]["parity_sample"] = {"workflows": sample.n_wf, "bit_exact": not d, "first_diffs": d[:3]}
+        # the timed replays' own rows, every workflow, against the oracle
+        out["rebuild"]["parity_full"] = full_parity(ctx, batch, res, canon)
     # (b) NDC branch decisions
     e, v, c = ndc.version_histories(canon)
     nb = ndc.tasks_from_histories(e, v, c, 0xCAD00025 + ctx.rank)
@@ -491,10 +529,18 @@ def ndc_line(ctx, nb):
                                                     ((got["status"] != 0) & (got["status"] != abi.Status.NDC_RETRY_TASK)).sum()))},
             "roofline": roofline(alg, k_ms, "crr::ndc_prepare_kernel", config_traffic("config5_ndc_prepare", n, n))}
     if ctx.rank == 0:
-        m = min(n, 200_000)
-        sub = ndc.NdcBatch(tasks=nb.tasks[:m], branches=nb.branches, items=nb.items, n_out_items=nb.n_out_items)
-        want, _ = oracle.ndc_prepare(sub)
-        line["parity_sample"] = {"tasks": m, "bit_exact": bool((got[:m].tobytes() == want.tobytes()))}
+        # every task of the timed launches' results (the results buffer of the last one) against the oracle
+        t0 = time.perf_counter()
+        want, want_items = oracle.ndc_prepare(nb)
+        got_items = out.cpu().numpy().view(abi.VH_ITEM)
+        nbr = np.nonzero((want["status"] == 0) & (want["action"] == abi.NDC_NEW_BRANCH))[0]
+        cnt = want["new_item_count"][nbr].astype(np.int64)
+        idx = (np.repeat(nb.tasks["out_begin"][nbr].astype(np.int64), cnt)
+               + np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+        line["parity_full"] = {"tasks": n, "new_branches": int(nbr.size), "new_branch_items": int(idx.size),
+                               "bit_exact": bool(got.tobytes() == want[:n].tobytes()
+                                                 and got_items[idx].tobytes() == want_items[idx].tobytes()),
+                               "oracle_s": time.perf_counter() - t0}
     return line
 
 
@@ -732,6 +778,49 @@ def cpu_baseline(ctx, gpu_res, gpu_batch, k):
     return out
 
 
+def summary(line):
+    """The essentials of every line in one short object: value, roofline fraction, traffic / algorithmic
+    bytes, and each parity / digest verdict."""
+    def rf(x):
+        r = x.get("roofline") or {}
+        t, a = r.get("traffic"), r.get("algorithmic_bytes_per_launch")
+        return {"frac": r.get("frac"), "kernel_ms": r.get("kernel_ms"), "traffic_x": (t / a) if (t and a) else None}
+
+    out = {"config2": {"value": line["value"], **rf(line), "all_ok": line.get("all_ok"),
+                       "parity_1M": (line.get("cpu_baseline") or {}).get("gpu_parity_bit_exact")}}
+    c = line.get("configs") or {}
+    for k in ("config3_mixed", "config4_long_tail"):
+        if k in c:
+            x = c[k]
+            out[k] = {"value": x["value"], **rf(x), "digest_ok": x["digest"]["matches_host_digest"],
+                      "parity_full": (x.get("parity_full") or {}).get("bit_exact"),
+                      "parity_full_workflows": (x.get("parity_full") or {}).get("workflows")}
+    if "passive_replication" in c:
+        x = c["passive_replication"]
+        vo = x.get("vs_oracle") or {}
+        out["passive_replication"] = {"value": x["value"], **rf(x), "mismatches_vs_one_shot": x["vs_one_shot"].get("mismatches"),
+                                      "mismatches_vs_oracle": vo.get("mismatches"),
+                                      "prefix_mismatches": (vo.get("prefix") or {}).get("mismatches")}
+    if "config5_ndc" in c:
+        x = c["config5_ndc"]
+        rb = x["rebuild"]
+        out["config5_rebuild"] = {"value": rb["value"], **rf(rb), "digest_ok": rb["digest"]["matches_host_digest"],
+                                  "parity_full": (rb.get("parity_full") or {}).get("bit_exact"),
+                                  "parity_full_workflows": (rb.get("parity_full") or {}).get("workflows")}
+        nd = x["ndc_prepare"]
+        out["ndc_prepare"] = {"value": nd["value"], **rf(nd), "parity_full": (nd.get("parity_full") or {}).get("bit_exact"),
+                              "parity_tasks": (nd.get("parity_full") or {}).get("tasks")}
+        cv = x["checksum_verify"]
+        out["checksum_verify"] = {"value": cv["value"], **rf(cv), "matches": cv["matches_replay_checksums"]}
+    for k, fig in (line.get("blob_to_rows") or {}).items():
+        out["blob_to_rows_" + k] = {"events_per_s": fig["events_per_s"],
+                                    "device_resident": fig["device_resident"]["events_per_s"],
+                                    "pcie_frac": fig["roofline"]["frac"]}
+    if "cpu_baseline" in line:
+        out["cpu_baseline"] = {"value": line["cpu_baseline"]["value"], "cores": line["cpu_baseline"]["cores"]}
+    return out
+
+
 def main():
     args = parse()
     ctx = Ctx(args)
@@ -757,7 +846,8 @@ def main():
             ctx, "config3", lambda: synth_native.mixed(n3, shard=shard),
             f"config 3: {args.c3_workflows} mixed histories per GPU (timers, signals, child workflows, cancel requests; "
             f"10..70 events), the rank's history shards of one {n3}-workflow workload",
-            lambda: synth_native.mixed(50_000, shard=shard))
+            lambda: synth_native.mixed(50_000, shard=shard),
+            global_ids=cdist.rank_workflows(n3, ctx.rank, ctx.world))
         del db3
         torch.cuda.empty_cache()
         progress("config 3 done")
@@ -775,7 +865,8 @@ def main():
         del db4, b4, r4
         torch.cuda.empty_cache()
         progress("config 4 done")
-        c5 = config5(ctx, args.c5_workflows, shard)
+        c5 = config5(ctx, args.c5_workflows, shard,
+                     global_ids=cdist.rank_workflows(args.c5_workflows * ctx.world, ctx.rank, ctx.world))
         torch.cuda.empty_cache()
         progress("config 5 done")
         line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr,
@@ -809,6 +900,7 @@ def main():
             fig["device_resident"]["vs_cpu_baseline"] = (fig["device_resident"]["events_per_s"]
                                                          / line["cpu_baseline"]["value"])
     if ctx.rank == 0:
+        line["summary"] = summary(line)   # last key: the figures of every line stay in a truncated stdout tail
         print(json.dumps(line), flush=True)
     if ctx.world > 1:
         ctx.dist.destroy_process_group()

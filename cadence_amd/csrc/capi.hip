@@ -275,8 +275,14 @@ int crr_segment_ms(float* out, int n) {
 
 int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
   if (!valid_inputs(in, out)) return -1;
-  if (in->n_wf == 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (in->n_wf == 0) {
+    // an empty batch still zeroes the digest (an empty rank's buffer joins the all-reduce)
+    if (!out->digest) return 0;
+    StreamDevice on_dev0(s);
+    if (!on_dev0.ok) return (int)hipErrorInvalidHandle;
+    return (int)hipMemsetAsync(out->digest, 0, CRR_DIGEST_WORDS * sizeof(int64_t), s);
+  }
   StreamDevice on_dev(s);
   if (!on_dev.ok) return (int)hipErrorInvalidHandle;
   DeviceState* d = current_state();

@@ -3261,6 +3261,19 @@ struct Digest {
 // (crr_inputs in, crr_outputs out, ...) first; the kernel-argument segment lays them out in that order at
 // their natural alignment.
 constexpr size_t kKernargOut = (sizeof(crr_inputs) + alignof(crr_outputs) - 1) / alignof(crr_outputs) * alignof(crr_outputs);
+// the two pointers are 8-byte fields at 8-byte-aligned offsets of structs that are 8-byte aligned, so the
+// offsets above are exact; every kernel that folds a digest is checked against that signature at the end of
+// this file (kDigestKernels)
+static_assert(alignof(crr_inputs) == 8 && alignof(crr_outputs) == 8, "kernarg layout: 8-byte aligned ABI structs");
+static_assert(offsetof(crr_inputs, digest_keys) % 8 == 0 && offsetof(crr_outputs, digest) % 8 == 0,
+              "kernarg layout: digest pointers at 8-byte offsets");
+static_assert(offsetof(crr_inputs, digest_keys) + 8 <= sizeof(crr_inputs) &&
+                  kKernargOut + offsetof(crr_outputs, digest) + 8 <= kKernargOut + sizeof(crr_outputs),
+              "kernarg layout: digest pointers inside the first two arguments");
+template <class F>
+struct DigestKernelSig : std::false_type {};
+template <class... A>
+struct DigestKernelSig<void (*)(crr_inputs, crr_outputs, A...)> : std::true_type {};
 // (a volatile read of the constant segment: a scalar load at the point of use, not merged with the kernel
 // start's)
 typedef const __attribute__((address_space(4))) char* kernarg_ptr;
@@ -4320,7 +4333,13 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   // keeps a stale or corrupted header from indexing past the lists
   const u32 n0 = min(__hip_atomic_load(out.scratch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
   const u32 n1 = min(__hip_atomic_load(out.scratch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), in.n_wf);
-  if (n0 == 0 && n1 == 0) return;  // uniform across the grid: nothing was handed back
+  if (n0 == 0 && n1 == 0) {  // uniform across the grid: nothing was handed back
+    // the big segment's gate counter still counted this phase's blocks in; no other block of this grid
+    // touches it, and every big block has finished (this kernel runs after the side streams joined)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      __hip_atomic_store(out.scratch + kScratchGate, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   build_crc_tables(crc_tables);
   Digest D;
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
@@ -4377,5 +4396,19 @@ __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_out
   u32 len = 0;
   checksums[w] = payload_crc(R, ids, G, TW, in.arena, crc_tables, &len);
 }
+
+// Every kernel that folds a digest (digest_flush / digest_flush_block read the pointers from the kernel
+// arguments at fixed offsets): (crr_inputs, crr_outputs, ...) must be its first two parameters.
+template <class... F>
+constexpr bool digest_kernels_ok(F...) { return (DigestKernelSig<F>::value && ...); }
+static_assert(digest_kernels_ok(&replay_lds_small_kernel<false, false>, &replay_lds_small_kernel<false, false, true>,
+                                &replay_lds_small_kernel<true, true>, &replay_lds_kernel<false, false>,
+                                &replay_lds_kernel<true, true>, &replay_global_kernel, &replay_wide_kernel,
+                                &replay_compact1_kernel<false, false>, &replay_compact1_kernel<true, true>,
+                                &replay_compact2_kernel<false, false>, &replay_compact2_kernel<true, true>,
+                                &replay_compact3_kernel<false, false>, &replay_compact3_kernel<true, true>,
+                                &replay_big_kernel, &replay_tail_kernel<false, false>, &replay_tail_kernel<true, true>,
+                                &replay_retry_kernel),
+              "a digest-folding kernel must take (crr_inputs, crr_outputs, ...) first (kernarg_late offsets)");
 
 }  // namespace crr

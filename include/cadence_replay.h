@@ -493,7 +493,8 @@ typedef struct crr_outputs {
 /* crr_replay's digest (crr_outputs.digest, with crr_inputs.digest_keys): CRR_DIGEST_STRIPES partial sums of
  * CRR_DIGEST_FIELDS int64 fields, stripe k at digest[k * CRR_DIGEST_STRIDE]; the digest is the field-wise
  * sum over the stripes, every sum wrapping mod 2^64 (so an all-reduce SUM of the whole buffer across ranks,
- * summed over stripes afterwards, is the job's digest).  crr_replay zeroes the buffer first.  Per workflow
+ * summed over stripes afterwards, is the job's digest).  crr_replay zeroes the buffer first (an empty
+ * batch, n_wf == 0, too: an empty rank's buffer is all zeros when it joins the all-reduce).  Per workflow
  * with key k, ok = (status == CRR_OK):
  *   0 ok ? ev_count : 0      1 ok      2 !ok      3 ok ? checksum : 0      4 ok ? k ^ checksum : 0
  *   5 inconsistencies        6 ok ? 0 : k ^ ((uint64)(uint32)status << 32 | (uint32)fail_step)

@@ -214,3 +214,44 @@ def test_fused_digest_equals_host_digest_every_path(eng):
     wf = pr.db_new.tensors["wf"][: pb.n_wf * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
     assert (got == dist.digest_numpy(res.exec, wf["ev_count"], keys)).all()
     assert fold_digest(pr.db_new.tensors["digest"].cpu().numpy())[0] == got[0]
+
+
+@pytest.mark.gpu
+def test_every_launch_leaves_scratch_counters_zeroed(eng):
+    """crr_replay leaves scratch[0..3] (the retry lists' counts, the retry pass's block count and the big
+    segment's gate counter) zeroed after every launch -- also when nothing was handed back to the retry pass,
+    whose early return then resets the gate the big blocks counted themselves into.  Valid long histories
+    with unbounded live sets: a big segment beside the wave tail, every bound exact (no retries)."""
+    import torch
+    from oracle import oracle
+    long = flatten(synth_mixed.long_tail_histories(80, 14, max_len=4000, run_cap=1500, multi_version=True,
+                                                   invalid_rate=0.0, caps=None), known_domains=KNOWN)
+    b = interleave(long)
+    assert b.tiers is not None and b.tiers[5] < b.n_wf, "needs a big segment"
+    assert b.wave_begin < b.tiers[5], "needs a wave tail beside it (the gated launch)"
+    db = eng.upload(b)
+    for _ in range(3):
+        eng.launch(db)
+        torch.cuda.synchronize()
+        assert (db.tensors["scratch"][:4].cpu().numpy() == 0).all(), db.tensors["scratch"][:4].cpu().numpy()
+    d = diff_results(b, eng.download(db), b, oracle.replay(b, 0))
+    assert not d, d
+
+
+@pytest.mark.gpu
+def test_empty_batch_zeroes_the_digest(eng):
+    """An empty rank (n_wf == 0) still zeroes its digest buffer: stale sums must not join the all-reduce."""
+    import ctypes
+    import torch
+    from cadence_amd import dist
+    b = interleave(_mixed(200, 3))
+    db = eng.upload(b)
+    eng.enable_digest(db, dist.device_keys(b))
+    db.tensors["digest"].fill_(12345)
+    ci = abi.CInputs()
+    ctypes.memmove(ctypes.byref(ci), ctypes.byref(db.c_in), ctypes.sizeof(ci))
+    ci.n_wf = 0
+    s = torch.cuda.current_stream(eng.dev)
+    assert eng.lib.crr_replay(ctypes.byref(ci), ctypes.byref(db.c_out), ctypes.c_void_p(s.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    assert (db.tensors["digest"].cpu().numpy() == 0).all()

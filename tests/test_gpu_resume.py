@@ -76,7 +76,7 @@ def test_resume_old_histories_in_the_compact_window(engine):
     from cadence_amd import abi
     from cadence_amd import flatten as fl
     caps = {"act": 3, "timer": 2, "child": 1, "rc": 1, "sig": 1}  # live sets a compact tier holds
-    hs = synth_mixed.long_tail_histories(600, 64, min_len=200, max_len=3000, run_cap=3000, multi_version=True,
+    hs = synth_mixed.long_tail_histories(1000, 64, min_len=200, max_len=3000, run_cap=3000, multi_version=True,
                                          caps=caps)
     pre, suf, mask = split_histories(hs, 8, last_only=True)
     pre_b = interleave(flatten(pre, known_domains=KNOWN))
@@ -87,7 +87,7 @@ def test_resume_old_histories_in_the_compact_window(engine):
     old = resumed & (loaded.exec["next_event_id"] > fl.COMPACT_MAX_EVENTS)
     assert (old & (tier < fl.WIDE)).sum() > 20 and (old & (tier == fl.WIDE)).sum() > 0
     loaded2, n = _device_split(engine, hs, 8, interleave, last_only=True)
-    assert n > 50   # Load-stable and equal to the one-shot replay (90 on this seed); every workflow equals the oracle
+    assert n > 100   # Load-stable and equal to the one-shot replay; every workflow equals the oracle
 
 
 @pytest.mark.gpu

@@ -24,6 +24,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #include "cadence_replay.h"
 
 // Checksums: the LdsTables kernels (config 2's) keep their CRC tables in LDS; the compact tiers and
@@ -2484,6 +2487,423 @@ struct WaveTables {
 };
 
 // ---------------------------------------------------------------------------------------------------
+// WaveRegTables: the wavefront path's pending maps (one workflow per wavefront) with their search state
+// in registers.  Slot j of a map is register j / 64 of lane j % 64: each slot's key / ID, its flags and
+// (activities, timers) the epilogue's candidate.  A search is a compare and a ballot per 64 slots, a free
+// slot the first lane with a clear LIVE bit, and a batch epilogue a wave minimum over registers: no LDS
+// round trip on the walk's critical path (WaveTables<LdsRows> searched 112-B LDS rows: 2-3 dependent
+// LDS round trips per map operation).  The rows themselves stay in the LDS arena (at finalize lane j % 64
+// reads row j), and the flags / timer-task bits the mirror holds are patched in when finalize writes them
+// to HBM.  Every lane stores a row it changes (the same values to the same LDS address): a store by its
+// owner lane alone is a branch on the lane, and the compiler then takes the whole walk -- the loop and
+// everything it carries -- as divergent (exec-mask regions, its state in VGPRs).  Nothing in the walk
+// branches on a per-lane value.
+// fl words: bits 0-7 the row's CRR_ROW_* flags; activities: bit 8 a candidate cached, 9-11 its timeout
+// type, 12 it is created, 16-19 TimerTaskStatus; timers: bit 8 TimerTaskStatusCreated.
+#ifndef CRR_WAVE_REG
+#define CRR_WAVE_REG 1
+#endif
+constexpr u32 kMirLive = CRR_ROW_LIVE, kMirMapped = CRR_ROW_MAPPED;
+constexpr u32 kMirHave = 1u << 8, kMirCreated = 1u << 12, kMirTimerCreated = 1u << 8;
+__device__ __forceinline__ i64 readlane_i64(i64 v, i32 l) {
+  const u32 lo = __builtin_amdgcn_readlane((u32)(u64)v, l);
+  const u32 hi = __builtin_amdgcn_readlane((u32)((u64)v >> 32), l);
+  return (i64)(((u64)hi << 32) | lo);
+}
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): the register arrays below are only ever
+// indexed by such constants, so they stay in registers (a loop index -- even one the unroller removes later --
+// leaves them in scratch memory)
+template <class F, int... K>
+__device__ __forceinline__ void each_(F&& f, std::integer_sequence<int, K...>) {
+  (f(std::integral_constant<int, K>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void each(F&& f) {
+  each_(f, std::make_integer_sequence<int, N>{});
+}
+template <class ARENA, int LIST>
+struct WaveRegTables {
+  static constexpr bool kResumable = false;  // a loaded state goes to the HBM-row pass
+  static constexpr int kList = LIST;
+  static constexpr i32 A = ARENA::A, T = ARENA::T, C = ARENA::C, R = ARENA::R, S = ARENA::S, P = ARENA::P;
+  static constexpr int NA = (A + 63) / 64, NT = (T + 63) / 64, NC = (C + 63) / 64, NR = (R + 63) / 64, NS = (S + 63) / 64;
+  static_assert(P <= 64, "reset-point keys: one register");
+  __device__ __forceinline__ static bool fits(i64) { return true; }
+  ARENA* M;
+  i32 lane;
+  i32 hw_act = 0, hw_timer = 0, hw_child = 0, hw_rc = 0, hw_sig = 0;  // slots ever used (wave-uniform)
+  bool retried = false;
+  bool dirty_act = false, dirty_timer = false;  // as WaveTables
+  i64 a_id[NA], a_ct[NA];   // ScheduleID; the cached earliest timer candidate's time
+  u32 a_key[NA], a_fl[NA];
+  u32 t_key[NT], t_fl[NT];
+  i64 t_ex[NT], t_sid[NT];  // ExpiryTime, StartedID
+  i64 c_id[NC], r_id[NR], s_id[NS];
+  u32 c_fl[NC], r_fl[NR], s_fl[NS];
+  u32 p_key;
+
+  __device__ __forceinline__ void init() {
+    lane = (i32)(threadIdx.x & 63);
+    hw_act = hw_timer = hw_child = hw_rc = hw_sig = 0;
+    retried = dirty_act = dirty_timer = false;
+    each<NA>([&](auto k) { a_id[k] = 0; a_ct[k] = 0; a_key[k] = 0; a_fl[k] = 0; });
+    each<NT>([&](auto k) { t_key[k] = 0; t_fl[k] = 0; t_ex[k] = 0; t_sid[k] = 0; });
+    each<NC>([&](auto k) { c_id[k] = 0; c_fl[k] = 0; });
+    each<NR>([&](auto k) { r_id[k] = 0; r_fl[k] = 0; });
+    each<NS>([&](auto k) { s_id[k] = 0; s_fl[k] = 0; });
+    p_key = 0;
+  }
+  __device__ __forceinline__ bool task_writer() const { return lane == 0; }
+
+  // slot j (wave-uniform) of a register array: the owner lane's value, uniform.  Register k is picked by
+  // selects on the uniform j / 64, never by an indexed access (which would put the arrays in scratch)
+  template <int N, class V>
+  __device__ __forceinline__ static V get(const V (&a)[N], i32 j) {
+    const i32 jk = j >> 6;
+    V x = a[0];
+    each<N>([&](auto k) { if constexpr (k > 0) x = jk == k ? a[k] : x; });
+    if constexpr (sizeof(V) == 8) return (V)readlane_i64((i64)x, j & 63);
+    else return (V)__builtin_amdgcn_readlane((u32)x, j & 63);
+  }
+  template <int N, class V>
+  __device__ __forceinline__ void put(V (&a)[N], i32 j, V v) const {
+    const i32 jk = j >> 6;
+    const bool me = lane == (j & 63);
+    each<N>([&](auto k) { a[k] = (me & (jk == k)) ? v : a[k]; });
+  }
+  template <int N>
+  __device__ __forceinline__ void set_bits(u32 (&a)[N], i32 j, u32 set, u32 clear) const {
+    const i32 jk = j >> 6;
+    const bool me = lane == (j & 63);
+    each<N>([&](auto k) { a[k] = (me & (jk == k)) ? ((a[k] & ~clear) | set) : a[k]; });
+  }
+  // first slot (< hw) whose lane-predicate holds, -1 if none.  Every register's ballot is taken (no early
+  // exit: a loop that can leave early may stay a loop, and index the arrays dynamically)
+  template <int N, class F>
+  __device__ __forceinline__ static i32 find(i32 hw, F pred) {
+    const i32 n = uniform32(hw);
+    i32 r = -1;
+    each<N>([&](auto kk) {
+      constexpr int k = N - 1 - (int)kk;
+      const u64 m = __builtin_amdgcn_ballot_w64(pred(std::integral_constant<int, k>{})) & (64 * k < n ? ~0ull : 0ull);
+      r = m ? 64 * k + (i32)__builtin_ctzll(m) : r;
+    });
+    return r;
+  }
+  // lowest free slot (GlobalTables::free_slot semantics: slots past hw are free), CAPACITY when `cap`
+  // rows are live, INTERNAL_RETRY past the arena
+  template <int N>
+  __device__ __forceinline__ static i32 take(const u32 (&fl)[N], i32& hw, i32 store_cap, i32 cap) {
+    i32 j = N * 64;
+    each<N>([&](auto kk) {
+      constexpr int k = N - 1 - (int)kk;
+      const u64 m = __builtin_amdgcn_ballot_w64(!(fl[k] & kMirLive));
+      j = m ? 64 * k + (i32)__builtin_ctzll(m) : j;
+    });
+    if (j >= cap) return -CRR_ERR_CAPACITY;
+    if (j >= store_cap) return -CRR_INTERNAL_RETRY;
+    if (j >= hw) hw = j + 1;
+    return j;
+  }
+  __device__ __forceinline__ i32 find_act_by_id(i64 sched) const {
+    return find<NA>(hw_act, [&](auto k) { return ((a_fl[k] & kMirLive) != 0) & (a_id[k] == sched); });
+  }
+  __device__ __forceinline__ i32 find_act_mapped(u32 key) const {
+    return find<NA>(hw_act, [&](auto k) { return ((a_fl[k] & (kMirLive | kMirMapped)) == (kMirLive | kMirMapped)) & (a_key[k] == key); });
+  }
+  // an activity's earliest timer candidate (timer_sequence.go:269-381 over its own timeouts) as fl bits 8-12
+  // and its time; tts: its TimerTaskStatus
+  __device__ __forceinline__ static u32 act_cand(i64& t, i64 sid, i64 sched_t, bool started, i64 start_t, i64 hb_t,
+                                                  i32 s2s, i32 s2c, i32 st2c, i32 hb, u32 tts) {
+    BestTimer B;
+    activity_candidates(B, 0, sid, sched_t, started, start_t, hb_t, s2s, s2c, st2c, hb, tts);
+    t = B.t;
+    return B.have ? (kMirHave | ((u32)B.y << 9) | (B.created ? kMirCreated : 0u)) : 0u;
+  }
+  __device__ __forceinline__ int act_insert(Lane& L, const Geo& G, const crr_activity_row& row) {
+    const i32 m = find_act_mapped(row.key);
+    const i32 j = take<NA>(a_fl, hw_act, A, G.act_cap);
+    if (j < 0) return -j;
+    if (m >= 0) set_bits<NA>(a_fl, m, 0u, kMirMapped);
+    M->act[j] = row;
+    i64 ct;
+    const u32 cw = act_cand(ct, row.schedule_id, row.scheduled_time, false, row.started_time, row.started_time,
+                            row.schedule_to_start, row.schedule_to_close, row.start_to_close, row.heartbeat, 0u);
+    put<NA>(a_id, j, row.schedule_id);
+    put<NA>(a_key, j, row.key);
+    put<NA>(a_ct, j, ct);
+    put<NA>(a_fl, j, (row.flags & 0xffu) | cw);
+    ++L.n_act;
+    dirty_act = true;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ int act_start(Lane& L, const Geo& G, i64 sched, i64 id, i64 ver, i32 s, i64 ts) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) return CRR_ERR_MISSING_ACTIVITY_INFO;
+    dirty_act = true;
+    crr_activity_row& r = M->act[j];
+    const i64 sched_t = r.scheduled_time;
+    const i32 s2s = r.schedule_to_start, s2c = r.schedule_to_close, st2c = r.start_to_close, hb = r.heartbeat;
+    r.version = ver;
+    r.started_id = id;
+    r.started_src = s;
+    r.started_time = ts;
+    r.last_heartbeat_time = ts;
+    const u32 fl = get<NA>(a_fl, j);
+    i64 ct;
+    const u32 cw = act_cand(ct, sched, sched_t, id != CRR_EMPTY_EVENT_ID, ts, ts, s2s, s2c, st2c, hb, (fl >> 16) & 0xffu);
+    put<NA>(a_ct, j, ct);
+    put<NA>(a_fl, j, (fl & ~(kMirHave | (7u << 9) | kMirCreated)) | cw);
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void act_delete(Lane& L, const Geo& G, i64 sched) {
+    const i32 j = find_act_by_id(sched);
+    if (j < 0) { ++L.inconsistencies; return; }
+    const u32 f = get<NA>(a_fl, j);
+    const u32 key = get<NA>(a_key, j);
+    put<NA>(a_fl, j, 0u);
+    --L.n_act;
+    dirty_act = true;
+    if (f & kMirMapped) return;
+    const i32 m = find_act_mapped(key);
+    if (m >= 0) set_bits<NA>(a_fl, m, 0u, kMirMapped);
+    else ++L.inconsistencies;
+  }
+  __device__ __forceinline__ void act_cancel(Lane& L, const Geo& G, u32 key, i64 id, i64 ver, i32 /*s*/) {
+    const i32 j = find_act_mapped(key);
+    if (j < 0) return;
+    crr_activity_row& r = M->act[j];
+    r.version = ver;
+    r.cancel_request_id = id;
+    set_bits<NA>(a_fl, j, CRR_ROW_CANCEL_REQUESTED, 0u);
+  }
+  __device__ __forceinline__ int timer_start(Lane& L, const Geo& G, const crr_timer_row& row) {
+    i32 j = find<NT>(hw_timer, [&](auto k) { return ((t_fl[k] & kMirLive) != 0) & (t_key[k] == row.key); });
+    if (j < 0) {
+      j = take<NT>(t_fl, hw_timer, T, G.timer_cap);
+      if (j < 0) return -j;
+      ++L.n_timer;
+    }
+    M->timer[j] = row;
+    put<NT>(t_key, j, row.key);
+    put<NT>(t_fl, j, row.flags & 0xffu);
+    put<NT>(t_ex, j, row.expiry_time);
+    put<NT>(t_sid, j, row.started_id);
+    dirty_timer = true;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void timer_delete(Lane& L, const Geo& G, u32 key) {
+    const i32 j = find<NT>(hw_timer, [&](auto k) { return ((t_fl[k] & kMirLive) != 0) & (t_key[k] == key); });
+    if (j < 0) { ++L.inconsistencies; return; }
+    put<NT>(t_fl, j, 0u);
+    --L.n_timer;
+    dirty_timer = true;
+  }
+  __device__ __forceinline__ int child_insert(Lane& L, const Geo& G, const crr_child_row& row) {
+    const i32 j = take<NC>(c_fl, hw_child, C, G.child_cap);
+    if (j < 0) return -j;
+    M->child[j] = row;
+    put<NC>(c_id, j, row.initiated_id);
+    put<NC>(c_fl, j, row.flags & 0xffu);
+    ++L.n_child;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ i32 find_child(i64 init) const {
+    return find<NC>(hw_child, [&](auto k) { return ((c_fl[k] & kMirLive) != 0) & (c_id[k] == init); });
+  }
+  __device__ __forceinline__ int child_start(Lane& L, const Geo& G, i64 init, i64 id, i32 s) {
+    const i32 j = find_child(init);
+    if (j < 0) return CRR_ERR_MISSING_CHILD_INFO;
+    M->child[j].started_id = id;
+    M->child[j].started_src = s;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void child_delete(Lane& L, const Geo& G, i64 init) {
+    const i32 j = find_child(init);
+    if (j < 0) { ++L.inconsistencies; return; }
+    put<NC>(c_fl, j, 0u);
+    --L.n_child;
+  }
+  __device__ __forceinline__ int init_insert(Lane& L, const Geo& G, bool is_rc, const crr_initiated_row& row) {
+    if (is_rc) {
+      const i32 j = take<NR>(r_fl, hw_rc, R, G.rc_cap);
+      if (j < 0) return -j;
+      M->rc[j] = row;
+      put<NR>(r_id, j, row.initiated_id);
+      put<NR>(r_fl, j, row.flags & 0xffu);
+      ++L.n_rc;
+    } else {
+      const i32 j = take<NS>(s_fl, hw_sig, S, G.sig_cap);
+      if (j < 0) return -j;
+      M->sig[j] = row;
+      put<NS>(s_id, j, row.initiated_id);
+      put<NS>(s_fl, j, row.flags & 0xffu);
+      ++L.n_sig;
+    }
+    return CRR_OK;
+  }
+  __device__ __forceinline__ void init_delete(Lane& L, const Geo& G, bool is_rc, i64 init) {
+    if (is_rc) {
+      const i32 j = find<NR>(hw_rc, [&](auto k) { return ((r_fl[k] & kMirLive) != 0) & (r_id[k] == init); });
+      if (j < 0) { ++L.inconsistencies; return; }
+      put<NR>(r_fl, j, 0u);
+      --L.n_rc;
+    } else {
+      const i32 j = find<NS>(hw_sig, [&](auto k) { return ((s_fl[k] & kMirLive) != 0) & (s_id[k] == init); });
+      if (j < 0) { ++L.inconsistencies; return; }
+      put<NS>(s_fl, j, 0u);
+      --L.n_sig;
+    }
+  }
+  __device__ __forceinline__ void rp_reset(Lane& L) { L.n_rp = 0; }
+  __device__ __forceinline__ int rp_push(Lane& L, const Geo& G, const crr_reset_point_row& row) {
+    if (L.n_rp >= G.rp_cap) return CRR_ERR_CAPACITY;
+    if (L.n_rp >= P) return CRR_INTERNAL_RETRY;
+    const i32 n = uniform32(L.n_rp);
+    M->rp[n] = row;
+    p_key = lane == n ? row.key : p_key;
+    ++L.n_rp;
+    return CRR_OK;
+  }
+  __device__ __forceinline__ bool rp_has(const Lane& L, const Geo& G, u32 key) const {
+    return __builtin_amdgcn_ballot_w64((lane < L.n_rp) & (p_key == key)) != 0;
+  }
+
+  // argmin over candidate slots of (time, ID): the minimum time by a DPP wave minimum of the per-lane
+  // minima, then the lowest ID among the slots holding it (IDs are unique among live rows); few candidates
+  // take a scalar pass instead.  Returns the slot, -1 if none.
+  template <int N>
+  __device__ __forceinline__ static i32 argmin(const u32 (&ok)[N], const i64 (&t)[N], const i64 (&id)[N], i64& tmin) {
+    u64 m[N];
+    i32 cnt = 0;
+    each<N>([&](auto k) { m[k] = __builtin_amdgcn_ballot_w64(ok[k] != 0); cnt += __builtin_popcountll(m[k]); });
+    if (cnt == 0) return -1;
+    i32 best = -1;
+    i64 bt = 0, be = 0;
+    if (cnt > CRR_WAVE_MIN_SCALAR) {
+      i64 v = 0x7fffffffffffffffLL;
+      each<N>([&](auto k) { v = (ok[k] && t[k] < v) ? t[k] : v; });
+      const i64 wm = WaveTables<HbmRows>::wave_min_i64(v);
+      each<N>([&](auto k) { m[k] = __builtin_amdgcn_ballot_w64(ok[k] && t[k] == wm); });
+    }
+    each<N>([&](auto k) {
+      for (u64 x = m[k]; x; x &= x - 1) {
+        const i32 l = (i32)__builtin_ctzll(x);
+        const i64 tt = readlane_i64(t[k], l), ee = readlane_i64(id[k], l);
+        if (best < 0 || tt < bt || (tt == bt && ee < be)) { best = 64 * k + l; bt = tt; be = ee; }
+      }
+    });
+    tmin = bt;
+    return best;
+  }
+  // CreateNextActivityTimer / CreateNextUserTimer (timer_sequence.go:127-199)
+  __device__ __forceinline__ void epilogue(Lane& L, const Geo& G, const TaskSink& K) {
+    if (L.n_act > 0 && dirty_act) {
+      u32 ok[NA];
+      each<NA>([&](auto k) { ok[k] = (a_fl[k] & (kMirLive | kMirHave)) == (kMirLive | kMirHave); });
+      i64 t = 0;
+      const i32 j = argmin<NA>(ok, a_ct, a_id, t);
+      if (j >= 0) {
+        const u32 fl = get<NA>(a_fl, j);
+        const i32 y = (i32)((fl >> 9) & 7u);
+        if (!(fl & kMirCreated)) {
+          set_bits<NA>(a_fl, j, kMirCreated | (timer_mask(y) << 16), 0u);
+          if (y == CRR_TIMEOUT_HEARTBEAT) M->act[j].last_hb_timeout_vis_s = unix_seconds(t);
+          if (K.on) K.add(L, G, CRR_TASK_ACTIVITY_TIMEOUT, y, L.current_version, t, get<NA>(a_id, j), M->act[j].attempt, -1);
+        }
+      }
+    }
+    dirty_act = false;
+    if (L.n_timer > 0 && dirty_timer) {
+      u32 ok[NT];
+      each<NT>([&](auto k) { ok[k] = (t_fl[k] & kMirLive) != 0; });
+      i64 t = 0;
+      const i32 j = argmin<NT>(ok, t_ex, t_sid, t);
+      if (j >= 0 && !(get<NT>(t_fl, j) & kMirTimerCreated)) {
+        set_bits<NT>(t_fl, j, kMirTimerCreated, 0u);
+        K.add(L, G, CRR_TASK_USER_TIMER, 0, L.current_version, t, get<NT>(t_sid, j), 0, -1);
+      }
+    }
+    dirty_timer = false;
+  }
+  // RefreshTasks' state effects (mutable_state_task_refresher.go:278-365)
+  __device__ __forceinline__ void refresh(Lane& L, const Geo& G) {
+    each<NA>([&](auto k) { a_fl[k] &= ~(kMirCreated | (0xffu << 16)); });
+    each<NT>([&](auto k) { t_fl[k] &= ~kMirTimerCreated; });
+    dirty_act = dirty_timer = true;
+    epilogue(L, G, TaskSink{false, false});
+  }
+
+  // live rows -> HBM slots 0..n-1 in event-ID order (rank = number of smaller live IDs), the mirror's flags
+  // patched in; the sorted IDs -> ids[] for the checksum lists
+  template <int N, class Row, class Patch>
+  __device__ __forceinline__ void scatter(const u32 (&fl)[N], const i64 (&id)[N], Row* rows, i64* ids,
+                                          Row* (Geo::*dst)(i32) const, const Geo& G, Patch patch) const {
+    i32 rank[N];
+    u64 live[N];
+    each<N>([&](auto k) { rank[k] = 0; live[k] = __builtin_amdgcn_ballot_w64((fl[k] & kMirLive) != 0); });
+    each<N>([&](auto k2) {
+      for (u64 x = live[k2]; x; x &= x - 1) {
+        const i64 o = readlane_i64(id[k2], (i32)__builtin_ctzll(x));
+        each<N>([&](auto k) { rank[k] += o < id[k] ? 1 : 0; });
+      }
+    });
+    each<N>([&](auto k) {
+      if ((fl[k] & kMirLive) != 0) {
+        Row r = rows[64 * k + lane];
+        patch(r, fl[k]);
+        *(G.*dst)(rank[k]) = r;
+        ids[rank[k]] = id[k];
+      }
+    });
+  }
+  __device__ __forceinline__ void finalize(Lane& L, const Geo& G) {
+    i64* ids = M->ids;
+    constexpr i32 oT = A, oC = oT + T, oR = oC + C, oS = oR + R;
+    scatter<NA>(a_fl, a_id, M->act, ids, &Geo::act, G, [](crr_activity_row& r, u32 f) {
+      r.flags = f & 0xffu;
+      r.timer_task_status = (i32)((f >> 16) & 0xffu);
+    });
+    scatter<NT>(t_fl, t_sid, M->timer, ids + oT, &Geo::timer, G, [](crr_timer_row& r, u32 f) {
+      r.flags = f & 0xffu;
+      r.task_status = (f & kMirTimerCreated) ? CRR_TIMER_TASK_STATUS_CREATED : CRR_TIMER_TASK_STATUS_NONE;
+    });
+    scatter<NC>(c_fl, c_id, M->child, ids + oC, &Geo::child, G, [](crr_child_row& r, u32 f) { r.flags = f & 0xffu; });
+    scatter<NR>(r_fl, r_id, M->rc, ids + oR, &Geo::rc, G, [](crr_initiated_row& r, u32 f) { r.flags = f & 0xffu; });
+    scatter<NS>(s_fl, s_id, M->sig, ids + oS, &Geo::sig, G, [](crr_initiated_row& r, u32 f) { r.flags = f & 0xffu; });
+    if (lane < L.n_rp) *G.rp(lane) = M->rp[lane];
+    wave_sync_lds();
+  }
+  __device__ __forceinline__ i64 act_id(const Geo&, i32 i) const { return M->ids[i]; }
+  __device__ __forceinline__ i64 timer_id(const Geo&, i32 i) const { return M->ids[A + i]; }
+  __device__ __forceinline__ i64 child_id(const Geo&, i32 i) const { return M->ids[A + T + i]; }
+  __device__ __forceinline__ i64 rc_id(const Geo&, i32 i) const { return M->ids[A + T + C + i]; }
+  __device__ __forceinline__ i64 sig_id(const Geo&, i32 i) const { return M->ids[A + T + C + R + i]; }
+  __device__ __forceinline__ void retry_push(const crr_inputs& in, const crr_outputs& out, u32 w) {
+    retried = true;
+    if constexpr (kList >= 0) {
+      if (lane == 0) {
+        const u32 k = atomicAdd(out.scratch + kList, 1u);
+        out.scratch[retry_slot(in, kList, k)] = w;
+      }
+    }
+  }
+};
+
+// The wavefront path's LDS-arena tables (CRR_WAVE_REG=0: the round-5 WaveTables over LDS rows, for A/B)
+#if CRR_WAVE_REG
+template <class ARENA, int LIST>
+using WaveLds = WaveRegTables<ARENA, LIST>;
+template <class ARENA, int LIST>
+__device__ __forceinline__ void bind_arena(WaveRegTables<ARENA, LIST>& T, ARENA* a) { T.M = a; }
+#else
+template <class ARENA, int LIST>
+using WaveLds = WaveTables<LdsRows<ARENA, LIST>>;
+template <class ARENA, int LIST>
+__device__ __forceinline__ void bind_arena(WaveTables<LdsRows<ARENA, LIST>>& T, ARENA* a) { T.S.M = a; }
+#endif
+
+// ---------------------------------------------------------------------------------------------------
 // Event sources.  LaneSource: one workflow per lane, the 8 column loads of step s+1 are issued before
 // step s is processed.  WaveSource: one workflow per wavefront, 64 consecutive events are loaded per
 // column in one coalesced instruction (one event per lane, the next chunk one chunk ahead) and step s
@@ -3603,8 +4023,11 @@ __device__ __forceinline__ void replay_body(const crr_inputs& in, const crr_outp
           if (bf >= 0) bfid = lane_i64(C.id_, bf);
         }
         if (!fast || ((OPS >> j) & 1)) {
-          const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base, (i32)(et & CRR_ETYPE_MASK), bfid, now_ns,
-                                     K, retention_days);
+          // the status is wave-uniform (every lane replays the same workflow), and read as such: a status the
+          // compiler takes as divergent makes the walk a divergent loop -- every branch of the visit an
+          // exec-mask region and its loop-carried state in VGPRs
+          const int rc = uniform32(apply_event(in, out, L, G, T, ev, s + L.src_base, (i32)(et & CRR_ETYPE_MASK), bfid,
+                                               now_ns, K, retention_days));
           if (rc) {
             wfail = j;
             wrc = rc;
@@ -3984,8 +4407,8 @@ __device__ __forceinline__ void replay_lds(const crr_inputs& in, const crr_outpu
     if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
     Geo G;
     load_geo(G, wfp, out, 1);
-    WaveTables<LdsRows<typename WaveTier<TIER>::Arena, 1>> T;  // outgrown: the retry pass's wave list
-    T.S.M = &arena.wave[wv];
+    WaveLds<typename WaveTier<TIER>::Arena, 1> T;  // outgrown: the retry pass's wave list
+    bind_arena(T, &arena.wave[wv]);
     T.init();
 
     WaveSource S(in.ev, wfp->ev_begin, 1, wfp->ev_count);
@@ -4075,19 +4498,19 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 // Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
 // the list counters, so the next crr_replay needs no memset.
 using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
-template <class ST, bool EMIT = true>
+template <class TT, bool EMIT = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
-                                                 WaveTables<ST>& T, const u32* crc_tables, Digest& D) {
+                                                 TT& T, const u32* crc_tables, Digest& D) {
   const crr_workflow* wfp = in.wf + w;
   if (((wfp->flags & CRR_WF_FLAG_NEW_RUN) != 0) != (phase == 0)) return;
   const i64 st = wf_stride(in, w);
   Geo G;
   load_geo(G, wfp, out, st);
-  if constexpr (std::is_same<ST, HbmRows>::value) T.S.G = G;
+  if constexpr (std::is_same<TT, WaveTables<HbmRows>>::value) T.S.G = G;
   T.init();
   T.hw_act = T.hw_timer = T.hw_child = T.hw_rc = T.hw_sig = 0;
   WaveSource S(in.ev, wfp->ev_begin, st, wfp->ev_count);
-  replay_body<EMIT, WaveTables<ST>, WaveSource>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
+  replay_body<EMIT, TT, WaveSource>(in, out, w, wfp, G, T, S, crc_tables, nullptr, &D);
 }
 __device__ __forceinline__ void replay_lane_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  LdsArena<HugeTier>* arena, const u32* crc_tables, Digest& D) {
@@ -4263,8 +4686,8 @@ __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outpu
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
   build_crc_tables(crc_tables);
-  WaveTables<LdsRows<BigArena, -1>> T;
-  T.S.M = &arena;
+  WaveLds<BigArena, -1> T;
+  bind_arena(T, &arena);
   Digest D;
   replay_wave_item(in, out, phase, w, T, crc_tables, D);
   if (T.retried) {
@@ -4306,14 +4729,14 @@ __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(
   __shared__ WaveTier<LargeTier>::Arena arena;
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
-  WaveTables<LdsRows<WaveTier<LargeTier>::Arena, RESUME ? -1 : 1>> T;
-  T.S.M = &arena;
+  WaveLds<WaveTier<LargeTier>::Arena, RESUME ? -1 : 1> T;
+  bind_arena(T, &arena);
   Digest D;
-  replay_wave_item<decltype(T.S), EMIT>(in, out, phase, w, T, crc_tables, D);
+  replay_wave_item<decltype(T), EMIT>(in, out, phase, w, T, crc_tables, D);
   if constexpr (RESUME) {
     if (T.retried) {
       WaveTables<HbmRows> H;
-      replay_wave_item<HbmRows, EMIT>(in, out, phase, w, H, crc_tables, D);
+      replay_wave_item<WaveTables<HbmRows>, EMIT>(in, out, phase, w, H, crc_tables, D);
     }
   }
   digest_flush(out, D);
@@ -4345,8 +4768,8 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
   for (u32 i = blockIdx.x; i < n1; i += gridDim.x) {  // 1. long-tail workflows (they run longest)
     const u32 w = (u32)uniform32((i32)out.scratch[retry_slot(in, 1, i)]);
     if (w >= in.n_wf) continue;
-    WaveTables<LdsRows<BigArena, -1>> T;
-    T.S.M = &arena.wave;
+    WaveLds<BigArena, -1> T;
+    bind_arena(T, &arena.wave);
     replay_wave_item(in, out, phase, w, T, crc_tables, D);
     if (T.retried) {
       WaveTables<HbmRows> H;

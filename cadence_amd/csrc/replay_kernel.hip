@@ -2503,6 +2503,10 @@ struct WaveTables {
 #ifndef CRR_WAVE_REG
 #define CRR_WAVE_REG 1
 #endif
+// register sets past the high-water mark skipped by scalar branches (big arenas: 5 activity registers)
+#ifndef CRR_WAVE_SKIP
+#define CRR_WAVE_SKIP 0
+#endif
 constexpr u32 kMirLive = CRR_ROW_LIVE, kMirMapped = CRR_ROW_MAPPED;
 constexpr u32 kMirHave = 1u << 8, kMirCreated = 1u << 12, kMirTimerCreated = 1u << 8;
 __device__ __forceinline__ i64 readlane_i64(i64 v, i32 l) {
@@ -2561,7 +2565,11 @@ struct WaveRegTables {
   __device__ __forceinline__ static V get(const V (&a)[N], i32 j) {
     const i32 jk = j >> 6;
     V x = a[0];
+#if CRR_WAVE_SKIP
+    each<N>([&](auto k) { if constexpr (k > 0) { if (jk == k) x = a[k]; } });
+#else
     each<N>([&](auto k) { if constexpr (k > 0) x = jk == k ? a[k] : x; });
+#endif
     if constexpr (sizeof(V) == 8) return (V)readlane_i64((i64)x, j & 63);
     else return (V)__builtin_amdgcn_readlane((u32)x, j & 63);
   }
@@ -2569,13 +2577,21 @@ struct WaveRegTables {
   __device__ __forceinline__ void put(V (&a)[N], i32 j, V v) const {
     const i32 jk = j >> 6;
     const bool me = lane == (j & 63);
+#if CRR_WAVE_SKIP
+    each<N>([&](auto k) { if (jk == k) a[k] = me ? v : a[k]; });
+#else
     each<N>([&](auto k) { a[k] = (me & (jk == k)) ? v : a[k]; });
+#endif
   }
   template <int N>
   __device__ __forceinline__ void set_bits(u32 (&a)[N], i32 j, u32 set, u32 clear) const {
     const i32 jk = j >> 6;
     const bool me = lane == (j & 63);
+#if CRR_WAVE_SKIP
+    each<N>([&](auto k) { if (jk == k) a[k] = me ? ((a[k] & ~clear) | set) : a[k]; });
+#else
     each<N>([&](auto k) { a[k] = (me & (jk == k)) ? ((a[k] & ~clear) | set) : a[k]; });
+#endif
   }
   // first slot (< hw) whose lane-predicate holds, -1 if none.  Every register's ballot is taken (no early
   // exit: a loop that can leave early may stay a loop, and index the arrays dynamically)
@@ -2585,8 +2601,15 @@ struct WaveRegTables {
     i32 r = -1;
     each<N>([&](auto kk) {
       constexpr int k = N - 1 - (int)kk;
+#if CRR_WAVE_SKIP
+      if (64 * k < n) {
+        const u64 m = __builtin_amdgcn_ballot_w64(pred(std::integral_constant<int, k>{}));
+        r = m ? 64 * k + (i32)__builtin_ctzll(m) : r;
+      }
+#else
       const u64 m = __builtin_amdgcn_ballot_w64(pred(std::integral_constant<int, k>{})) & (64 * k < n ? ~0ull : 0ull);
       r = m ? 64 * k + (i32)__builtin_ctzll(m) : r;
+#endif
     });
     return r;
   }
@@ -2595,10 +2618,18 @@ struct WaveRegTables {
   template <int N>
   __device__ __forceinline__ static i32 take(const u32 (&fl)[N], i32& hw, i32 store_cap, i32 cap) {
     i32 j = N * 64;
+    const i32 h = uniform32(hw);
     each<N>([&](auto kk) {
       constexpr int k = N - 1 - (int)kk;
+#if CRR_WAVE_SKIP
+      if (64 * k <= h) {  // the first free slot is at most hw
+        const u64 m = __builtin_amdgcn_ballot_w64(!(fl[k] & kMirLive));
+        j = m ? 64 * k + (i32)__builtin_ctzll(m) : j;
+      }
+#else
       const u64 m = __builtin_amdgcn_ballot_w64(!(fl[k] & kMirLive));
       j = m ? 64 * k + (i32)__builtin_ctzll(m) : j;
+#endif
     });
     if (j >= cap) return -CRR_ERR_CAPACITY;
     if (j >= store_cap) return -CRR_INTERNAL_RETRY;

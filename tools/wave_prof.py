@@ -35,10 +35,10 @@ PATCHES = [
     ("      i32 wfail = -1;\n      int wrc = CRR_OK;\n      while (vm) {\n",
      "      i32 wfail = -1;\n      int wrc = CRR_OK;\n      const u64 wt1_ = __builtin_readcyclecounter();\n"
      "      wp_[1] += wt1_ - wt0_; wp_[8] += 1;\n      while (vm) {\n"),
-    ("        if (!fast || ((OPS >> j) & 1)) {\n          const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base,",
+    ("        if (!fast || ((OPS >> j) & 1)) {\n          // the status is wave-uniform",
      "        const u64 wv0_ = __builtin_readcyclecounter();\n"
      "        const bool isop_ = fast && ((OPS >> j) & 1) && (et & CRR_ETYPE_MASK) != CRR_EV_DECISION_TASK_COMPLETED;\n"
-     "        if (!fast || ((OPS >> j) & 1)) {\n          const int rc = apply_event(in, out, L, G, T, ev, s + L.src_base,"),
+     "        if (!fast || ((OPS >> j) & 1)) {\n          // the status is wave-uniform"),
     ("        if (et & CRR_ETYPE_BATCH_LAST) {\n          T.epilogue(L, G, K);  // :634-640 GenerateActivityTimerTasks / GenerateUserTimerTasks\n"
      "          if (!fast) {",
      "        const u64 wv1_ = __builtin_readcyclecounter();\n"

@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1
@@ -298,8 +298,13 @@ class CInputs(ctypes.Structure):
                 ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32), ("digest_keys", ctypes.c_void_p)]
 
 
+# the live-ID sidecar (crr_outputs.live_ids, ABI v6): one int64 column per pending map, addressed like its rows
+ID_TABLES = ("act", "timer", "child", "rc", "sig")
+
+
 class COutputs(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES] + [("scratch",), ("digest",)]]
+    _fields_ = ([(name, ctypes.c_void_p) for name, *_ in [("exec",)] + [(t[0],) for t in TABLES] + [("scratch",), ("digest",)]]
+                + [("live_ids", ctypes.c_void_p * len(ID_TABLES))])
 
 
 # crr_replay's fused digest (crr_outputs.digest): stripes of partial sums (cadence_replay.h)

@@ -202,6 +202,9 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   if ((in->flags & CRR_IN_EMIT_TASKS) && !out->tasks) return false;
   if (in->stride == 64 && !out->scratch) return false;
   if (out->digest && !in->digest_keys) return false;
+  if (out->live_ids[0])  // the sidecar: all five columns or none
+    for (int t = 1; t < 5; ++t)
+      if (!out->live_ids[t]) return false;
   if (in->flags & CRR_IN_WAVE_TAIL) {
     if (in->stride != 64 || in->wave_begin > in->n_wf) return false;
   }

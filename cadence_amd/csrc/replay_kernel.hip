@@ -3146,9 +3146,12 @@ struct TokenWords {
 template <class IDS>
 // last_id / last_ver (have_last): the last version-history item as the replay holds it in registers (the
 // row it just wrote is not read back: a store -> load round trip per workflow)
+// sink (crr_outputs.live_ids, NULL or five columns): every ID the lists encode is also stored at its slot
+// of the live-ID sidecar (by `sink_writer` lanes only: the wave path's lanes all compute the same payload)
 __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids, const Geo& G, const TokenWords& TW,
                                            const uint8_t* arena, const u32* tables, u32* out_len,
-                                           bool have_last = false, i64 last_id = 0, i64 last_ver = 0) {
+                                           bool have_last = false, i64 last_id = 0, i64 last_ver = 0,
+                                           int64_t* const* sink = nullptr, bool sink_writer = false) {
   Crc K;
   K.init(tables);
   K.u8(0x59);                                                            // preambleVersion0
@@ -3162,16 +3165,21 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
   K.field(10, 36); K.be64(R.decision_version);
   K.field(10, 37); K.be64(R.decision_schedule_id);
   K.field(10, 38); K.be64(R.decision_started_id);
+  const bool sk = sink != nullptr && sink_writer;
+  auto put = [&](int t, i64 base, i32 i, i64 id) {
+    if (sk) sink[t][base + (i64)i * G.st] = id;
+    K.be64(id);
+  };
   K.list_header(45, 10, (u32)R.n_timer);                                 // PendingTimerStartedIDs
-  for (i32 i = 0; i < R.n_timer; ++i) K.be64(ids.timer_id(G, i));
+  for (i32 i = 0; i < R.n_timer; ++i) put(1, G.timer_base, i, ids.timer_id(G, i));
   K.list_header(46, 10, (u32)R.n_activity);                              // PendingActivityScheduledIDs
-  for (i32 i = 0; i < R.n_activity; ++i) K.be64(ids.act_id(G, i));
+  for (i32 i = 0; i < R.n_activity; ++i) put(0, G.act_base, i, ids.act_id(G, i));
   K.list_header(47, 10, (u32)R.n_signal);                                // PendingSignalInitiatedIDs
-  for (i32 i = 0; i < R.n_signal; ++i) K.be64(ids.sig_id(G, i));
+  for (i32 i = 0; i < R.n_signal; ++i) put(4, G.sig_base, i, ids.sig_id(G, i));
   K.list_header(48, 10, (u32)R.n_rc);                                    // PendingReqCancelInitiatedIDs
-  for (i32 i = 0; i < R.n_rc; ++i) K.be64(ids.rc_id(G, i));
+  for (i32 i = 0; i < R.n_rc; ++i) put(3, G.rc_base, i, ids.rc_id(G, i));
   K.list_header(49, 10, (u32)R.n_child);                                 // PendingChildInitiatedIDs
-  for (i32 i = 0; i < R.n_child; ++i) K.be64(ids.child_id(G, i));
+  for (i32 i = 0; i < R.n_child; ++i) put(2, G.child_base, i, ids.child_id(G, i));
   K.field(11, 55); K.be32(0);                                            // StickyTaskListName ""
   K.field(12, 56);                                                       // VersionHistories (shared.go:91639)
   K.field(8, 10); K.be32(0);                                             //   CurrentVersionHistoryIndex
@@ -4347,7 +4355,12 @@ done_events:
   R.expiration_ns = L.expiration_ns;
   R.src_next = L.src_base + n_ev;
   R.reserved = 0;
-  if (want_crc) R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len, true, L.vh_last_id, L.vh_last_ver);
+  if (want_crc) {
+    // the live-ID sidecar (crr_outputs.live_ids) is written with the lists, by one lane of a wavefront-path replay
+    int64_t* const* sink = out.live_ids[0] ? out.live_ids : nullptr;
+    R.checksum = payload_crc(R, T, G, TW, in.arena, crc_tables, &R.payload_len, true, L.vh_last_id, L.vh_last_ver, sink,
+                             !std::is_same<SRC, WaveSource>::value || (threadIdx.x & 63) == 0);
+  }
   CRR_PHASE(5);
   out.exec[w] = R;
   // the digest's terms: one lane per workflow (the wave path's lanes all hold the same result)
@@ -4834,6 +4847,17 @@ __global__ void __launch_bounds__(64) replay_retry_kernel(crr_inputs in, crr_out
 
 
 
+// The ID lists of a checksum from the live-ID sidecar (crr_outputs.live_ids): slot i of each column, addressed
+// like the rows (base + i * stride), so a wavefront reading slot i of 64 interleaved workflows reads 512
+// contiguous bytes.
+struct SidecarIds {
+  int64_t* const* c;
+  __device__ __forceinline__ i64 act_id(const Geo& G, i32 i) const { return c[0][G.act_base + (i64)i * G.st]; }
+  __device__ __forceinline__ i64 timer_id(const Geo& G, i32 i) const { return c[1][G.timer_base + (i64)i * G.st]; }
+  __device__ __forceinline__ i64 child_id(const Geo& G, i32 i) const { return c[2][G.child_base + (i64)i * G.st]; }
+  __device__ __forceinline__ i64 rc_id(const Geo& G, i32 i) const { return c[3][G.rc_base + (i64)i * G.st]; }
+  __device__ __forceinline__ i64 sig_id(const Geo& G, i32 i) const { return c[4][G.sig_base + (i64)i * G.st]; }
+};
 // Recompute checksums from already-written rows (mutable_state_builder.go:334-348 verify path).
 __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_outputs out, u32* checksums) {
   __shared__ u32 crc_tables[8 * 256];
@@ -4844,11 +4868,16 @@ __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_out
   Geo G;
   load_geo(G, wfp, out, wf_stride(in, w));
   const crr_exec_row R = out.exec[w];
-  GlobalTables ids;
   TokenWords TW;
   TW.issue(token_desc(wfp), R.token_src, in.arena);
   u32 len = 0;
-  checksums[w] = payload_crc(R, ids, G, TW, in.arena, crc_tables, &len);
+  if (out.live_ids[0]) {  // the ID lists from the dense sidecar the replay wrote
+    const SidecarIds ids{out.live_ids};
+    checksums[w] = payload_crc(R, ids, G, TW, in.arena, crc_tables, &len);
+  } else {                // ... or one field of each AoS row
+    GlobalTables ids;
+    checksums[w] = payload_crc(R, ids, G, TW, in.arena, crc_tables, &len);
+  }
 }
 
 // Every kernel that folds a digest (digest_flush / digest_flush_block read the pointers from the kernel

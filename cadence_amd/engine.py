@@ -108,7 +108,7 @@ class ReplayEngine:
         self.dev = self.torch.device("cuda", device)
 
     # -- upload ------------------------------------------------------------------------------------
-    def upload(self, batch: HistoryBatch) -> DeviceBatch:
+    def upload(self, batch: HistoryBatch, live_ids: bool = True) -> DeviceBatch:
         torch = self.torch
         dev = self.dev
         T = {}
@@ -158,6 +158,12 @@ class ReplayEngine:
             setattr(co, name, T["out_" + name].data_ptr())
         T["scratch"] = torch.zeros(2 * batch.n_wf + abi.SCRATCH_EXTRA_WORDS, dtype=torch.int32, device=dev)
         co.scratch = T["scratch"].data_ptr()
+        if live_ids:
+            # the live-ID sidecar (crr_outputs.live_ids): one int64 per row slot of each pending map, written by the
+            # replay for every OK workflow and read by crr_checksum instead of the rows
+            for t, name in enumerate(abi.ID_TABLES):
+                T["ids_" + name] = torch.zeros(max(batch.table_rows.get(name, 0), 1), dtype=torch.int64, device=dev)
+                co.live_ids[t] = T["ids_" + name].data_ptr()
         return DeviceBatch(batch, T, ci, co, self.device)
 
     # -- the fused digest (crr_outputs.digest) -------------------------------------------------------

@@ -154,6 +154,8 @@ class PassiveReplication:
             dn.c_in.large_begin = dn.c_in.compact_begin = 0
         for name, *_ in abi.TABLES:                # only db's outputs are used
             dn.tensors.pop("out_" + name, None)
+        for name in abi.ID_TABLES:                 # (the live-ID sidecar too)
+            dn.tensors.pop("ids_" + name, None)
         dn.tensors.pop("exec", None)
         self.db_new = dn
         self.snapshot = {k: db.tensors[k].clone() for k in self._state_keys()}

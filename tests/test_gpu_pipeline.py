@@ -255,3 +255,66 @@ def test_empty_batch_zeroes_the_digest(eng):
     assert eng.lib.crr_replay(ctypes.byref(ci), ctypes.byref(db.c_out), ctypes.c_void_p(s.cuda_stream)) == 0
     torch.cuda.synchronize()
     assert (db.tensors["digest"].cpu().numpy() == 0).all()
+
+
+@pytest.mark.gpu
+def test_live_id_sidecar_matches_rows_every_path(eng):
+    """The live-ID sidecar (crr_outputs.live_ids, ABI v6) holds, for every OK workflow, the IDs of its live rows
+    in slots 0..n-1 of each pending map (the checksum's lists) on every kernel path -- tier segments, retry
+    pass, wavefront tail / big kernels, canonical global kernel, task emission, a passive-replication step --
+    and crr_checksum reading it equals crr_checksum reading the rows and the replay's own checksums."""
+    import ctypes
+    import torch
+    from cadence_amd.replication import PassiveReplication
+    mixed = _mixed(3000, 15, mean_len=60, invalid_rate=0.1, can_rate=0.3)
+    long = flatten(synth_mixed.long_tail_histories(60, 16, max_len=4000, run_cap=1500, multi_version=True, caps=None),
+                   known_domains=KNOWN)
+    emit = interleave(mixed)
+    emit.emit_tasks = True
+    cases = [("mixed", interleave(mixed)), ("lanes", interleave(mixed, long_threshold=None)), ("canonical", mixed),
+             ("long", interleave(long)), ("emit", emit)]
+    id_field = {"act": "schedule_id", "timer": "started_id", "child": "initiated_id", "rc": "initiated_id",
+                "sig": "initiated_id"}
+    counts = {"act": "n_activity", "timer": "n_timer", "child": "n_child", "rc": "n_rc", "sig": "n_signal"}
+    base = {t[0]: t[2] for t in abi.TABLES}
+
+    def check_db(name, b, db):
+        res = eng.download(db)
+        ok = np.nonzero(res.exec["status"] == 0)[0]
+        st = b.wf_strides()
+        n_ids = 0
+        for t in abi.ID_TABLES:
+            side = db.tensors["ids_" + t].cpu().numpy()
+            rows = res.tables[t]
+            for w in ok[:: max(1, ok.size // 400)]:
+                n = int(res.exec[counts[t]][w])
+                idx = int(b.wf[base[t]][w]) + np.arange(n, dtype=np.int64) * int(st[w])
+                assert (side[idx] == rows[id_field[t]][idx]).all(), (name, t, int(w))
+                n_ids += n
+        # crr_checksum over the sidecar == over the rows == the replay's checksums
+        with_side = eng.checksum(db)
+        co = abi.COutputs()
+        ctypes.memmove(ctypes.byref(co), ctypes.byref(db.c_out), ctypes.sizeof(co))
+        for t in range(len(abi.ID_TABLES)):
+            co.live_ids[t] = None
+        out = torch.zeros(max(db.n_wf, 1), dtype=torch.int32, device=eng.dev)
+        s = torch.cuda.current_stream(eng.dev)
+        assert eng.lib.crr_checksum(ctypes.byref(db.c_in), ctypes.byref(co), ctypes.c_void_p(out.data_ptr()),
+                                    ctypes.c_void_p(s.cuda_stream)) == 0
+        rows_cs = out.cpu().numpy().view(np.uint32)[:db.n_wf]
+        assert (with_side[ok] == res.exec["checksum"][ok]).all(), name
+        assert (rows_cs[ok] == res.exec["checksum"][ok]).all(), name
+        return n_ids
+
+    total = 0
+    for name, b in cases:
+        db = eng.upload(b)
+        eng.launch(db)
+        total += check_db(name, b, db)
+    assert total > 1000
+    pb = interleave(_mixed(1500, 17, mean_len=40))
+    pr = PassiveReplication(eng, pb)
+    pr.setup()
+    pr.restore()
+    pr.step()
+    check_db("passive", pr.batch, pr.db)

@@ -4541,7 +4541,14 @@ __global__ void __launch_bounds__(kBlock) replay_global_kernel(crr_inputs in, cr
 //      its workflow again at once over its HBM rows.
 // Nothing is pushed during the pass, so no block waits on another.  The last block to finish zeroes
 // the list counters, so the next crr_replay needs no memset.
-using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;
+using BigArena = WaveArena<320, 160, 96, 64, 64, 64>;  // the retry pass's wave arena
+// replay_big_kernel's: the big segment holds the histories whose live sets the host expects past the wave
+// tail's arena (64 activities, 48 timers) -- in config 4 they peak at 65-71 -- so two registers per map
+// (WaveRegTables) cover them; a live set past this is replayed again over the 320-slot arena, then HBM rows
+#ifndef CRR_BIG_ARENA
+#define CRR_BIG_ARENA 128, 128, 64, 64, 64, 64
+#endif
+using BigSegArena = WaveArena<CRR_BIG_ARENA>;
 template <class TT, bool EMIT = true>
 __device__ __forceinline__ void replay_wave_item(const crr_inputs& in, const crr_outputs& out, int phase, u32 w,
                                                  TT& T, const u32* crc_tables, Digest& D) {
@@ -4722,21 +4729,32 @@ template __global__ void replay_compact3_kernel<true, true>(crr_inputs, crr_outp
 // Long-tail workflows the host expects to outgrow the fast kernels' per-wave arenas
 // (CRR_IN_TIERED, [big_begin, n_wf)): one wavefront each with the 57 KB row arena, then HBM rows;
 // launched next to the fast kernels, so the longest of them is not replayed after them.
+union BigArenas {
+  BigSegArena seg;
+  BigArena big;
+};
 __global__ void __launch_bounds__(64) replay_big_kernel(crr_inputs in, crr_outputs out, int phase, u32 lo, u32 hi) {
   __shared__ u32 crc_tables[8 * 256];
-  __shared__ BigArena arena;
+  __shared__ BigArenas arena;
   // resident: counted in before anything else (tail_gate_kernel holds the tail back until every block is)
   if (threadIdx.x == 0) atomicAdd(out.scratch + kScratchGate, 1u);
   const u32 w = lo + blockIdx.x;
   if (w >= hi) return;
   build_crc_tables(crc_tables);
-  WaveLds<BigArena, -1> T;
-  bind_arena(T, &arena);
   Digest D;
+  // two registers per map first; a live set past that is replayed again with the retry pass's 320-slot arena
+  // (five registers per map), then over the HBM rows
+  WaveLds<BigSegArena, -1> T;
+  bind_arena(T, &arena.seg);
   replay_wave_item(in, out, phase, w, T, crc_tables, D);
   if (T.retried) {
-    WaveTables<HbmRows> H;
-    replay_wave_item(in, out, phase, w, H, crc_tables, D);
+    WaveLds<BigArena, -1> T2;
+    bind_arena(T2, &arena.big);
+    replay_wave_item(in, out, phase, w, T2, crc_tables, D);
+    if (T2.retried) {
+      WaveTables<HbmRows> H;
+      replay_wave_item(in, out, phase, w, H, crc_tables, D);
+    }
   }
   digest_flush(out, D);
 }

@@ -121,12 +121,13 @@ class PassiveReplication:
     hbm_rows: bool = False                # continue every lane workflow over its HBM rows (A/B only)
     pre_wf: np.ndarray = None             # the prefix replay's descriptors
     suffix: HistoryBatch = None           # the new events (the step's inputs, host copy)
+    live_ids: bool = True                 # keep the live-ID sidecar (crr_outputs.live_ids)
 
     def setup(self):
         eng, torch, b = self.eng, self.eng.torch, self.batch
         cut = last_batch_cut(b)
         pre, suf, self.split = split_descriptors(b, cut)
-        db = eng.upload(b)
+        db = eng.upload(b, live_ids=self.live_ids)
         self.db = db
         wf_dev = db.tensors["wf"]
         nb = pre.nbytes

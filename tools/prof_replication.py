@@ -20,6 +20,7 @@ def main():
     p.add_argument("--wf", type=int, default=1_250_000)
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
+    p.add_argument("--no-live-ids", action="store_true", help="no live-ID sidecar (crr_outputs.live_ids)")
     p.add_argument("--hbm-rows", action="store_true", help="every lane workflow over its HBM rows (round-3 path)")
     p.add_argument("--phases", action="store_true", help="a -DCRR_PHASE_PROF=1 library: per-phase wave clocks")
     a = p.parse_args()
@@ -41,7 +42,7 @@ def main():
     one_shot = eng.download(db)
     del db
     torch.cuda.empty_cache()
-    pr = PassiveReplication(eng, batch, hbm_rows=a.hbm_rows)
+    pr = PassiveReplication(eng, batch, hbm_rows=a.hbm_rows, live_ids=not a.no_live_ids)
     pr.setup()
     setup_s = time.time() - t0
     ms = []

@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--c4-workflows", type=int, default=2000, help="config 4 logical workflows per GPU")
     p.add_argument("--c5-workflows", type=int, default=1_000_000, help="config 5 multi-version workflows per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer, host-ingest and blob -> rows figures")
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the CPUs this process may use)")
     p.add_argument("--cpu-sample", type=int, default=1_000_000, help="config 2 workflows in the CPU baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum wall seconds per CPU-baseline figure")
@@ -411,7 +412,8 @@ def config5(ctx, n_wf, shard, global_ids=None):
     from cadence_amd.flatten import interleave
     args, torch, eng = ctx.args, ctx.torch, ctx.eng
     t0 = time.time()
-    canon = as_rebuilds(synth_native.mixed(n_wf * ctx.world, multi_version=True, shard=shard, seed=0xCAD00005), 0xCAD00005)
+    canon = as_rebuilds(synth_native.mixed(n_wf * ctx.world, multi_version=True, shard=shard, seed=0xCAD00005), 0xCAD00005,
+                        global_ids)
     batch = interleave(canon)
     db = eng.upload(batch)
     setup = time.time() - t0
@@ -446,24 +448,41 @@ def config5(ctx, n_wf, shard, global_ids=None):
     return out
 
 
-def as_rebuilds(canon, seed):
+def as_rebuilds(canon, seed, global_ids=None):
     """Rebuild inputs for every workflow of a canonical batch: StateRebuilder.Rebuild replays the history
     onto a new branch whose token it installs (state_rebuilder.go:150), checks the last VersionHistory item
     against the requested (event ID, version) (:160-176; 2 % are given a mismatching one) and refreshes the
-    tasks (:183)."""
+    tasks (:183).  With ``global_ids`` (the workflows' indices in the whole job) every draw is a hash of
+    (seed, workflow), so a rank's part of the job equals the same workflows of the N = 1 run."""
     from cadence_amd import abi, synth
+    from cadence_amd import dist as cdist
     rng = np.random.default_rng(seed)
+    n = canon.n_wf
+    if global_ids is not None and len(global_ids) == n:
+        g = np.asarray(global_ids, np.uint64)
+        with np.errstate(over="ignore"):
+            h = np.stack([cdist.mix64(g * np.uint64(4) + np.uint64(seed) + np.uint64(k)) for k in range(3)], axis=1)
+        raw = h[:, :2].copy().view(np.uint8).reshape(n, 16)
+        tok = synth.branch_tokens(canon.arena[(canon.wf["start_token_off"].astype(np.int64)[:, None] + 8
+                                               + np.arange(36)[None, :])], synth.uuid_ascii_raw(raw))
+        mismatch = (h[:, 2] % np.uint64(10000)) < np.uint64(200)
+        return _install_rebuilds(canon, tok, mismatch)
+    tree = canon.arena[(canon.wf["start_token_off"].astype(np.int64)[:, None] + 8 + np.arange(36)[None, :])]
+    tok = synth.branch_tokens(tree, synth.uuid_ascii(rng, n))
+    return _install_rebuilds(canon, tok, rng.random(n) < 0.02)
+
+
+def _install_rebuilds(canon, tok, mismatch):
+    from cadence_amd import abi
     n = canon.n_wf
     cnt = canon.wf["ev_count"].astype(np.int64)
     last = canon.wf["ev_begin"].astype(np.int64) + np.maximum(cnt - 1, 0)
-    tree = canon.arena[(canon.wf["start_token_off"].astype(np.int64)[:, None] + 8 + np.arange(36)[None, :])]
-    tok = synth.branch_tokens(tree, synth.uuid_ascii(rng, n))
     base = canon.arena.size
     canon.arena = np.concatenate([canon.arena, tok.reshape(-1)])
     canon.wf["final_token_off"] = base + np.arange(n, dtype=np.int64) * 96
     canon.wf["final_token_len"] = 96
     ok = cnt > 0
-    canon.wf["rebuild_last_event_id"] = np.where(ok, canon.cols["event_id"][last], 0) + (rng.random(n) < 0.02)
+    canon.wf["rebuild_last_event_id"] = np.where(ok, canon.cols["event_id"][last], 0) + mismatch
     canon.wf["rebuild_last_event_version"] = np.where(ok, canon.cols["version"][last], 0)
     canon.wf["flags"] |= abi.WF_FLAG_REFRESH_TASKS
     return canon
@@ -871,7 +890,7 @@ def main():
         progress("config 5 done")
         line["configs"] = {"config3_mixed": c3, "config4_long_tail": c4, "passive_replication": pr,
                            "config5_ndc": c5}
-    if ctx.rank == 0 and ctx.world == 1 and not args.headline_only:
+    if ctx.rank == 0 and ctx.world == 1 and not args.headline_only and not args.no_e2e:
         line["pcie_inclusive"] = end_to_end(ctx, args.workflows, args.activities)
         progress("end to end (columns) done")
         e2e = line["pcie_inclusive"]

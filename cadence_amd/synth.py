@@ -23,7 +23,13 @@ _HEX = np.frombuffer(b"0123456789abcdef", np.uint8)
 
 def uuid_ascii(rng: np.random.Generator, n: int) -> np.ndarray:
     """n random UUIDv4 strings as an (n, 36) uint8 ASCII array (stand-in for uuid.New())."""
-    raw = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    return uuid_ascii_raw(rng.integers(0, 256, size=(n, 16), dtype=np.uint8))
+
+
+def uuid_ascii_raw(raw: np.ndarray) -> np.ndarray:
+    """UUIDv4 strings from (n, 16) random bytes (version / variant bits set here)."""
+    raw = raw.copy()
+    n = raw.shape[0]
     raw[:, 6] = (raw[:, 6] & 0x0F) | 0x40
     raw[:, 8] = (raw[:, 8] & 0x3F) | 0x80
     hexd = np.empty((n, 32), np.uint8)

@@ -2,7 +2,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -38,7 +37,6 @@ constexpr int kBlock = 256;
 constexpr unsigned kSegPrioMask = 0x1E;
 constexpr int kWideBlock = 256;  // replay_wide_kernel's block
 constexpr unsigned kRetryGrid = 512;  // 2 blocks (one wave, 67 KB LDS arena each) per CU x 256 CUs
-constexpr int kTailWavesPerSimd = 2;  // replay_tail_kernel's grid: wavefronts per SIMD (tail_grid)
 
 // Launch state is kept per HIP device, not per host thread: a cgo caller's goroutines migrate between
 // OS threads, and one thread may drive several devices.  Each device's state is created on first use
@@ -128,12 +126,6 @@ struct DeviceState {
   // finished, relative to the fork
   bool seg_on = false, seg_valid = false, seg_events = false;
   hipEvent_t seg_start = nullptr, seg_end[kSide + 1] = {};
-  int n_cu = -1;  // compute units (the tail kernel's grid), read on first use
-
-  int compute_units() {
-    if (n_cu < 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) n_cu = 0;
-    return n_cu;
-  }
 
   bool ensure_events() {
     if (!events) events = create_events(ev, 6, hipEventDefault);
@@ -227,29 +219,12 @@ bool valid_inputs(const crr_inputs* in, const crr_outputs* out) {
   return true;
 }
 
-// Every crr_replay leaves the retry-list counters, the big segment's gate and the tail's work list
-// (scratch[0..5]) zeroed; an
+// Every crr_replay leaves the retry-list counters and the big segment's gate (scratch[0..3]) zeroed; an
 // error return after the fast kernels were enqueued must reset them itself (the retry pass that would have
 // is not launched).
 int fail_reset(const crr_outputs* out, hipStream_t s, hipError_t err) {
-  if (out->scratch) (void)hipMemsetAsync(out->scratch, 0, 6 * sizeof(uint32_t), s);
+  if (out->scratch) (void)hipMemsetAsync(out->scratch, 0, 4 * sizeof(uint32_t), s);
   return (int)err;
-}
-
-// The tail kernel's grid: its wavefronts take runs off a work list (replay_tail_kernel), so the grid is a few
-// wavefronts per SIMD rather than one per run.  Tuning switches read per call (A/B runs, tests): the
-// environment's CRR_TAIL_WAVES_PER_SIMD overrides the default (0: one wavefront per run), CRR_TAIL_GRID (> 0)
-// sets the wavefront count itself.
-unsigned tail_grid(unsigned n_tail, int n_cu) {
-  unsigned cap = 0;
-  if (const char* g = getenv("CRR_TAIL_GRID")) cap = (unsigned)strtoul(g, nullptr, 10);
-  if (cap == 0) {
-    int wps = kTailWavesPerSimd;
-    if (const char* e = getenv("CRR_TAIL_WAVES_PER_SIMD")) wps = atoi(e);
-    if (wps <= 0 || n_cu <= 0) return n_tail;
-    cap = (unsigned)n_cu * 4u * (unsigned)wps;
-  }
-  return n_tail < cap ? n_tail : cap;
 }
 
 }  // namespace
@@ -420,7 +395,7 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream) {
           // behind the big segment's blocks (tail_gate_kernel): they cannot start once tail wavefronts hold the LDS
           if (run_big && fork)
             hipLaunchKernelGGL(crr::tail_gate_kernel, dim3(1), dim3(64), 0, s_tail, out->scratch, in->n_wf - tail_end);
-          const dim3 g_(tail_grid(tail_end - n_lane, d->compute_units())), b_(64);
+          const dim3 g_(tail_end - n_lane), b_(64);
           if (emit && resume) hipLaunchKernelGGL((crr::replay_tail_kernel<true, true>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else if (emit) hipLaunchKernelGGL((crr::replay_tail_kernel<true, false>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);
           else if (resume) hipLaunchKernelGGL((crr::replay_tail_kernel<false, true>), g_, b_, 0, s_tail, *in, *out, phase, n_lane, tail_end);

@@ -64,9 +64,6 @@ constexpr int kBlock = 256;
 constexpr int CRR_INTERNAL_RETRY = 200;  // LDS slots exhausted: replay again with GlobalTables
 constexpr u32 kScratchHeader = 64;       // scratch[0], [1] = retry list counts; lists follow the header
 constexpr u32 kScratchGate = 3;          // scratch[3]: big-segment blocks resident (tail_gate_kernel)
-// scratch[4], [5]: the tail kernel's work list -- the next run to take, the wavefronts done (the last one
-// to finish zeroes both, so every launch starts from zero)
-constexpr u32 kScratchTailNext = 4, kScratchTailDone = 5;
 // Retry lists: list 0 (fast path -> big-arena wavefront pass) at scratch[64 + k], list 1 (big arena ->
 // HBM-row wavefront pass) at scratch[64 + n_wf + k]; scratch holds >= 2 * n_wf + 64 words.
 __device__ __forceinline__ u32 retry_slot(const crr_inputs& in, int list, u32 k) {
@@ -4787,44 +4784,24 @@ __global__ void __launch_bounds__(64) tail_gate_kernel(const u32* scratch, u32 n
     __builtin_amdgcn_s_sleep(2);
   }
 }
-// Work list: the grid may be smaller than the tail (crr_replay sizes it to a few wavefronts per SIMD), and each
-// wavefront takes the next run of [lo, hi) -- longest first, the host's order -- until none is left, so a
-// SIMD's wavefronts split its share of the tail's events between them instead of holding whichever runs the
-// dispatcher placed there (config 4: ~2,000 of the 2,792 tail runs are ~10k events; one wavefront per run
-// put three of them on some SIMDs and two on others).
 template <bool EMIT, bool RESUME>
 __global__ void __launch_bounds__(64, CRR_TAIL_WAVES_PER_EU) replay_tail_kernel(crr_inputs in, crr_outputs out, int phase,
                                                                              u32 lo, u32 hi) {
   const u32* crc_tables = kCrcGlobal.v;
   __shared__ WaveTier<LargeTier>::Arena arena;
+  const u32 w = lo + blockIdx.x;
+  if (w >= hi) return;
+  WaveLds<WaveTier<LargeTier>::Arena, RESUME ? -1 : 1> T;
+  bind_arena(T, &arena);
   Digest D;
-  const u32 n = hi - lo;
-  for (;;) {
-    u32 i = 0;
-    if (threadIdx.x == 0) i = atomicAdd(out.scratch + kScratchTailNext, 1u);
-    i = (u32)uniform32(__shfl((int)i, 0, 64));
-    if (i >= n) break;
-    const u32 w = lo + i;
-    WaveLds<WaveTier<LargeTier>::Arena, RESUME ? -1 : 1> T;
-    bind_arena(T, &arena);
-    replay_wave_item<decltype(T), EMIT>(in, out, phase, w, T, crc_tables, D);
-    if constexpr (RESUME) {
-      if (T.retried) {
-        WaveTables<HbmRows> H;
-        replay_wave_item<WaveTables<HbmRows>, EMIT>(in, out, phase, w, H, crc_tables, D);
-      }
+  replay_wave_item<decltype(T), EMIT>(in, out, phase, w, T, crc_tables, D);
+  if constexpr (RESUME) {
+    if (T.retried) {
+      WaveTables<HbmRows> H;
+      replay_wave_item<WaveTables<HbmRows>, EMIT>(in, out, phase, w, H, crc_tables, D);
     }
   }
   digest_flush(out, D);
-  // every wavefront has taken its last index: the last one to finish resets the list for the next launch
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const u32 done = atomicAdd(out.scratch + kScratchTailDone, 1u);
-    if (done == gridDim.x - 1) {
-      __hip_atomic_store(out.scratch + kScratchTailNext, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(out.scratch + kScratchTailDone, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 template __global__ void replay_tail_kernel<false, false>(crr_inputs, crr_outputs, int, u32, u32);
 template __global__ void replay_tail_kernel<true, false>(crr_inputs, crr_outputs, int, u32, u32);

@@ -162,6 +162,7 @@ IN_EMIT_TASKS = 8
 IN_TIERED = 16              # lane workflows ordered by expected live-set size (large_begin / wide_begin)
 IN_HAS_RESUME = 32          # some workflow resumes a loaded state: the compact tiers continue it in LDS
 IN_ADVANCED_VISIBILITY = 64  # RefreshTasks emits the search-attributes task
+IN_STARTED_AUX = 128       # ActivityTaskStarted's aux = its scheduled event's act_side index (or -1)
 
 # ---- numpy dtypes (byte-identical to the C structs) ------------------------------------------------
 ACTIVITY_SIDE = np.dtype([

@@ -2009,6 +2009,17 @@ __device__ __forceinline__ void put_slot(const Plan& P, const Dst& D, u64 dst, u
     const u64 ni = side_start_base + (u64)a * side_stride + lane;
     D.start[ni] = P.start[x];
     a = (i32)ni;
+  } else if (t == CRR_EV_ACTIVITY_TASK_STARTED) {
+    // CRR_IN_STARTED_AUX (flatten._join_started): the scheduled event d = ID - ScheduledEventID steps back, when
+    // it is an ActivityTaskScheduled with that ID -- its side record's interleaved index; else -1
+    const i64 ref = P.ref[x];
+    const u64 d = (u64)P.id[x] - (u64)ref;
+    a = -1;
+    if (d >= 1 && d <= (u64)k) {
+      const u64 xs = x - d;
+      if ((P.etype[xs] & CRR_ETYPE_MASK) == CRR_EV_ACTIVITY_TASK_SCHEDULED && P.id[xs] == ref)
+        a = (i32)(side_act_base + (u64)P.aux[xs] * side_stride + lane);
+    }
   } else if (t == CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW && a >= 0 && (u32)a < P.n_wf) {
     a = (i32)P.inv[a];   // the new-run history's device position
   }

@@ -1665,8 +1665,12 @@ struct CompactTables {
       const crr_activity_row* r = G_act_loaded(f);
       sched_t = r->scheduled_time; s2c = r->schedule_to_close; st2c = r->start_to_close; hb = r->heartbeat;
     } else {
+      // the scheduled event's timeouts: through this event's own aux when the layout joined it
+      // (CRR_IN_STARTED_AUX; ss is that event's step, flatten._join_started), else through the scheduled
+      // event's aux -- one dependent gather less per ActivityTaskStarted
       const i64 six = ix(ss);
-      const crr_activity_side sa = in->act_side[in->ev.aux[six]];
+      const i32 pa = (in->flags & CRR_IN_STARTED_AUX) ? ev.aux() : -1;
+      const crr_activity_side sa = in->act_side[pa >= 0 ? pa : in->ev.aux[six]];
       sched_t = in->ev.timestamp[six]; s2c = sa.schedule_to_close; st2c = sa.start_to_close; hb = sa.heartbeat;
     }
     i64 ct = add_seconds(sched_t, s2c);
@@ -2979,9 +2983,11 @@ struct LaneSource {
   i32 n;
   Ev nx;      // step s+1 (type and the columns it needs), in flight during step s
   u32 et_nx;  // type byte of step s+2, in flight during step s
-  u64 ts_mask;  // types whose timestamp is read (uniform)
-  __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count, bool tasks)
-      : E(e), begin(b), st(stride), n(count), ts_mask(need::kTs | (tasks ? need::kTsTasks : 0ull)) {}
+  u64 ts_mask;   // types whose timestamp is read (uniform)
+  u64 aux_mask;  // types whose aux is read (uniform): ActivityTaskStarted's too with CRR_IN_STARTED_AUX (compact tiers)
+  __device__ __forceinline__ LaneSource(const crr_events& e, i64 b, i64 stride, i32 count, bool tasks, bool started_aux = false)
+      : E(e), begin(b), st(stride), n(count), ts_mask(need::kTs | (tasks ? need::kTsTasks : 0ull)),
+        aux_mask(need::kAux | (started_aux ? need::bit(CRR_EV_ACTIVITY_TASK_STARTED) : 0ull)) {}
   __device__ __forceinline__ i64 ix(i32 step) const { return begin + (i64)step * st; }
   __device__ __forceinline__ Ev load(i32 step, u32 et) const {
     Ev e;
@@ -2992,7 +2998,7 @@ struct LaneSource {
     e.ts_ = need::has(ts_mask, et) ? E.timestamp[i] : 0;
     e.ref_ = need::has(need::kRef, et) ? E.ref[i] : 0;
     e.key_ = need::has(need::kKey, et) ? E.key[i] : 0u;
-    e.aux_ = need::has(need::kAux, et) ? E.aux[i] : 0;
+    e.aux_ = need::has(aux_mask, et) ? E.aux[i] : 0;
     e.task_ = 0;
     return e;
   }
@@ -4676,7 +4682,8 @@ __device__ __forceinline__ void replay_compact(const crr_inputs& in, const crr_o
   }
   CompactTables<TIER, RESUME> T;
   T.init(&arena, &in, ev_begin, ev_count0);
-  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0);
+  LaneSource S(in.ev, ev_begin, 64, wfp->ev_count, EMIT && (in.flags & CRR_IN_EMIT_TASKS) != 0,
+               (in.flags & CRR_IN_STARTED_AUX) != 0);
   replay_body<EMIT, CompactTables<TIER, RESUME>, LaneSource>(in, out, w, wfp, G, T, S, crc_tables,
                                                              RESUME ? &X0 : nullptr, &D);
 }

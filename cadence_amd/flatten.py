@@ -47,6 +47,9 @@ class HistoryBatch:
     emit_tasks: bool = False
     # config.AdvancedVisibilityWritingMode != off: RefreshTasks' search-attributes task (CRR_IN_ADVANCED_VISIBILITY)
     advanced_visibility: bool = False
+    # CRR_IN_STARTED_AUX: every ActivityTaskStarted's aux is its scheduled event's act_side index, or -1
+    # (interleave: the device layouts)
+    started_aux: bool = False
     # CRR_IN_TIERED: (large_begin, compact_begin, compact2_begin, wide_begin, hbm_begin, big_begin) --
     # lane workflows ordered by expected live-set size (TIER_SLOTS, then HBM rows); long-tail workflows
     # no fast per-wave arena is expected to hold from big_begin on
@@ -69,7 +72,8 @@ class HistoryBatch:
         resume = self.tiers is not None and self.n_wf and bool((self.wf["flags"] & abi.WF_FLAG_RESUME).any())
         return ((abi.IN_WAVE_TAIL if self.wave_begin is not None else 0) | (abi.IN_EMIT_TASKS if self.emit_tasks else 0)
                 | (abi.IN_TIERED if self.tiers is not None else 0) | (abi.IN_HAS_RESUME if resume else 0)
-                | (abi.IN_ADVANCED_VISIBILITY if self.advanced_visibility else 0))
+                | (abi.IN_ADVANCED_VISIBILITY if self.advanced_visibility else 0)
+                | (abi.IN_STARTED_AUX if self.started_aux else 0))
 
     @property
     def n_wf(self) -> int:
@@ -521,6 +525,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
                                 cols, n, n_lane, n_groups, wave, group, lane)
     start_side = _interleave_side(batch.start_side, ev_type == ET.WorkflowExecutionStarted, wf_pos, src_idx, dst_idx,
                                   cols, n, n_lane, n_groups, wave, group, lane)
+    _join_started(batch, ev_type, wf_pos, step, src_idx, dst_idx, src_begin, dev_begin, dev_stride, cols)
 
     wf = batch.wf[perm].copy()
     wf["ev_begin"] = dev_begin
@@ -532,7 +537,7 @@ def interleave(batch: HistoryBatch, wave: int = WAVE, long_threshold: Optional[i
                        reset_keys=batch.reset_keys, arena=batch.arena, wf=wf, stride=wave,
                        key_off=key_off, key_len=key_len, key_arena=batch.key_arena, perm=perm,
                        wave_begin=n_lane if long_threshold is not None else None, emit_tasks=batch.emit_tasks,
-                       advanced_visibility=batch.advanced_visibility, tiers=tiers, init=batch.init.permuted(perm) if batch.init is not None else None,
+                       advanced_visibility=batch.advanced_visibility, started_aux=True, tiers=tiers, init=batch.init.permuted(perm) if batch.init is not None else None,
                        key_dict=kd, interners=[batch.interners[i] for i in perm] if batch.interners else None)
     for name, _dt, base_f, cap_f, _n in abi.TABLES:
         cap = np.zeros(n_groups * wave, np.int64)
@@ -577,6 +582,31 @@ def _interleave_side(side: np.ndarray, sel: np.ndarray, wf_pos, src_idx, dst_idx
     out[new_idx] = side[cols["aux"][dst]]
     cols["aux"][dst] = new_idx.astype(np.int32)
     return out
+
+
+def _join_started(batch, ev_type, wf_pos, step, src_idx, dst_idx, src_begin, dev_begin, dev_stride, cols):
+    """CRR_IN_STARTED_AUX: each ActivityTaskStarted's aux becomes the (already re-homed) act_side index of its
+    ActivityTaskScheduled event -- the event d = ID - ScheduledEventID steps before it in the same history, when
+    that one is an ActivityTaskScheduled with ID == ScheduledEventID (IDs increase by one within a call) -- else
+    -1.  The compact tiers read the scheduled event's timeouts from it (replay_kernel.hip act_started) instead of
+    gathering that event's aux first (mutable_state_builder.go:2254-2276 reads the ActivityInfo the scheduled
+    event built).  crr_ingest_layout writes the same (ingest_kernel.hip put_slot)."""
+    st = ev_type == ET.ActivityTaskStarted
+    if not st.any():
+        return
+    sel = np.nonzero(st)[0]
+    src = src_idx[sel]
+    ref = batch.cols["ref"][src].astype(np.int64)
+    d = batch.cols["event_id"][src].astype(np.int64) - ref
+    k = step[sel]
+    ok = (d >= 1) & (d <= k)
+    ks = np.where(ok, k - d, 0)
+    w = wf_pos[sel]
+    cand = src_begin[w] + ks                                   # canonical (stride 1) slot of the candidate
+    ok &= ((batch.cols["etype"][cand] & abi.ETYPE_MASK) == ET.ActivityTaskScheduled) & \
+        (batch.cols["event_id"][cand].astype(np.int64) == ref)
+    dst_s = dev_begin[w] + ks * dev_stride[w]
+    cols["aux"][dst_idx[sel]] = np.where(ok, cols["aux"][dst_s], -1).astype(np.int32)
 
 
 def table_rows_of(batch: HistoryBatch, exec_rows: np.ndarray, tables: Dict[str, np.ndarray], w: int):

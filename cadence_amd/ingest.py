@@ -199,7 +199,8 @@ class DeviceIngest:
         ci.wave_begin = int(S.wave_begin)
         (ci.large_begin, ci.compact_begin, ci.compact2_begin, ci.wide_begin, ci.hbm_begin, ci.big_begin) = \
             tuple(int(x) for x in S.tiers)
-        ci.flags = (abi.IN_WAVE_TAIL | abi.IN_TIERED | (abi.IN_HAS_NEW_RUN if S.has_new_run else 0)
+        # the layout joins each ActivityTaskStarted to its scheduled event's side record (CRR_IN_STARTED_AUX)
+        ci.flags = (abi.IN_WAVE_TAIL | abi.IN_TIERED | abi.IN_STARTED_AUX | (abi.IN_HAS_NEW_RUN if S.has_new_run else 0)
                     | (abi.IN_LDS_SMALL if S.lds_small_tail else 0) | (abi.IN_EMIT_TASKS if emit_tasks else 0))
         co = abi.COutputs()
         T["exec"] = torch.zeros(max(n, 1) * abi.EXEC_ROW.itemsize, dtype=torch.uint8, device=dev)

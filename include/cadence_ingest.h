@@ -103,7 +103,9 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
 
 /* `dst`: device buffers sized from the summary (columns n_slots entries each; the wf descriptors
  * n_wf; act_side / start_side / reset_keys / arena their counts, arena 8-byte padded); the scalar
- * fields of *dst (n_wf, stride, flags, wave_begin, tiers) are the caller's to set from the summary.
+ * fields of *dst (n_wf, stride, flags, wave_begin, tiers) are the caller's to set from the summary; the
+ * columns it writes satisfy CRR_IN_STARTED_AUX (each ActivityTaskStarted's aux joined to its scheduled event's
+ * side record), so the caller may set that flag.
  * `summary_host`: the plan's summary, as read back.  Also writes perm[n_wf] (device position ->
  * workflow index of the blob batch) when perm != NULL.  For both calls `bytes` of the blob batch must be
  * 16-byte aligned and readable CRR_INGEST_PAD bytes past the end of the last blob: the parser's register

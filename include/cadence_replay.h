@@ -343,6 +343,12 @@ typedef struct crr_inputs {
                                    CRR_IN_LDS_SMALL (which it overrides): speed only, never results */
 #define CRR_IN_ADVANCED_VISIBILITY 64u /* config.AdvancedVisibilityWritingMode != off: RefreshTasks also emits
                                    the search-attributes task (mutable_state_task_refresher.go:160-167) */
+#define CRR_IN_STARTED_AUX 128u /* (stride-64 batches) every ActivityTaskStarted event's aux holds the act_side
+                                   index of its ActivityTaskScheduled event in this call -- the event d = ID -
+                                   ScheduledEventID steps before it, when that one is an ActivityTaskScheduled with
+                                   ID ScheduledEventID -- or -1 (flatten.interleave, crr_ingest_layout).  The compact
+                                   tiers then read the scheduled event's timeouts straight from it instead of first
+                                   gathering that event's aux: a layout hint, results never depend on it */
 #define CRR_IN_HAS_RESUME 32u   /* some workflow carries CRR_WF_FLAG_RESUME (CRR_IN_TIERED batches): the
                                    compact tiers (and the long-tail kernel) run the instantiations that
                                    continue loaded states.  Without it -- or for a loaded state in the 1- or

@@ -25,6 +25,7 @@ def main():
     p.add_argument("--segments", action="store_true", help="report when each concurrent tier segment finished")
     p.add_argument("--digest", action="store_true", help="the fused multi-GPU digest on (as bench.py's config 2)")
     p.add_argument("--no-live-ids", action="store_true", help="no live-ID sidecar (crr_outputs.live_ids)")
+    p.add_argument("--no-started-aux", action="store_true", help="CRR_IN_STARTED_AUX off (A/B)")
     p.add_argument("--merge", type=int, default=0, help="tier experiment: 1 = the 2-slot segment replayed by compact "
                    "tier 1, 2 = the 1-slot segment too")
     a = p.parse_args()
@@ -57,6 +58,8 @@ def main():
         if a.merge == 2:
             t[0] = 0                          # large_begin
         b.tiers = tuple(t)
+    if a.no_started_aux:   # A/B: the compact tiers gather the scheduled event's aux themselves
+        b.started_aux = False
     db = eng.upload(b, live_ids=not a.no_live_ids)
     if a.digest:
         from cadence_amd import dist as cdist

@@ -21,6 +21,7 @@ def main():
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--lib", default=None, help="replay library to load (variant builds)")
     p.add_argument("--no-live-ids", action="store_true", help="no live-ID sidecar (crr_outputs.live_ids)")
+    p.add_argument("--no-started-aux", action="store_true", help="CRR_IN_STARTED_AUX off (A/B)")
     p.add_argument("--hbm-rows", action="store_true", help="every lane workflow over its HBM rows (round-3 path)")
     p.add_argument("--phases", action="store_true", help="a -DCRR_PHASE_PROF=1 library: per-phase wave clocks")
     a = p.parse_args()
@@ -36,6 +37,7 @@ def main():
 
     t0 = time.time()
     batch = interleave(synth_native.mixed(a.wf, shard=(cdist.NUM_SHARDS, 1, 0)), long_threshold=256)   # bench.py's N=1 shard
+    batch.started_aux = not a.no_started_aux
     eng = ReplayEngine(0)
     db = eng.upload(batch)
     eng.launch(db)

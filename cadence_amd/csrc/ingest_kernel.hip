@@ -113,6 +113,10 @@ struct Plan {       // pointers into the caller's scratch (carved by carve())
   u32* dom_table; u32 dom_cap;
   u32 n_blobs, n_wf;
   u64 max_events;
+  // resume (crr_ingest_plan_resume): device order = the batch's, keys seeded from the loaded dictionaries
+  u32 resume;
+  const crr_workflow* res_wf;
+  const u32* key_begin; const u32* key_count; const u64* key_off; const u32* key_len;
 };
 // per-workflow info words (canonical index)
 enum { WI_COUNT = 0, WI_EMPTY_AT, WI_ACT, WI_TIMER, WI_CHILD, WI_RC, WI_SIG, WI_VH, WI_RP, WI_TASKS, WI_STARTED,
@@ -1523,7 +1527,7 @@ __device__ __forceinline__ u64 bcast_u64(u64 v, int j) {
 // once at the end.
 constexpr u32 kWfWaveBlock = 256;
 __global__ __launch_bounds__(kWfWaveBlock) void wf_pass_wave_kernel(crr_blob_batch in, Plan P) {
-  if (!plan_ok(P)) return;
+  if (P.resume || !plan_ok(P)) return;   // (resume: seeded interning, wf_pass_kernel's)
   const u32 lane = threadIdx.x & 63;
   const u32 wave0 = blockIdx.x * (kWfWaveBlock / 64) + threadIdx.x / 64;
   const u32 n_waves = gridDim.x * (kWfWaveBlock / 64);
@@ -1697,18 +1701,40 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u64 r0 = P.off[1 * NB + bb], r1 = P.off[1 * NB + be];
   const u32 n = (u32)(e1 - e0);
   const u32 nr = (u32)(r1 - r0);
-  if (wave_shaped(n, nr, src.blob_count)) return;   // wf_pass_wave_kernel's
-  // this workflow's scratch table: 4 * (events + reset points) + 64 u64 words from its own base
-  const u64 tbase = 4 * e0 + 4 * r0 + 64ull * w;
+  if (!P.resume && wave_shaped(n, nr, src.blob_count)) return;   // wf_pass_wave_kernel's
+  // resume: the loaded state's K keys seed the dictionary (entries n + nr + k, ids k + 1)
+  const u32 K = P.resume ? P.key_count[w] : 0u, kb = P.resume ? P.key_begin[w] : 0u;
+  // this workflow's scratch table: 4 * (events + reset points + seeded keys) + 64 u64 words from its own base
+  const u64 tbase = 4 * e0 + 4 * r0 + 4ull * kb + 64ull * w;
+  if (P.resume && tbase + 4ull * (n + nr + K) + 64 > 8 * P.max_events + 64ull * P.n_wf) {
+    record_error(P.err, 0, kErrScratch);   // the seeds do not fit: the caller plans again with more
+    return;
+  }
   u64* tab = P.table + tbase;
-  const u32 cap_i = pow2_at_least(2 * (n + nr) + 2);
+  const u32 cap_i = pow2_at_least(2 * (n + nr + K) + 2);
   for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
+  auto seed_ref = [&](u32 k) -> KeyRef {
+    KeyRef r;
+    r.off = P.key_off[kb + k]; r.len = P.key_len[kb + k];
+    r.hash = r.len ? str_hash_bytes(in.bytes, r.off, r.len) : 0u;
+    r.head[0] = 0; r.head[1] = 0;
+    return r;
+  };
+  for (u32 k = 0; k < K; ++k) {   // the loaded strings are distinct: inserted without a compare
+    const KeyRef s = seed_ref(k);
+    if (s.len == 0) continue;
+    u32 slot = s.hash & (cap_i - 1);
+    while (tab[slot] != 0) slot = (slot + 1) & (cap_i - 1);
+    tab[slot] = ((u64)s.hash << 32) | (u64)(n + nr + k + 1);
+  }
 
   // One pass over the events in order: interning (WfFlattener::key_of: "" is key 0, new strings get 1, 2,
-  // ... in first-seen order; a Started event's previous reset points before anything after it), the
-  // side-record ordinals, capacities, VH items, tasks (WfFlattener::add / batch_end / finish).
-  // Table entries: (hash << 32) | (entry + 1), entry = event index (keys) or n + reset index (resets).
-  u32 next_key = 1;
+  // ... in first-seen order -- after the K loaded ones when resuming; a Started event's previous reset points
+  // before anything after it), the side-record ordinals, capacities, VH items, tasks (WfFlattener::add /
+  // batch_end / finish).
+  // Table entries: (hash << 32) | (entry + 1), entry = event index (keys), n + reset index (resets) or
+  // n + nr + loaded key index (seeds).
+  u32 next_key = K + 1;
   auto intern = [&](const KeyRef& kr, u32 entry) -> u32 {
     if (kr.len == 0) return 0u;
     u32 slot = kr.hash & (cap_i - 1);
@@ -1720,9 +1746,9 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
       }
       if ((u32)(ent >> 32) == kr.hash) {
         const u32 o = (u32)ent - 1;
-        const KeyRef other = o < n ? P.keys[e0 + o] : P.resets[r0 + (o - n)];
+        const KeyRef other = o < n ? P.keys[e0 + o] : o < n + nr ? P.resets[r0 + (o - n)] : seed_ref(o - n - nr);
         if (other.len == kr.len && same_bytes(in.bytes, kr.off, other.off, kr.len))
-          return o < n ? P.key[e0 + o] : P.reset_ids[r0 + (o - n)];
+          return o < n ? P.key[e0 + o] : o < n + nr ? P.reset_ids[r0 + (o - n)] : o - n - nr + 1;
       }
       slot = (slot + 1) & (cap_i - 1);
     }
@@ -1773,7 +1799,8 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
         }
       }
     }
-    if (src.blob_count == 0) empty_at = 0;
+    // no batch at all: ApplyEvents' empty history (state_builder.go:98-100); resuming, nothing to apply
+    if (src.blob_count == 0) empty_at = P.resume ? -1 : 0;
   }
   const i32 rp_cap = max_prev * (n_started > 1 ? n_started : 1) + n_dtc;
 
@@ -1968,6 +1995,17 @@ __global__ void summary_kernel(Plan P, u32 n_lane, u32 n_groups, u32 n_tail, crr
   S->tiers[5] = P.n_wf - P.counters[C_N_BIG];
   S->has_new_run = P.counters[C_NEW_RUN] ? 1u : 0u;
   S->lds_small_tail = P.counters[C_SMALL_TAIL_BAD] == 0 ? 1u : 0u;
+  if (P.resume) {   // the tiering, output tables and tokens are the loaded layout's (cadence_ingest.h)
+    for (int t = 0; t < 8; ++t) S->table_rows[t] = 0;
+    for (int k = 0; k < 6; ++k) S->tiers[k] = 0;
+    S->arena_bytes = 0;
+  }
+}
+
+// resume: device position p is blob-batch workflow p (positions_kernel reads the order from sort_out)
+__global__ void identity_order_kernel(Plan P) {
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < P.n_wf) P.sort_out[p] = p;
 }
 
 // ---- layout -----------------------------------------------------------------------------------------------
@@ -2080,6 +2118,15 @@ __global__ void layout_wf_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u
     const i32 c = wi[wi_k * nw + w];
     return c > 0 ? c : 0;
   };
+  if (P.resume) {   // the loaded descriptor, continuing with the new events (replication.split_descriptors)
+    d = P.res_wf[p];
+    d.ev_begin = (i64)pos(GV_LEN);
+    d.ev_count = wi[WI_COUNT * nw + w];
+    d.empty_batch_at = wi[WI_EMPTY_AT * nw + w];
+    d.flags |= CRR_WF_FLAG_RESUME;
+    D.wf[p] = d;
+    return;
+  }
   d.ev_begin = (i64)pos(GV_LEN);
   d.ev_count = wi[WI_COUNT * nw + w];
   d.empty_batch_at = wi[WI_EMPTY_AT * nw + w];
@@ -2241,8 +2288,24 @@ size_t crr_ingest_scratch_bytes(uint32_t n_blobs, uint32_t n_wf, uint64_t max_ev
   return carve(nullptr, n_blobs, n_wf, max_events, sort_tmp_bytes(n_wf)).bytes;
 }
 
-int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, crr_ingest_summary* summary,
-                    void* stream) {
+}  // extern "C"
+
+namespace {
+// the resume inputs into the plan (validated), or none
+bool set_resume(Plan& P, const crr_blob_batch* in, const crr_ingest_resume* R) {
+  P.resume = 0;
+  P.res_wf = nullptr; P.key_begin = nullptr; P.key_count = nullptr; P.key_off = nullptr; P.key_len = nullptr;
+  if (!R) return true;
+  if (R->wave_begin > in->n_wf) return false;
+  if (in->n_wf && (!R->loaded_wf || !R->key_begin || !R->key_count || !R->key_off || !R->key_len)) return false;
+  P.resume = 1;
+  P.res_wf = R->loaded_wf; P.key_begin = R->key_begin; P.key_count = R->key_count;
+  P.key_off = R->key_off; P.key_len = R->key_len;
+  return true;
+}
+
+int plan_impl(const crr_blob_batch* in, const crr_ingest_resume* R, void* scratch, size_t scratch_bytes,
+              crr_ingest_summary* summary, void* stream) {
   if (!valid_batch(in) || !scratch || !summary) return -1;
   if (in->n_wf == 0 && in->n_blobs > 0) return -1;   // blobs no workflow owns
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -2253,6 +2316,7 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   if (max_events == 0) return -1;
   Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events, stmp);
   Plan P = c.P;
+  if (!set_resume(P, in, R)) return -1;
   const u32 nb = in->n_blobs, nw = in->n_wf;
   const u64 NB = (u64)nb + 1;
   u32 dom_cap = 0;
@@ -2292,7 +2356,9 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
       hipLaunchKernelGGL(wf_pass_kernel, dim3(gw), dim3(kBlock), 0, s, *in, P);
     }
     multi_scan<u64>(P.arena_off, nw, nw, 1, P.tile, P.arena_off, (u64)nw + 1, s);
-    if (nw) {
+    if (nw && P.resume) {
+      hipLaunchKernelGGL(identity_order_kernel, dim3(gw), dim3(kBlock), 0, s, P);
+    } else if (nw) {
       size_t tmp = P.sort_tmp_bytes;
       if ((e = hipcub::DeviceRadixSort::SortKeys(P.sort_tmp, tmp, P.sort_in, P.sort_out, (int)nw, 0, 64, s)) != hipSuccess)
         return (int)e;
@@ -2307,6 +2373,7 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return (int)e;
     if (!flags) break;
   }
+  if (P.resume) n_lane = R->wave_begin;   // the loaded layout's split
   const bool failed = err != ~0ull || n_lane > nw || n_events > max_events || n_resets > max_events;
   const u32 n_groups = failed ? 0 : (n_lane + 63) / 64, n_tail = failed ? 0 : nw - n_lane;
   // B: geometry and the summary (after a failed decode only the error and the counts)
@@ -2324,9 +2391,10 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
   return 0;
 }
 
-int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, const crr_ingest_summary* S,
-                      const crr_inputs* dst, uint32_t* perm, void* stream) {
+int layout_impl(const crr_blob_batch* in, const crr_ingest_resume* R, void* scratch, size_t scratch_bytes,
+                const crr_ingest_summary* S, const crr_inputs* dst, uint32_t* perm, void* stream) {
   if (!valid_batch(in) || !scratch || !S || !dst || S->err || S->n_wf != in->n_wf) return -1;
+  if (R && S->wave_begin != R->wave_begin) return -1;
   if (!dst->wf || !dst->act_side || !dst->start_side || !dst->reset_keys || !dst->arena) return -1;
   const crr_events& ev = dst->ev;
   if (!ev.etype || !ev.event_id || !ev.version || !ev.timestamp || !ev.task_id || !ev.ref || !ev.key || !ev.aux) return -1;
@@ -2337,6 +2405,7 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
   const uint64_t max_events = max_events_of(scratch_bytes, in->n_blobs, in->n_wf, stmp);
   Carved c = carve(scratch, in->n_blobs, in->n_wf, max_events, stmp);
   Plan P = c.P;
+  if (!set_resume(P, in, R)) return -1;
   const u32 nw = in->n_wf, n_lane = S->wave_begin, n_groups = (n_lane + 63) / 64, n_tail = nw - n_lane;
   Dst D;
   D.ev = ev;
@@ -2361,6 +2430,31 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
     return (int)e;
   if (perm && nw && (e = hipMemcpyAsync(perm, P.perm, 4ull * nw, hipMemcpyDeviceToDevice, s)) != hipSuccess) return (int)e;
   return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" {
+
+int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, crr_ingest_summary* summary,
+                    void* stream) {
+  return plan_impl(in, nullptr, scratch, scratch_bytes, summary, stream);
+}
+
+int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes, const crr_ingest_summary* S,
+                      const crr_inputs* dst, uint32_t* perm, void* stream) {
+  return layout_impl(in, nullptr, scratch, scratch_bytes, S, dst, perm, stream);
+}
+
+int crr_ingest_plan_resume(const crr_blob_batch* in, const crr_ingest_resume* resume, void* scratch,
+                           size_t scratch_bytes, crr_ingest_summary* summary, void* stream) {
+  if (!resume) return -1;
+  return plan_impl(in, resume, scratch, scratch_bytes, summary, stream);
+}
+
+int crr_ingest_layout_resume(const crr_blob_batch* in, const crr_ingest_resume* resume, void* scratch,
+                             size_t scratch_bytes, const crr_ingest_summary* S, const crr_inputs* dst, void* stream) {
+  if (!resume) return -1;
+  return layout_impl(in, resume, scratch, scratch_bytes, S, dst, nullptr, stream);
 }
 
 }  // extern "C"

@@ -37,6 +37,13 @@ class CIngestSummary(ctypes.Structure):
                 ("tiers", ctypes.c_uint32 * 6), ("has_new_run", ctypes.c_uint32), ("lds_small_tail", ctypes.c_uint32)]
 
 
+class CIngestResume(ctypes.Structure):
+    """crr_ingest_resume (cadence_ingest.h): the loaded states a resume ingest continues."""
+    _fields_ = [("loaded_wf", ctypes.c_void_p), ("wave_begin", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("key_begin", ctypes.c_void_p), ("key_count", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
+                ("key_len", ctypes.c_void_p)]
+
+
 SCRATCH_TOO_SMALL = -100
 # CRR_INGEST_PAD (cadence_ingest.h): blob bytes readable this far past the last blob (the parser loads the
 # two 16-byte-aligned words around its cursor)
@@ -63,6 +70,10 @@ def _bind(L):
     L.crr_ingest_plan.restype = ctypes.c_int
     L.crr_ingest_layout.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp, vp]
     L.crr_ingest_layout.restype = ctypes.c_int
+    L.crr_ingest_plan_resume.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp]
+    L.crr_ingest_plan_resume.restype = ctypes.c_int
+    L.crr_ingest_layout_resume.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
+    L.crr_ingest_layout_resume.restype = ctypes.c_int
     L._ingest_bound = True
     return L
 
@@ -132,16 +143,23 @@ class DeviceIngest:
             self.scratch_bytes = need
         return self.scratch_bytes
 
-    def plan(self, db: DeviceBlobs, stream=None, max_events: Optional[int] = None) -> CIngestSummary:
-        """crr_ingest_plan (grows the scratch and plans again if the blobs hold more events than it fits)."""
+    def plan(self, db: DeviceBlobs, stream=None, max_events: Optional[int] = None,
+             resume: Optional[CIngestResume] = None) -> CIngestSummary:
+        """crr_ingest_plan (grows the scratch and plans again if the blobs hold more events than it fits);
+        with ``resume``, crr_ingest_plan_resume (new batches onto the loaded states it names)."""
         torch = self.torch
         s = stream if stream is not None else torch.cuda.current_stream(self.eng.dev)
         cap = max_events if max_events is not None else max(4096, db.blobs.n_bytes // 40)
         while True:
             size = self.ensure_scratch(db, cap)
             S = CIngestSummary()
-            rc = self.lib.crr_ingest_plan(ctypes.byref(db.c), ctypes.c_void_p(self.scratch.data_ptr()),
-                                          ctypes.c_size_t(size), ctypes.byref(S), ctypes.c_void_p(s.cuda_stream))
+            if resume is None:
+                rc = self.lib.crr_ingest_plan(ctypes.byref(db.c), ctypes.c_void_p(self.scratch.data_ptr()),
+                                              ctypes.c_size_t(size), ctypes.byref(S), ctypes.c_void_p(s.cuda_stream))
+            else:
+                rc = self.lib.crr_ingest_plan_resume(ctypes.byref(db.c), ctypes.byref(resume),
+                                                     ctypes.c_void_p(self.scratch.data_ptr()), ctypes.c_size_t(size),
+                                                     ctypes.byref(S), ctypes.c_void_p(s.cuda_stream))
             if rc != 0:
                 raise RuntimeError(f"crr_ingest_plan failed: {rc}")
             if S.err == SCRATCH_TOO_SMALL:
@@ -168,6 +186,35 @@ class DeviceIngest:
         if rc != 0:
             raise RuntimeError(f"crr_ingest_layout failed: {rc}")
         return out
+
+    def layout_resume(self, db: DeviceBlobs, resume: CIngestResume, S: CIngestSummary, ci: abi.CInputs,
+                      stream=None):
+        """crr_ingest_layout_resume into the inputs ``ci`` points at (sized from ``S`` by ``allocate_inputs``):
+        the new events' columns, side records, reset keys and the loaded descriptors continued."""
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.eng.dev)
+        rc = self.lib.crr_ingest_layout_resume(ctypes.byref(db.c), ctypes.byref(resume),
+                                               ctypes.c_void_p(self.scratch.data_ptr()),
+                                               ctypes.c_size_t(self.scratch_bytes), ctypes.byref(S), ctypes.byref(ci),
+                                               ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_ingest_layout_resume failed: {rc}")
+
+    def allocate_inputs(self, S: CIngestSummary, T: dict, ci: abi.CInputs, slack: float = 1.0):
+        """(Re)allocate the event columns, side records, reset keys and descriptors a resume layout writes
+        into ``T`` (``slack`` x the summary's sizes, reused while large enough) and point ``ci`` at them."""
+        torch, dev = self.torch, self.eng.dev
+        need = {"ev_" + name: max(int(S.n_slots), 1) * np.dtype(t).itemsize + 16 for name, t in abi.EVENT_COLUMNS}
+        need.update({"act_side": int(S.n_act_side) * abi.ACTIVITY_SIDE.itemsize + 16,
+                     "start_side": int(S.n_start_side) * abi.START_SIDE.itemsize + 16,
+                     "reset_keys": max(int(S.n_reset_keys), 1) * 4 + 16,
+                     "wf": max(int(S.n_wf), 1) * abi.WORKFLOW.itemsize + 16})
+        for k, nb in need.items():
+            if k not in T or T[k].numel() < nb:
+                T[k] = torch.zeros(int(nb * slack) + 16, dtype=torch.uint8, device=dev)
+        for name, _t in abi.EVENT_COLUMNS:
+            setattr(ci.ev, name, T["ev_" + name].data_ptr())
+        for k in ("act_side", "start_side", "reset_keys", "wf"):
+            setattr(ci, k, T[k].data_ptr())
 
     @staticmethod
     def input_shapes(S: CIngestSummary):

@@ -231,6 +231,134 @@ class PassiveReplication:
                 "resumed_ok": int((res.exec["status"] == 0).sum()), "mismatches": bad}
 
 
+def resume_blob_set(b: HistoryBatch, canon_bs, cut: np.ndarray, split: np.ndarray, pre_wf: np.ndarray):
+    """What passive replication receives, laid out for ``crr_ingest_plan_resume``: device position p's
+    replication-task payload -- the persisted blob(s) of its last event batch (``canon_bs``: the whole
+    histories of ``b``'s canonical batch, one blob per ApplyEvents batch; an empty batch at or after the cut
+    comes along) -- and the loaded state's key dictionary (the strings of key ids 1..K interned by the prefix,
+    ``key_dict_from_events`` over the prefix descriptors ``pre_wf``), its strings appended after the blobs.
+    Workflows that are not split get no blob (they apply nothing).  Returns (BlobSet, seeds: dict of
+    key_begin / key_count / key_off / key_len arrays)."""
+    from .blobs import BlobSet
+    n = b.n_wf
+    perm = b.perm if b.perm is not None else np.arange(n)
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)
+    src = canon_bs.wf[perm].copy()
+    bc = src["blob_count"].astype(np.int64)
+    bb = src["blob_begin"].astype(np.int64)
+    ea = b.wf["empty_batch_at"].astype(np.int64)
+    j = bc - 1 - np.where((ea >= 0) & (ea >= cut), 1, 0)
+    take = np.where(split, bc - j, 0)
+    tot = int(take.sum())
+    blob_idx = np.repeat(bb + j, take) + (np.arange(tot) - np.repeat(np.cumsum(take) - take, take))
+    bo = canon_bs.blob_off.astype(np.int64)
+    lens = bo[blob_idx + 1] - bo[blob_idx]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    nbytes = int(off[-1])
+    byte_src = np.repeat(bo[blob_idx], lens) + (np.arange(nbytes) - np.repeat(off[:-1], lens))
+    # seeds: the dictionary the prefix interned -- ids 1..K, K the largest id its events' keys or its Started
+    # events' previous reset points (interned with them, WfFlattener::add) carry; each id's string from the
+    # whole history's events, or the encoder's name for an id no event names (blob_encode.cpp "rk-<id>")
+    K = _prefix_key_count(b, pre_wf)
+    kb, kc, ko, kl, arena = key_dict_from_events(b)
+    arena = arena if arena is not None else np.zeros(0, np.uint8)
+    wf_of = np.repeat(np.arange(n), K)
+    kid = np.arange(int(K.sum())) - np.repeat(np.cumsum(K) - K, K) + 1
+    have = kid < kc.astype(np.int64)[wf_of]
+    e = np.where(have, kb.astype(np.int64)[wf_of] + kid, 0)
+    s_off = np.where(have, ko[e], 0).astype(np.int64)
+    s_len = np.where(have, kl[e], 0).astype(np.int64)
+    missing = np.nonzero(s_len == 0)[0]
+    extra = [b"rk-%d" % int(kid[i]) for i in missing]
+    if extra:
+        ex_len = np.array([len(x) for x in extra], np.int64)
+        s_off[missing] = arena.size + np.concatenate([[0], np.cumsum(ex_len)[:-1]])
+        s_len[missing] = ex_len
+        arena = np.concatenate([arena, np.frombuffer(b"".join(extra), np.uint8)])
+    seed_base = (nbytes + 15) // 16 * 16
+    data = np.zeros(seed_base + arena.size + 32, np.uint8)
+    data[:nbytes] = canon_bs.bytes[byte_src]
+    data[seed_base:seed_base + arena.size] = arena
+    src["blob_begin"] = (np.cumsum(take) - take).astype(np.uint32)
+    src["blob_count"] = take.astype(np.uint32)
+    nr = src["new_run_wf"].astype(np.int64)
+    src["new_run_wf"] = np.where(nr >= 0, inv[np.clip(nr, 0, n - 1)], -1).astype(np.int32)
+    bs = BlobSet(bytes=data, blob_off=off.astype(np.uint64), wf=src, strings=canon_bs.strings)
+    seeds = {"key_begin": (np.cumsum(K) - K).astype(np.uint32), "key_count": K.astype(np.uint32),
+             "key_off": (seed_base + s_off).astype(np.uint64), "key_len": s_len.astype(np.uint32)}
+    return bs, seeds
+
+
+def _prefix_key_count(b: HistoryBatch, pre_wf: np.ndarray) -> np.ndarray:
+    """Per workflow: the largest key id its prefix (``pre_wf``'s events) interned -- an event's key or a
+    previous reset point of a WorkflowExecutionStarted event."""
+    cnt = pre_wf["ev_count"].astype(np.int64)
+    st = b.wf_strides()
+    wf_idx = np.repeat(np.arange(b.n_wf), cnt)
+    step = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    x = pre_wf["ev_begin"].astype(np.int64)[wf_idx] + step * st[wf_idx]
+    K = np.zeros(b.n_wf, np.int64)
+    np.maximum.at(K, wf_idx, b.cols["key"][x].astype(np.int64))
+    started = (b.cols["etype"][x] & abi.ETYPE_MASK) == abi.EventType.WorkflowExecutionStarted
+    if started.any():
+        ss = b.start_side[b.cols["aux"][x[started]].astype(np.int64)]
+        c = np.maximum(ss["prev_reset_count"].astype(np.int64), 0)
+        w = np.repeat(wf_idx[started], c)
+        j = np.repeat(ss["prev_reset_key_off"].astype(np.int64), c) + (np.arange(int(c.sum())) - np.repeat(np.cumsum(c) - c, c))
+        if j.size:
+            np.maximum.at(K, w, b.reset_keys[j].astype(np.int64))
+    return K
+
+
+@dataclasses.dataclass
+class BlobReplication:
+    """The same replication step from the task's persisted bytes, on the device: the last batches' blobs
+    resident in HBM (as the replication task carries them, ``replication_task.go:386-390``) are decoded and
+    laid out by ``crr_ingest_plan_resume`` / ``crr_ingest_layout_resume`` (``serializer.go:109-119``), then
+    replayed onto the loaded rows in place -- every stage on the device, inside ``step``."""
+    pr: PassiveReplication
+    canon_bs: object                      # blobs.BlobSet of the whole histories (canonical order)
+    ing: object = None                    # ingest.DeviceIngest
+    blobs: object = None                  # ingest.DeviceBlobs: the tasks' payloads + the seeds' strings
+    resume: object = None                 # ingest.CIngestResume
+    db: DeviceBatch = None                # inputs written by the layout, outputs = the loaded rows
+    tensors: Dict[str, object] = None
+    n_events: int = 0
+
+    def setup(self):
+        from .ingest import CIngestResume, DeviceIngest
+        pr, eng, torch = self.pr, self.pr.eng, self.pr.eng.torch
+        b = pr.batch
+        cut = last_batch_cut(b)
+        bs, seeds = resume_blob_set(b, self.canon_bs, cut, pr.split, pr.pre_wf)
+        self.ing = self.ing or DeviceIngest(eng)
+        self.blobs = self.ing.upload(bs)
+        T = {k: torch.from_numpy(np.ascontiguousarray(v)).to(eng.dev) if v.size else
+             torch.zeros(1, dtype=torch.int64, device=eng.dev) for k, v in seeds.items()}
+        T["loaded_wf"] = torch.from_numpy(b.wf.view(np.uint8).copy()).to(eng.dev)   # the loaded descriptors
+        R = CIngestResume()
+        R.loaded_wf = T["loaded_wf"].data_ptr()
+        R.wave_begin = b.wave_begin if b.wave_begin is not None else b.n_wf
+        for k in seeds:
+            setattr(R, k, T[k].data_ptr())
+        self.resume = R
+        ci = abi.CInputs.from_buffer_copy(pr.db_new.c_in)   # the host path's flags and tiering
+        ci.arena = pr.db.c_in.arena                          # the loaded descriptors' branch tokens
+        self.db = DeviceBatch(pr.db_new.batch, T, ci, pr.db_new.c_out, eng.device)
+        self.tensors = T
+        S = self.ing.plan(self.blobs, resume=R)
+        self.ing.allocate_inputs(S, T, ci, slack=1.05)
+        self.n_events = int(S.n_events)
+
+    def step(self, stream=None):
+        S = self.ing.plan(self.blobs, stream, resume=self.resume)
+        self.ing.allocate_inputs(S, self.tensors, self.db.c_in, slack=1.05)
+        self.ing.layout_resume(self.blobs, self.resume, S, self.db.c_in, stream)
+        self.pr.eng.launch(self.db, stream)
+        return S
+
+
 def key_dict_from_events(b: HistoryBatch):
     """Per-workflow key id -> string tables (flatten.key_dict_from_interners' format, batch order) from the
     events' own key strings: a workflow's ids are interned over its history, so every id its rows hold

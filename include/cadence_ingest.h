@@ -16,7 +16,8 @@
  * with its default long-history threshold and tiering) on the same blobs: the same columns, side
  * records, descriptors, tier boundaries and slot-table sizes.  Only thriftrw (and empty) blobs are
  * decoded here; a batch holding json / unknown-encoded blobs goes through the host decoder
- * (cadence_decode.h), and so do loaded states (CRR_WF_FLAG_RESUME), which are not blobs.
+ * (cadence_decode.h).  New batches applied onto loaded states (CRR_WF_FLAG_RESUME, passive replication)
+ * take crr_ingest_plan_resume / crr_ingest_layout_resume at the end of this header.
  *
  * Two calls, because the caller sizes the replay's buffers between them:
  *   crr_ingest_plan   parse every blob (twice: count, then decode into a canonical scratch layout),
@@ -114,6 +115,47 @@ int crr_ingest_plan(const crr_blob_batch* in, void* scratch, size_t scratch_byte
 #define CRR_INGEST_PAD 32
 int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_bytes,
                       const crr_ingest_summary* summary_host, const crr_inputs* dst, uint32_t* perm, void* stream);
+
+/* ---- resume: a replication task's new batches onto loaded states already in HBM ------------------------
+ *
+ * Passive replication (service/history/ndc/replication_task.go:386-390 -> serializer.go:109-119 deserializes
+ * the task's event blob; ndc/history_replicator.go:385-460 applies it, :396, onto the state
+ * mutableStateBuilder.Load read back, mutable_state_builder.go:306-349).  The loaded states are the rows a
+ * previous crr_replay left in its crr_outputs (slots 0..n-1 of each workflow's regions); this pair decodes
+ * the new batches' blobs on the device and lays them out as the crr_inputs of a CRR_WF_FLAG_RESUME replay
+ * that writes into those same outputs.
+ *
+ * Differences from crr_ingest_plan / _layout:
+ *   order     blob-batch workflow p IS device position p of the loaded layout (no sort: the outputs are
+ *             addressed by position); lanes [0, wave_begin) interleaved 64-wide, the tail contiguous
+ *   keys      WfFlattener::key_of continued from the loaded state's dictionary: workflow p's loaded key k
+ *             (1..key_count[p]) is the string at key_off[key_begin[p] + k - 1] (byte offset into the blob
+ *             batch's `bytes`, which the caller uploads after the last blob) / key_len; a new string gets the
+ *             next id in first-seen order -- the ids the one-shot layout of the whole history assigns
+ *   descriptors  loaded_wf[p] (the loaded layout's descriptor: table bases / capacities, branch tokens,
+ *             rebuild fields, flags) with ev_begin / ev_count / empty_batch_at of the new events and
+ *             CRR_WF_FLAG_RESUME; a workflow without blobs applies nothing (ev_count 0, empty_batch_at -1)
+ *   not written  the arena (the caller keeps the loaded inputs' arena: the descriptors' token offsets point
+ *             into it); the summary's tiers, table_rows and arena_bytes are 0 -- the tiering is the caller's
+ *             (the loaded layout's), the output tables the loaded ones
+ * The new events' side records, reset keys and (CRR_IN_STARTED_AUX) started joins are written as by
+ * crr_ingest_layout.  key_begin must be the exclusive prefix sum of key_count; the scratch must hold the
+ * seeded keys' hash-table entries too (summary.err CRR_INGEST_SCRATCH_TOO_SMALL: plan again with more). */
+typedef struct crr_ingest_resume {
+    const crr_workflow* loaded_wf;  /* [n_wf] device order */
+    uint32_t        wave_begin;     /* the loaded layout's lane / tail split (<= n_wf) */
+    uint32_t        reserved;
+    const uint32_t* key_begin;      /* [n_wf] */
+    const uint32_t* key_count;      /* [n_wf] */
+    const uint64_t* key_off;        /* [sum key_count] into the blob batch's bytes */
+    const uint32_t* key_len;        /* [sum key_count] (0: an id no string names; never matches) */
+} crr_ingest_resume;
+
+int crr_ingest_plan_resume(const crr_blob_batch* in, const crr_ingest_resume* resume, void* scratch,
+                           size_t scratch_bytes, crr_ingest_summary* summary, void* stream);
+int crr_ingest_layout_resume(const crr_blob_batch* in, const crr_ingest_resume* resume, void* scratch,
+                             size_t scratch_bytes, const crr_ingest_summary* summary_host, const crr_inputs* dst,
+                             void* stream);
 
 #ifdef __cplusplus
 }

@@ -177,3 +177,67 @@ def test_inconsistent_loaded_states_route_to_retry_or_capacity(engine):
             idx = int(suf_b.wf[base_f][w]) + np.arange(int(suf_b.wf[cap_f][w])) * int(suf_b.wf_strides()[w])
             own[idx[idx < own.size]] = True
         assert same[~own].all(), name
+
+
+@pytest.mark.parametrize("gen", ["native", "python"])
+def test_passive_replication_from_blobs_on_device(gen):
+    """Passive replication from the task's persisted bytes (replication_task.go:386-390 -> serializer.go:109-119,
+    then ApplyEvents onto the loaded state): the last batches' thriftrw blobs, resident in HBM, are decoded and
+    laid out on the device (crr_ingest_plan_resume / crr_ingest_layout_resume: keys interned on from the loaded
+    dictionaries, the loaded descriptors continued) and replayed onto the loaded rows in place.  The laid-out
+    inputs equal the host path's (replication.suffix_batch: every column, the side records each event names,
+    the descriptors), and the rows equal the host path's step and the oracle's, bit for bit."""
+    import dataclasses
+    from cadence_amd import abi, synth_native
+    from cadence_amd.blobs import encode_batch
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.replication import BlobReplication, PassiveReplication
+    eng = ReplayEngine(0)
+    if gen == "native":
+        canon = synth_native.mixed(20000, can_rate=0.3, multi_version=True)
+    else:
+        canon = flatten(synth_mixed.mixed_histories(3000, 45, mean_len=120, multi_version=True, can_rate=0.3,
+                                                    invalid_rate=0.05),
+                        known_domains={"domain-a", "domain-b", "parent-domain"})
+    b = interleave(canon, long_threshold=150)
+    pr = PassiveReplication(eng, b)
+    pr.setup()
+    pr.restore()
+    pr.step()
+    host = eng.download(pr.db)
+    br = BlobReplication(pr, encode_batch(canon))
+    br.setup()
+    for _ in range(2):
+        pr.restore()
+        S = br.step()
+    dev = eng.download(pr.db)
+    eng.torch.cuda.synchronize()
+    # the inputs the device laid out against the host path's suffix batch
+    sb, T = pr.suffix, br.tensors
+    n_slots = int(S.n_slots)
+    assert n_slots == sb.cols["etype"].size and int(S.n_events) == sb.n_events
+    got = {name: T["ev_" + name][:n_slots * np.dtype(t).itemsize].cpu().numpy().view(t) for name, t in abi.EVENT_COLUMNS}
+    for name, _t in abi.EVENT_COLUMNS:
+        if name != "aux":
+            np.testing.assert_array_equal(got[name], sb.cols[name], err_msg=name)
+    from cadence_amd.abi import EventType as ET
+    et = sb.cols["etype"] & abi.ETYPE_MASK
+    g_side = T["act_side"][:int(S.n_act_side) * abi.ACTIVITY_SIDE.itemsize].cpu().numpy().view(abi.ACTIVITY_SIDE)
+    sched = et == ET.ActivityTaskScheduled   # the side record it names
+    assert sched.sum() > 100
+    assert g_side[got["aux"][sched]].tobytes() == sb.act_side[sb.cols["aux"][sched]].tobytes()
+    # ActivityTaskStarted joined to a scheduled event of the same new batch (rare in a last batch: the scheduled
+    # one is usually in the loaded state, where the replay reads the loaded row)
+    started = (et == ET.ActivityTaskStarted) & (got["aux"] >= 0)
+    assert g_side[got["aux"][started]].tobytes() == sb.act_side[sb.cols["aux"][started]].tobytes()
+    rest = ~np.isin(et, [ET.ActivityTaskScheduled, ET.ActivityTaskStarted, ET.WorkflowExecutionStarted])
+    np.testing.assert_array_equal(got["aux"][rest], sb.cols["aux"][rest])
+    g_wf = T["wf"][:b.n_wf * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
+    assert g_wf.tobytes() == sb.wf.tobytes()
+    # the rows: the host path's step, byte for byte
+    assert dev.exec.tobytes() == host.exec.tobytes()
+    for name, *_r in abi.TABLES:
+        if name != "tasks":
+            assert dev.tables[name].tobytes() == host.tables[name].tobytes(), name
+    vo = pr.verify_oracle(_oracle().replay, 0)
+    assert vo["mismatches"] == 0 and vo["compared_workflows"] > 0.5 * b.n_wf, vo

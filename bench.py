@@ -358,13 +358,16 @@ def parity_sample(ctx, sample_fn, long_threshold):
             "oracle_s": dt, "ok": int((gpu.exec["status"] == 0).sum())}
 
 
-def passive_replication(ctx, batch, one_shot):
+def passive_replication(ctx, batch, one_shot, make_canon=None):
     from cadence_amd.replication import PassiveReplication
     args, eng = ctx.args, ctx.eng
     pr = PassiveReplication(eng, batch)
     pr.setup()
     wall, ms = timed_steps(ctx, pr.db_new, args.config_steps, 1, before_step=pr.restore)
     v = pr.verify(one_shot)
+    blob_path = None
+    if make_canon is not None and not args.no_e2e:
+        blob_path = replication_blob_path(ctx, pr, make_canon)
     tot_ev, tot_tasks = ctx.reduce([float(pr.n_events), float(v["split_workflows"])], op="sum")
     out = {"workload": "config 3 shard: the last event batch of every history applied onto its loaded mutable state "
                        "(ndc/history_replicator.go:385-460 -> StateBuilder.ApplyEvents on a Load-ed state), rows in HBM",
@@ -375,6 +378,8 @@ def passive_replication(ctx, batch, one_shot):
            "vs_one_shot": v,
            "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP,
                                 config_traffic("passive_replication", pr.batch.n_wf, pr.n_events))}
+    if blob_path is not None:
+        out["blob_path"] = blob_path
     if ctx.rank == 0:   # every split workflow, the Load-unstable ones included: the oracle given the same split
         from oracle import oracle
         t0 = time.perf_counter()
@@ -385,6 +390,89 @@ def passive_replication(ctx, batch, one_shot):
         out["vs_oracle"]["prefix"] = pr.verify_prefix_oracle(oracle.replay, host_cpus())
         out["vs_oracle"]["prefix"]["oracle_s"] = time.perf_counter() - t0
     del pr
+    return out
+
+
+def replication_blob_path(ctx, pr, make_canon):
+    """The same replication step from the tasks' persisted bytes: each split workflow's last batch as the
+    thriftrw blob persistence stored (replication_task.go:386-390), decoded and laid out on the device onto
+    the loaded states (crr_ingest_plan_resume -- its two stream syncs included -- + crr_ingest_layout_resume,
+    serializer.go:109-119), then replayed onto the loaded rows in place.  `device_resident`: the blobs already
+    in HBM; `pcie_inclusive`: from pinned host buffers, the H2D copies inside the clock.  Each step restores
+    the loaded rows first (outside the clock); the rows after the timed steps equal the host path's step."""
+    from cadence_amd import abi
+    from cadence_amd.blobs import encode_batch
+    from cadence_amd.replication import BlobReplication
+    torch, eng, args = ctx.torch, ctx.eng, ctx.args
+    t0 = time.time()
+    canon = make_canon()
+    bs = encode_batch(canon)
+    del canon
+    enc_s = time.time() - t0
+    br = BlobReplication(pr, bs)
+    br.setup()
+    stream = torch.cuda.current_stream()
+    # the host path's step: what the blob path's rows must equal
+    pr.restore()
+    pr.step(stream)
+    want = eng.download(pr.db)
+    # per task over PCIe: the blobs, their offsets and per-workflow ranges; the loaded key dictionaries (after the
+    # blobs in the same buffer), the string arena and the known domains stay resident with the loaded states
+    rb = br.blobs.blobs
+    host = {"bytes": rb.bytes[:rb.n_bytes], "blob_off": rb.blob_off, "wf": rb.wf.view(np.uint8)}
+    pinned = {k: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).pin_memory() for k, a in host.items()}
+    h2d_bytes = sum(int(t.numel()) for t in pinned.values())
+
+    def run(steps, pcie):
+        wall = 0.0
+        for _ in range(steps):
+            pr.restore(stream)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            if pcie:
+                for k, t in pinned.items():
+                    if t.numel():
+                        br.blobs.tensors[k][:t.numel()].copy_(t, non_blocking=True)
+            br.step(stream)
+            torch.cuda.synchronize()
+            wall += time.perf_counter() - t1
+        return wall
+
+    run(1, False)
+    ctx.barrier()
+    eng.timing_begin()
+    wall = ctx.reduce([run(args.config_steps, False)])[0]
+    ms = eng.timing_read()
+    got = eng.download(pr.db)
+    same = got.exec.tobytes() == want.exec.tobytes() and all(
+        got.tables[t[0]].tobytes() == want.tables[t[0]].tobytes() for t in abi.TABLES if t[0] != "tasks")
+    run(1, True)
+    ctx.barrier()
+    wall_p = ctx.reduce([run(args.config_steps, True)])[0]
+    got_p = eng.download(pr.db)
+    same_p = got_p.exec.tobytes() == want.exec.tobytes()
+    # attribution: plan + layout alone (a sync after the layout), the rest is the replay
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.config_steps):
+        S = br.ing.plan(br.blobs, stream, resume=br.resume)
+        br.ing.layout_resume(br.blobs, br.resume, S, br.db.c_in, stream)
+    torch.cuda.synchronize()
+    ingest_ms = (time.perf_counter() - t1) / args.config_steps * 1e3
+    tot_ev, tot_tasks = ctx.reduce([float(br.n_events), float(pr.split.sum())], op="sum")
+    k = args.config_steps
+    out = {"workload": "the replication tasks' persisted batches (one thriftrw blob per split workflow) -> device decode + "
+                       "layout onto the loaded states -> ApplyEvents onto the loaded rows in place",
+           "device_resident": {"events_per_s": tot_ev * k / wall, "replication_tasks_per_s": tot_tasks * k / wall,
+                               "ms_per_step": wall / k * 1e3, "ingest_ms": ingest_ms,
+                               "replay_kernel_ms": float(np.mean(ms)), "rows_equal_host_path": bool(same)},
+           "pcie_inclusive": {"events_per_s": tot_ev * k / wall_p, "ms_per_step": wall_p / k * 1e3,
+                              "h2d_bytes": h2d_bytes, "h2d_GBs": h2d_bytes * k / wall_p / 1e9,
+                              "rows_equal_host_path": bool(same_p)},
+           "blobs": int(rb.n_blobs), "blob_bytes": int(rb.n_bytes), "events_per_gpu": br.n_events,
+           "setup_s": {"encode": enc_s}}
+    del br, pinned
+    torch.cuda.empty_cache()
     return out
 
 
@@ -820,6 +908,13 @@ def summary(line):
         out["passive_replication"] = {"value": x["value"], **rf(x), "mismatches_vs_one_shot": x["vs_one_shot"].get("mismatches"),
                                       "mismatches_vs_oracle": vo.get("mismatches"),
                                       "prefix_mismatches": (vo.get("prefix") or {}).get("mismatches")}
+        bp = x.get("blob_path")
+        if bp:
+            out["passive_replication"]["blob_path"] = {
+                "device_resident_events_per_s": bp["device_resident"]["events_per_s"],
+                "device_resident_ms": bp["device_resident"]["ms_per_step"],
+                "pcie_inclusive_events_per_s": bp["pcie_inclusive"]["events_per_s"],
+                "rows_equal_host_path": bp["device_resident"]["rows_equal_host_path"] and bp["pcie_inclusive"]["rows_equal_host_path"]}
     if "config5_ndc" in c:
         x = c["config5_ndc"]
         rb = x["rebuild"]
@@ -870,7 +965,7 @@ def main():
         del db3
         torch.cuda.empty_cache()
         progress("config 3 done")
-        pr = passive_replication(ctx, b3, r3)
+        pr = passive_replication(ctx, b3, r3, make_canon=lambda: synth_native.mixed(n3, shard=shard))
         progress("passive replication done")
         del b3, r3
         torch.cuda.empty_cache()

@@ -1701,7 +1701,10 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   const u64 r0 = P.off[1 * NB + bb], r1 = P.off[1 * NB + be];
   const u32 n = (u32)(e1 - e0);
   const u32 nr = (u32)(r1 - r0);
-  if (!P.resume && wave_shaped(n, nr, src.blob_count)) return;   // wf_pass_wave_kernel's
+  // wf_pass_wave_kernel's.  Resuming, every workflow is this kernel's: a replication task's batch is a few
+  // events, and a lane per workflow beat a wavefront per workflow with the loaded keys in lanes (config-3
+  // shard, 1.25M tasks: 0.60 ms against 0.79 ms with a wavefront per workflow at once, 1.01 ms grid-stride)
+  if (!P.resume && wave_shaped(n, nr, src.blob_count)) return;
   // resume: the loaded state's K keys seed the dictionary (entries n + nr + k, ids k + 1)
   const u32 K = P.resume ? P.key_count[w] : 0u, kb = P.resume ? P.key_begin[w] : 0u;
   // this workflow's scratch table: 4 * (events + reset points + seeded keys) + 64 u64 words from its own base
@@ -1713,20 +1716,31 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   u64* tab = P.table + tbase;
   const u32 cap_i = pow2_at_least(2 * (n + nr + K) + 2);
   for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
-  auto seed_ref = [&](u32 k) -> KeyRef {
+  auto seed_ref = [&](u32 k) -> KeyRef {   // (the hash through 8-byte unaligned loads: the pad follows the seeds)
     KeyRef r;
     r.off = P.key_off[kb + k]; r.len = P.key_len[kb + k];
-    r.hash = r.len ? str_hash_bytes(in.bytes, r.off, r.len) : 0u;
+    r.hash = 0;
+    if (r.len) {
+      RdT<false> rd;
+      rd.init(in.bytes, r.off, r.off + r.len);
+      r.hash = rd.hash(r.off, r.len);
+    }
     r.head[0] = 0; r.head[1] = 0;
     return r;
   };
-  for (u32 k = 0; k < K; ++k) {   // the loaded strings are distinct: inserted without a compare
-    const KeyRef s = seed_ref(k);
-    if (s.len == 0) continue;
-    u32 slot = s.hash & (cap_i - 1);
-    while (tab[slot] != 0) slot = (slot + 1) & (cap_i - 1);
-    tab[slot] = ((u64)s.hash << 32) | (u64)(n + nr + k + 1);
-  }
+  // the seeds go in at the first named key (a batch without one never hashes them); the loaded strings are
+  // distinct: inserted without a compare
+  bool seeded = K == 0;
+  auto seed_all = [&]() {
+    seeded = true;
+    for (u32 k = 0; k < K; ++k) {
+      const KeyRef sr = seed_ref(k);
+      if (sr.len == 0) continue;
+      u32 slot = sr.hash & (cap_i - 1);
+      while (tab[slot] != 0) slot = (slot + 1) & (cap_i - 1);
+      tab[slot] = ((u64)sr.hash << 32) | (u64)(n + nr + k + 1);
+    }
+  };
 
   // One pass over the events in order: interning (WfFlattener::key_of: "" is key 0, new strings get 1, 2,
   // ... in first-seen order -- after the K loaded ones when resuming; a Started event's previous reset points
@@ -1737,6 +1751,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   u32 next_key = K + 1;
   auto intern = [&](const KeyRef& kr, u32 entry) -> u32 {
     if (kr.len == 0) return 0u;
+    if (!seeded) seed_all();
     u32 slot = kr.hash & (cap_i - 1);
     for (;;) {
       const u64 ent = tab[slot];
@@ -1808,7 +1823,7 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   // ID, ref < event ID) / inserted timer keys -1; the running maximum --
   i32 bound[kMaps] = {0, 0, 0, 0, 0, 0};
   bool compact_ok = n <= (u32)kCompactMaxEvents;
-  {
+  if (!P.resume) {   // (resume: the tiering is the loaded layout's, no bounds to find)
     const u32 cap_b = pow2_at_least(2 * n + 2);   // <= the interning table's region
     for (u32 i = 0; i < cap_b; ++i) tab[i] = 0;
     auto map_of = [](u32 t, int& dir) -> int {
@@ -2119,6 +2134,14 @@ __global__ void layout_wf_kernel(crr_blob_batch in, Plan P, Dst D, u32 n_lane, u
     return c > 0 ? c : 0;
   };
   if (P.resume) {   // the loaded descriptor, continuing with the new events (replication.split_descriptors)
+    if (P.res_wf == D.wf) {   // in place: only the per-call fields
+      crr_workflow* o = D.wf + p;
+      o->ev_begin = (i64)pos(GV_LEN);
+      o->ev_count = wi[WI_COUNT * nw + w];
+      o->empty_batch_at = wi[WI_EMPTY_AT * nw + w];
+      o->flags |= CRR_WF_FLAG_RESUME;
+      return;
+    }
     d = P.res_wf[p];
     d.ev_begin = (i64)pos(GV_LEN);
     d.ev_count = wi[WI_COUNT * nw + w];
@@ -2418,8 +2441,12 @@ int layout_impl(const crr_blob_batch* in, const crr_ingest_resume* R, void* scra
   // side records no event references stay zero, like flatten's zero-filled arrays
   if ((e = hipMemsetAsync(D.act, 0, S->n_act_side * sizeof(crr_activity_side), s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(D.start, 0, S->n_start_side * sizeof(crr_start_side), s)) != hipSuccess) return (int)e;
-  // 16 wavefronts per group of 64 lanes: a wavefront writes one slot row of the group per step
-  if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(1024), 0, s, *in, P, D, n_lane, n_groups);
+  // up to 16 wavefronts per group of 64 lanes (a wavefront writes one slot row of the group per step): as many
+  // as the mean group length uses -- short groups (a replication task's batch: 1-3 rows) take one or two
+  const u64 lane_rows = n_groups ? S->n_slots / 64 : 0;   // (the tail counted too: an upper bound)
+  u32 waves = n_groups ? (u32)((lane_rows + n_groups - 1) / n_groups) : 1;
+  waves = waves < 1 ? 1 : waves > 16 ? 16 : waves;
+  if (n_groups) hipLaunchKernelGGL(layout_groups_kernel, dim3(n_groups), dim3(64 * waves), 0, s, *in, P, D, n_lane, n_groups);
   if (n_tail) hipLaunchKernelGGL(layout_tail_kernel, dim3(n_tail), dim3(kBlock), 0, s, *in, P, D, n_lane, n_groups, n_tail);
   if (nw) hipLaunchKernelGGL(layout_wf_kernel, dim3((nw + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, P, D, n_lane,
                              n_groups, n_tail);

@@ -199,9 +199,10 @@ class DeviceIngest:
         if rc != 0:
             raise RuntimeError(f"crr_ingest_layout_resume failed: {rc}")
 
-    def allocate_inputs(self, S: CIngestSummary, T: dict, ci: abi.CInputs, slack: float = 1.0):
+    def allocate_inputs(self, S: CIngestSummary, T: dict, ci: abi.CInputs, slack: float = 1.0, wf_in_place=None):
         """(Re)allocate the event columns, side records, reset keys and descriptors a resume layout writes
-        into ``T`` (``slack`` x the summary's sizes, reused while large enough) and point ``ci`` at them."""
+        into ``T`` (``slack`` x the summary's sizes, reused while large enough) and point ``ci`` at them;
+        ``wf_in_place``: a device tensor of the loaded descriptors the layout updates in place instead."""
         torch, dev = self.torch, self.eng.dev
         need = {"ev_" + name: max(int(S.n_slots), 1) * np.dtype(t).itemsize + 16 for name, t in abi.EVENT_COLUMNS}
         need.update({"act_side": int(S.n_act_side) * abi.ACTIVITY_SIDE.itemsize + 16,
@@ -215,6 +216,8 @@ class DeviceIngest:
             setattr(ci.ev, name, T["ev_" + name].data_ptr())
         for k in ("act_side", "start_side", "reset_keys", "wf"):
             setattr(ci, k, T[k].data_ptr())
+        if wf_in_place is not None:
+            ci.wf = wf_in_place.data_ptr()
 
     @staticmethod
     def input_shapes(S: CIngestSummary):

@@ -348,12 +348,13 @@ class BlobReplication:
         self.db = DeviceBatch(pr.db_new.batch, T, ci, pr.db_new.c_out, eng.device)
         self.tensors = T
         S = self.ing.plan(self.blobs, resume=R)
-        self.ing.allocate_inputs(S, T, ci, slack=1.05)
+        # the loaded descriptors are the replay's: the layout writes the new events' fields into them in place
+        self.ing.allocate_inputs(S, T, ci, slack=1.05, wf_in_place=T["loaded_wf"])
         self.n_events = int(S.n_events)
 
     def step(self, stream=None):
         S = self.ing.plan(self.blobs, stream, resume=self.resume)
-        self.ing.allocate_inputs(S, self.tensors, self.db.c_in, slack=1.05)
+        self.ing.allocate_inputs(S, self.tensors, self.db.c_in, slack=1.05, wf_in_place=self.tensors["loaded_wf"])
         self.ing.layout_resume(self.blobs, self.resume, S, self.db.c_in, stream)
         self.pr.eng.launch(self.db, stream)
         return S

@@ -142,7 +142,8 @@ int crr_ingest_layout(const crr_blob_batch* in, void* scratch, size_t scratch_by
  * crr_ingest_layout.  key_begin must be the exclusive prefix sum of key_count; the scratch must hold the
  * seeded keys' hash-table entries too (summary.err CRR_INGEST_SCRATCH_TOO_SMALL: plan again with more). */
 typedef struct crr_ingest_resume {
-    const crr_workflow* loaded_wf;  /* [n_wf] device order */
+    const crr_workflow* loaded_wf;  /* [n_wf] device order; may be the layout's own dst->wf (then only
+                                       ev_begin / ev_count / empty_batch_at / flags are written, in place) */
     uint32_t        wave_begin;     /* the loaded layout's lane / tail split (<= n_wf) */
     uint32_t        reserved;
     const uint32_t* key_begin;      /* [n_wf] */

@@ -179,7 +179,7 @@ def test_inconsistent_loaded_states_route_to_retry_or_capacity(engine):
         assert same[~own].all(), name
 
 
-@pytest.mark.parametrize("gen", ["native", "python"])
+@pytest.mark.parametrize("gen", ["native", "python", "long"])
 def test_passive_replication_from_blobs_on_device(gen):
     """Passive replication from the task's persisted bytes (replication_task.go:386-390 -> serializer.go:109-119,
     then ApplyEvents onto the loaded state): the last batches' thriftrw blobs, resident in HBM, are decoded and
@@ -195,9 +195,12 @@ def test_passive_replication_from_blobs_on_device(gen):
     eng = ReplayEngine(0)
     if gen == "native":
         canon = synth_native.mixed(20000, can_rate=0.3, multi_version=True)
-    else:
+    elif gen == "python":
         canon = flatten(synth_mixed.mixed_histories(3000, 45, mean_len=120, multi_version=True, can_rate=0.3,
                                                     invalid_rate=0.05),
+                        known_domains={"domain-a", "domain-b", "parent-domain"})
+    else:   # long histories: loaded dictionaries past 64 keys take the lane-per-workflow resume pass
+        canon = flatten(synth_mixed.long_tail_histories(150, 62, max_len=4000, run_cap=2000, multi_version=True, caps=None),
                         known_domains={"domain-a", "domain-b", "parent-domain"})
     b = interleave(canon, long_threshold=150)
     pr = PassiveReplication(eng, b)
@@ -224,7 +227,7 @@ def test_passive_replication_from_blobs_on_device(gen):
     et = sb.cols["etype"] & abi.ETYPE_MASK
     g_side = T["act_side"][:int(S.n_act_side) * abi.ACTIVITY_SIDE.itemsize].cpu().numpy().view(abi.ACTIVITY_SIDE)
     sched = et == ET.ActivityTaskScheduled   # the side record it names
-    assert sched.sum() > 100
+    assert sched.sum() > (3 if gen == "long" else 100)
     assert g_side[got["aux"][sched]].tobytes() == sb.act_side[sb.cols["aux"][sched]].tobytes()
     # ActivityTaskStarted joined to a scheduled event of the same new batch (rare in a last batch: the scheduled
     # one is usually in the loaded state, where the replay reads the loaded row)
@@ -232,7 +235,7 @@ def test_passive_replication_from_blobs_on_device(gen):
     assert g_side[got["aux"][started]].tobytes() == sb.act_side[sb.cols["aux"][started]].tobytes()
     rest = ~np.isin(et, [ET.ActivityTaskScheduled, ET.ActivityTaskStarted, ET.WorkflowExecutionStarted])
     np.testing.assert_array_equal(got["aux"][rest], sb.cols["aux"][rest])
-    g_wf = T["wf"][:b.n_wf * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)
+    g_wf = T["loaded_wf"][:b.n_wf * abi.WORKFLOW.itemsize].cpu().numpy().view(abi.WORKFLOW)   # (updated in place)
     assert g_wf.tobytes() == sb.wf.tobytes()
     # the rows: the host path's step, byte for byte
     assert dev.exec.tobytes() == host.exec.tobytes()
@@ -240,4 +243,4 @@ def test_passive_replication_from_blobs_on_device(gen):
         if name != "tasks":
             assert dev.tables[name].tobytes() == host.tables[name].tobytes(), name
     vo = pr.verify_oracle(_oracle().replay, 0)
-    assert vo["mismatches"] == 0 and vo["compared_workflows"] > 0.5 * b.n_wf, vo
+    assert vo["mismatches"] == 0 and vo["compared_workflows"] > 0.5 * int(pr.split.sum()), vo

@@ -24,6 +24,8 @@ def main():
     p.add_argument("--no-started-aux", action="store_true", help="CRR_IN_STARTED_AUX off (A/B)")
     p.add_argument("--hbm-rows", action="store_true", help="every lane workflow over its HBM rows (round-3 path)")
     p.add_argument("--phases", action="store_true", help="a -DCRR_PHASE_PROF=1 library: per-phase wave clocks")
+    p.add_argument("--blobs", action="store_true", help="the step from the tasks' persisted blobs (BlobReplication: "
+                                                          "device resume ingest + replay), wall time per step")
     a = p.parse_args()
     if a.lib:
         os.environ["CRR_LIB_PATH"] = os.path.abspath(a.lib)
@@ -36,7 +38,8 @@ def main():
     from cadence_amd.replication import PassiveReplication
 
     t0 = time.time()
-    batch = interleave(synth_native.mixed(a.wf, shard=(cdist.NUM_SHARDS, 1, 0)), long_threshold=256)   # bench.py's N=1 shard
+    canon = synth_native.mixed(a.wf, shard=(cdist.NUM_SHARDS, 1, 0))
+    batch = interleave(canon, long_threshold=256)   # bench.py's N=1 shard
     batch.started_aux = not a.no_started_aux
     eng = ReplayEngine(0)
     db = eng.upload(batch)
@@ -47,6 +50,22 @@ def main():
     pr = PassiveReplication(eng, batch, hbm_rows=a.hbm_rows, live_ids=not a.no_live_ids)
     pr.setup()
     setup_s = time.time() - t0
+    if a.blobs:
+        from cadence_amd.blobs import encode_batch
+        from cadence_amd.replication import BlobReplication
+        br = BlobReplication(pr, encode_batch(canon))
+        br.setup()
+        wall = []
+        for _ in range(a.reps + 1):
+            pr.restore()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            br.step()
+            torch.cuda.synchronize()
+            wall.append((time.perf_counter() - t1) * 1e3)
+        print(json.dumps({"blobs": True, "workflows": pr.batch.n_wf, "events": br.n_events, "step_ms": wall[1:],
+                          "median_ms": float(np.median(wall[1:])), "verify": pr.verify(one_shot)}), flush=True)
+        return
     ms = []
     if a.phases:
         import ctypes

@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--c4-workflows", type=int, default=2000, help="config 4 logical workflows per GPU")
     p.add_argument("--c5-workflows", type=int, default=1_000_000, help="config 5 multi-version workflows per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-token-crc", action="store_true", help="hash the start tokens in the replay (A/B of crr_inputs.token_crc)")
     p.add_argument("--no-e2e", action="store_true", help="skip the host-buffer, host-ingest and blob -> rows figures")
     p.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: the CPUs this process may use)")
     p.add_argument("--cpu-sample", type=int, default=1_000_000, help="config 2 workflows in the CPU baseline sample")
@@ -176,7 +177,7 @@ def config2(ctx):
     ids = cdist.rank_workflows(args.workflows * ctx.world, ctx.rank, ctx.world)
     canon = synth.activity_chain(ids.size, k, synth.SEED_C2, with_keys=False, wf_ids=ids)
     batch = interleave(canon)
-    db = eng.upload(batch)
+    db = eng.upload(batch, token_crc=not ctx.args.no_token_crc)
     # the digest is folded into every replay launch (crr_outputs.digest), bound to each device position's
     # global workflow ID; the step's exchange is then the one RCCL all-reduce of its 1-KB buffer
     eng.enable_digest(db, cdist.device_keys(batch, ids))
@@ -200,7 +201,7 @@ def config2(ctx):
     kernel_name = f"{tier}<{str(tail).lower()}, {str(emit).lower()}"  # <WAVE_TAIL, EMIT[, LANES]>, as rocprofv3 names it
     # the small tier's third parameter (divergent dispatch) is set only for multi-segment (mixed) batches
     kernel_name += ", false>" if tier == "replay_lds_small_kernel" else ">"
-    alg_bytes = synth.algorithmic_bytes(batch, res)
+    alg_bytes = synth.algorithmic_bytes(batch, res, token_crc=not ctx.args.no_token_crc)
     traffic = None
     if os.path.exists(PROFILE_TRAFFIC):
         try:
@@ -269,7 +270,7 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256, g
     t1 = time.time()
     batch = interleave(canon, long_threshold=long_threshold)
     t2 = time.time()
-    db = eng.upload(batch)
+    db = eng.upload(batch, token_crc=not ctx.args.no_token_crc)
     keys = digest_keys(ctx, batch, global_ids)
     eng.enable_digest(db, keys)
     wall, ms = timed_steps(ctx, db, args.config_steps, 1, per_step=digest_exchange(ctx, db))
@@ -283,7 +284,7 @@ def run_config(ctx, name, make_canon, workload, sample_fn, long_threshold=256, g
            "workflows_per_s": tot_wf * args.config_steps / wall,
            "tiers": list(batch.tiers) if batch.tiers else None, "wave_tail": batch.n_wf - (batch.wave_begin or batch.n_wf),
            "digest": dg,
-           "roofline": roofline(synth.algorithmic_bytes(batch, res), grp_ms, FAST_GROUP,
+           "roofline": roofline(synth.algorithmic_bytes(batch, res, token_crc=not ctx.args.no_token_crc), grp_ms, FAST_GROUP,
                                 config_traffic(name, batch.n_wf, batch.n_events)),
            "setup_s": {"generate": t1 - t0, "interleave": t2 - t1}}
     if ctx.rank == 0:
@@ -503,7 +504,7 @@ def config5(ctx, n_wf, shard, global_ids=None):
     canon = as_rebuilds(synth_native.mixed(n_wf * ctx.world, multi_version=True, shard=shard, seed=0xCAD00005), 0xCAD00005,
                         global_ids)
     batch = interleave(canon)
-    db = eng.upload(batch)
+    db = eng.upload(batch, token_crc=not ctx.args.no_token_crc)
     setup = time.time() - t0
     keys = digest_keys(ctx, batch, global_ids)
     eng.enable_digest(db, keys)
@@ -520,7 +521,7 @@ def config5(ctx, n_wf, shard, global_ids=None):
                        "events_per_gpu": batch.n_events, "workflows_per_gpu": batch.n_wf,
                        "workflows_ok": dg["digest"][1], "digest": dg,
                        "vh_items_per_workflow": float(res.exec["n_vh_items"][res.exec["status"] == 0].mean()),
-                       "roofline": roofline(synth.algorithmic_bytes(batch, res), float(np.mean(ms)), FAST_GROUP,
+                       "roofline": roofline(synth.algorithmic_bytes(batch, res, token_crc=not ctx.args.no_token_crc), float(np.mean(ms)), FAST_GROUP,
                                             config_traffic("config5_rebuild", batch.n_wf, batch.n_events)),
                        "setup_s": setup}}
     if ctx.rank == 0:

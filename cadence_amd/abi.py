@@ -8,7 +8,7 @@ import enum
 
 import numpy as np
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # common/constants.go:30-58
 FIRST_EVENT_ID = 1
@@ -296,7 +296,8 @@ class CInputs(ctypes.Structure):
                 ("n_wf", ctypes.c_uint32), ("stride", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("wave_begin", ctypes.c_uint32), ("large_begin", ctypes.c_uint32), ("compact_begin", ctypes.c_uint32),
                 ("compact2_begin", ctypes.c_uint32), ("wide_begin", ctypes.c_uint32),
-                ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32), ("digest_keys", ctypes.c_void_p)]
+                ("big_begin", ctypes.c_uint32), ("hbm_begin", ctypes.c_uint32), ("digest_keys", ctypes.c_void_p),
+                ("token_crc", ctypes.c_void_p)]
 
 
 # the live-ID sidecar (crr_outputs.live_ids, ABI v6): one int64 column per pending map, addressed like its rows

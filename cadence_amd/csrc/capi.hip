@@ -27,6 +27,7 @@ __global__ void replay_global_kernel(crr_inputs in, crr_outputs out, int phase, 
 __global__ void tail_gate_kernel(const uint32_t* scratch, uint32_t need);
 __global__ void replay_retry_kernel(crr_inputs in, crr_outputs out, int phase);
 __global__ void checksum_kernel(crr_inputs in, crr_outputs out, uint32_t* checksums);
+__global__ void token_crc_kernel(crr_inputs in, uint32_t* out);
 }
 
 namespace {
@@ -448,6 +449,16 @@ int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksu
   if (!on_dev.ok) return (int)hipErrorInvalidHandle;
   const unsigned grid = (in->n_wf + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(crr::checksum_kernel, dim3(grid), dim3(kBlock), 0, s, *in, *out, checksums);
+  return (int)hipGetLastError();
+}
+
+int crr_token_crc(const crr_inputs* in, uint32_t* crc, void* stream) {
+  if (!in || (in->n_wf && (!in->wf || !in->arena || !crc))) return -1;
+  if (in->n_wf == 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  StreamDevice on_dev(s);
+  if (!on_dev.ok) return (int)hipErrorInvalidHandle;
+  hipLaunchKernelGGL(crr::token_crc_kernel, dim3((in->n_wf + 255) / 256), dim3(256), 0, s, *in, crc);
   return (int)hipGetLastError();
 }
 

@@ -134,6 +134,11 @@ struct Crc {
     nbuf = 0;
     return ~crc;
   }
+  // kSpliceBytes bytes whose raw CRC (from a zero register) is `raw`: the bytes still buffered go in first, then
+  // the register advances over kSpliceBytes zero bytes -- linear in the register: r -> sum of the columns of
+  // kShiftSplice its set bits select -- and the bytes' own contribution is XORed in (the update is linear
+  // over GF(2) in register and data together)
+  __device__ __forceinline__ void splice(u32 raw);
 };
 
 // The same slicing-by-8 tables built at compile time in constant memory, for kernels that keep no CRC
@@ -155,6 +160,54 @@ constexpr CrcTab make_crc_tab() {
   return T;
 }
 __constant__ CrcTab kCrcGlobal = make_crc_tab();
+
+// the splice length: NewHistoryBranchToken's 96-byte HistoryBranch (tree and branch UUIDs, no ancestors)
+constexpr u32 kSpliceBytes = 96;
+struct ShiftCols { u32 v[32]; };
+constexpr ShiftCols make_shift_cols() {   // column i: the register 1 << i advanced over kSpliceBytes zero bytes
+  const CrcTab T = make_crc_tab();
+  ShiftCols c{};
+  for (int i = 0; i < 32; ++i) {
+    u32 r = 1u << i;
+    for (u32 k = 0; k < kSpliceBytes; ++k) r = T.v[r & 0xff] ^ (r >> 8);
+    c.v[i] = r;
+  }
+  return c;
+}
+__constant__ ShiftCols kShiftSplice = make_shift_cols();
+
+__device__ __forceinline__ void Crc::splice(u32 raw) {
+  for (int i = 0; i < nbuf; ++i) {
+    const u32 b = (u32)(buf >> (8 * i)) & 0xff;
+    crc = T[(crc ^ b) & 0xff] ^ (crc >> 8);
+  }
+  nbuf = 0;
+  buf = 0;
+  u32 r = raw;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) r ^= kShiftSplice.v[i] & (0u - ((crc >> i) & 1u));   // the column index is uniform
+  crc = r;
+  len += kSpliceBytes;
+}
+
+// crr_token_crc: a lane per workflow, the raw CRC of its start token (the constant tables, through the L1)
+__global__ void __launch_bounds__(256) token_crc_kernel(crr_inputs in, u32* out) {
+  const u32 w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= in.n_wf) return;
+  const crr_workflow* wfp = in.wf + w;
+  const u32 off = wfp->start_token_off, len = wfp->start_token_len;
+  Crc K;
+  K.init(kCrcGlobal.v);
+  K.crc = 0u;
+  const uint8_t* tp = in.arena + off;
+  u32 i = 0;
+  if ((off & 7u) == 0) {
+    const u64* tw = reinterpret_cast<const u64*>(tp);
+    for (; i + 8 <= len; i += 8) K.push(tw[i >> 3], 8);
+  }
+  for (; i < len; ++i) K.u8(tp[i]);
+  out[w] = ~K.finish();
+}
 
 // NT: the block size when the launch fixes it (no read of the dispatch packet), 0: blockDim.x
 template <int NT = 0>
@@ -3137,11 +3190,16 @@ struct TokenWords {
   static constexpr int kWords = 12;
   u64 w[kWords];
   u32 off, len, held;  // held: bytes in w (a multiple of 8)
-  __device__ __forceinline__ void issue(const TokenDesc& d, i32 token_src, const uint8_t* arena) {
+  u32 raw;             // spliced: the start token's raw CRC (crr_inputs.token_crc), no word read
+  bool spliced;
+  __device__ __forceinline__ void issue(const TokenDesc& d, i32 token_src, const uint8_t* arena,
+                                        const uint32_t* token_crc = nullptr, u32 wi = 0) {
     off = 0; len = 0;
     if (token_src == 1) { off = d.so; len = d.sl; }
     if (token_src == 2) { off = d.fo; len = d.fl; }
-    held = (off & 7u) ? 0u : (len & ~7u);
+    spliced = token_src == 1 && token_crc != nullptr && len == kSpliceBytes;
+    raw = spliced ? token_crc[wi] : 0u;
+    held = (off & 7u) || spliced ? 0u : (len & ~7u);
     held = held < 8u * kWords ? held : 8u * kWords;
     const u64* tw = reinterpret_cast<const u64*>(arena + off);
 #pragma unroll
@@ -3192,7 +3250,9 @@ __device__ __forceinline__ u32 payload_crc(const crr_exec_row& R, const IDS& ids
   K.list_header(20, 12, 1u);                                             //   Histories: list<struct> of 1
   const u32 tlen = TW.len;
   K.field(11, 10); K.be32(tlen);                                         //   VersionHistory.BranchToken (shared.go:92043)
-  {
+  if (TW.spliced) {
+    K.splice(TW.raw);   // the token's precomputed contribution (crr_inputs.token_crc)
+  } else {
 #pragma unroll
     for (int j = 0; j < TokenWords::kWords; ++j)
       if (8u * j + 8u <= TW.held) K.push(TW.w[j], 8);
@@ -4295,7 +4355,7 @@ done_events:
   // the checksum's branch-token words go out before the row write-back, whose work hides their latency
   bool want_crc = L.status == CRR_OK;
   TokenWords TW;
-  TW.issue(tok, want_crc ? L.token_src : 0, in.arena);
+  TW.issue(tok, want_crc ? L.token_src : 0, in.arena, in.token_crc, w);
   // the workflow's digest key with them: read before the loop it would be held across it (registers the
   // loop spills for), read at the add its round trip would end every wavefront
   u64 dkey = 0;
@@ -4894,7 +4954,7 @@ __global__ void __launch_bounds__(kBlock) checksum_kernel(crr_inputs in, crr_out
   load_geo(G, wfp, out, wf_stride(in, w));
   const crr_exec_row R = out.exec[w];
   TokenWords TW;
-  TW.issue(token_desc(wfp), R.token_src, in.arena);
+  TW.issue(token_desc(wfp), R.token_src, in.arena, in.token_crc, w);
   u32 len = 0;
   if (out.live_ids[0]) {  // the ID lists from the dense sidecar the replay wrote
     const SidecarIds ids{out.live_ids};

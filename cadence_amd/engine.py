@@ -37,6 +37,8 @@ def lib():
         L.crr_replay.restype = ctypes.c_int
         L.crr_checksum.argtypes = [vp, vp, vp, vp]
         L.crr_checksum.restype = ctypes.c_int
+        L.crr_token_crc.argtypes = [vp, vp, vp]
+        L.crr_token_crc.restype = ctypes.c_int
         L.crr_set_device.argtypes = [ctypes.c_int]
         L.crr_set_device.restype = ctypes.c_int
         L.crr_release.restype = ctypes.c_int
@@ -108,7 +110,7 @@ class ReplayEngine:
         self.dev = self.torch.device("cuda", device)
 
     # -- upload ------------------------------------------------------------------------------------
-    def upload(self, batch: HistoryBatch, live_ids: bool = True) -> DeviceBatch:
+    def upload(self, batch: HistoryBatch, live_ids: bool = True, token_crc: bool = True) -> DeviceBatch:
         torch = self.torch
         dev = self.dev
         T = {}
@@ -164,6 +166,14 @@ class ReplayEngine:
             for t, name in enumerate(abi.ID_TABLES):
                 T["ids_" + name] = torch.zeros(max(batch.table_rows.get(name, 0), 1), dtype=torch.int64, device=dev)
                 co.live_ids[t] = T["ids_" + name].data_ptr()
+        if token_crc and batch.n_wf:
+            # crr_inputs.token_crc: each start token's raw CRC, computed once the arena is in HBM (a token is
+            # fixed for its branch); the replay splices it into the checksum instead of hashing the token
+            T["token_crc"] = torch.zeros(batch.n_wf, dtype=torch.int32, device=dev)
+            ci.token_crc = T["token_crc"].data_ptr()
+            s = torch.cuda.current_stream(dev)
+            if self.lib.crr_token_crc(ctypes.byref(ci), ctypes.c_void_p(ci.token_crc), ctypes.c_void_p(s.cuda_stream)) != 0:
+                raise RuntimeError("crr_token_crc failed")
         return DeviceBatch(batch, T, ci, co, self.device)
 
     # -- the fused digest (crr_outputs.digest) -------------------------------------------------------

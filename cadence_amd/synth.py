@@ -217,11 +217,12 @@ def activity_chain(n_wf: int, k: int, seed: int, version: int = 1, with_keys: bo
     return batch
 
 
-def algorithmic_bytes(batch: HistoryBatch, res=None) -> int:
+def algorithmic_bytes(batch: HistoryBatch, res=None, token_crc: bool = True) -> int:
     """Algorithmic HBM bytes of one replay launch (DESIGN.md "Roofline").
 
     reads : 49 B per event (8 columns) + 32 / 48 B per activity / start side record read
-            + the workflow descriptor (168 B) + the branch token bytes checksummed
+            + the workflow descriptor (168 B) + the branch token bytes checksummed (token_crc: a 96-byte
+            start token's 4-byte precomputed CRC instead, crr_inputs.token_crc)
     writes: the execution row (192 B) + 16 B per version-history item + the live pending rows
             (activity 112, timer 40, child 48, request-cancel / signal 32, reset point 16 B)
     """
@@ -230,7 +231,8 @@ def algorithmic_bytes(batch: HistoryBatch, res=None) -> int:
     real = t != abi.EV_PAD
     n_act_sched = int(((t == ET.ActivityTaskScheduled) & real).sum())
     n_started = int(((t == ET.WorkflowExecutionStarted) & real).sum())
-    tok = int(np.minimum(batch.wf["start_token_len"], 4096).sum())
+    tl = np.minimum(batch.wf["start_token_len"].astype(np.int64), 4096)
+    tok = int(np.where(token_crc & (tl == 96), 4, tl).sum())
     b = (n_ev * abi.BYTES_PER_EVENT + abi.ACTIVITY_SIDE.itemsize * n_act_sched + abi.START_SIDE.itemsize * n_started
          + batch.n_wf * abi.WORKFLOW.itemsize + tok)
     b += batch.n_wf * abi.EXEC_ROW.itemsize

@@ -48,7 +48,7 @@ extern "C" {
  *    RefreshTasks' own task rows (task_cap), RefreshTasks' state effects without CRR_IN_EMIT_TASKS too,
  *    the fused digest (crr_inputs.digest_keys, crr_outputs.digest), crr_sizeof(13 / 14)
  * 6: the live-ID sidecar (crr_outputs.live_ids) */
-#define CRR_ABI_VERSION 6
+#define CRR_ABI_VERSION 7
 
 /* ---- constants restated from the reference ------------------------------------------------ */
 /* common/constants.go:30-58 */
@@ -328,6 +328,14 @@ typedef struct crr_inputs {
        per workflow the identity key the digest binds its result to (e.g. a hash of the workflow ID), in batch
        order; NULL (with crr_outputs.digest NULL): no digest. */
     const uint64_t*          digest_keys;
+    /* (ABI v7) Per workflow (batch order) the raw CRC of its start branch token -- the CRC-32 register after
+       the token's bytes from a zero register, no final inversion: what the token contributes to the
+       checksum's GenerateCRC32 (crc.go:35-54) -- as crr_token_crc writes it once the arena is in HBM (a token
+       is fixed for its branch, so the caller computes it once per token).  A 96-byte start token (the
+       HistoryBranch NewHistoryBranchToken writes) is then spliced into the checksum by a 32x32 GF(2) shift
+       of the register instead of being read and hashed byte by byte; NULL, other lengths and final tokens
+       (rebuilds): the token's bytes as before.  Results never depend on it. */
+    const uint32_t*          token_crc;
 } crr_inputs;
 
 #define CRR_IN_HAS_NEW_RUN 1u   /* some workflow carries CRR_WF_FLAG_NEW_RUN: launch phase 0 */
@@ -585,6 +593,10 @@ int crr_replay(const crr_inputs* in, const crr_outputs* out, void* stream);
  * sidecar set (crr_outputs.live_ids, as the replay that wrote the rows left it) the ID lists are read from
  * it, else from the rows. */
 int crr_checksum(const crr_inputs* in, const crr_outputs* out, uint32_t* checksums, void* stream);
+
+/* crr_inputs.token_crc: the raw CRC of every workflow's start token (in->arena at start_token_off /
+ * start_token_len) into crc[n_wf], on `stream`. */
+int crr_token_crc(const crr_inputs* in, uint32_t* crc, void* stream);
 
 /* Batched prepareVersionHistory over device arrays (one result per task). */
 int crr_ndc_prepare(const crr_ndc_inputs* in, crr_ndc_result* results, crr_vh_item* out_items, void* stream);

@@ -318,3 +318,30 @@ def test_live_id_sidecar_matches_rows_every_path(eng):
     pr.restore()
     pr.step()
     check_db("passive", pr.batch, pr.db)
+
+
+@pytest.mark.gpu
+def test_token_crc_splice_matches_hashing_the_token():
+    """crr_inputs.token_crc (ABI v7): the start token's precomputed raw CRC spliced into the checksum by a GF(2)
+    shift of the register gives the same checksums -- replay and the Load verify path -- as hashing the token's
+    bytes (NULL token_crc), on every kernel path, with rebuild (final) tokens and odd token lengths left to the
+    bytes."""
+    from cadence_amd import abi, synth, synth_native
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.flatten import interleave
+    eng = ReplayEngine(0)
+    batches = [interleave(synth.activity_chain(5000, 4, synth.SEED_C2, with_keys=False)),
+               interleave(synth_native.mixed(20000, multi_version=True, can_rate=0.3)),
+               interleave(synth_native.long_tail(30, max_len=12_000, run_cap=4_000))]
+    for b in batches:
+        got, want = [], []
+        for tc, out in ((True, got), (False, want)):
+            db = eng.upload(b, token_crc=tc)
+            assert bool(db.c_in.token_crc) == tc
+            eng.launch(db)
+            res = eng.download(db)
+            out.append(res.exec.tobytes())
+            out.append(eng.checksum(db).tobytes())
+        assert got == want
+        ex = np.frombuffer(got[0], abi.EXEC_ROW)
+        assert (ex["status"] == 0).sum() > 0.5 * b.n_wf

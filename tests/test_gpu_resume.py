@@ -244,3 +244,52 @@ def test_passive_replication_from_blobs_on_device(gen):
             assert dev.tables[name].tobytes() == host.tables[name].tobytes(), name
     vo = pr.verify_oracle(_oracle().replay, 0)
     assert vo["mismatches"] == 0 and vo["compared_workflows"] > 0.5 * int(pr.split.sum()), vo
+
+
+def test_resume_ingest_seed_scratch_and_bad_blobs():
+    """crr_ingest_plan_resume's edges: loaded dictionaries larger than the scratch's table region report
+    CRR_INGEST_SCRATCH_TOO_SMALL with the events counted right (DeviceIngest.plan then grows the scratch and the
+    step's rows still equal the host path's); a task whose blob is not thriftrw fails the plan as the host
+    decoder does (CadenceDeserializationError, serializer.go:320-333), naming that blob."""
+    import ctypes
+    from cadence_amd import abi
+    from cadence_amd.blobs import BlobSet, encode_batch
+    from cadence_amd.engine import ReplayEngine
+    from cadence_amd.ingest import SCRATCH_TOO_SMALL, CIngestSummary, IngestError
+    from cadence_amd.replication import BlobReplication, PassiveReplication
+    eng = ReplayEngine(0)
+    canon = flatten(synth_mixed.long_tail_histories(150, 62, max_len=4000, run_cap=2000, multi_version=True, caps=None),
+                    known_domains={"domain-a", "domain-b", "parent-domain"})
+    b = interleave(canon, long_threshold=150)
+    pr = PassiveReplication(eng, b)
+    pr.setup()
+    pr.restore()
+    pr.step()
+    want = eng.download(pr.db)
+    br = BlobReplication(pr, encode_batch(canon))
+    br.setup()
+    ing, db = br.ing, br.blobs
+    n_ev = br.n_events
+    assert int(br.tensors["key_count"].cpu().numpy().astype(np.int64).sum()) > 4 * n_ev   # the seeds dominate the table region
+    size = int(ing.lib.crr_ingest_scratch_bytes(db.c.n_blobs, db.c.n_wf, n_ev + 1))   # the events fit, the seeds not
+    ing.scratch = ing.torch.zeros(size, dtype=ing.torch.uint8, device=eng.dev)
+    ing.scratch_bytes = size
+    S = CIngestSummary()
+    s = eng.torch.cuda.current_stream(eng.dev)
+    rc = ing.lib.crr_ingest_plan_resume(ctypes.byref(db.c), ctypes.byref(br.resume), ctypes.c_void_p(ing.scratch.data_ptr()),
+                                        ctypes.c_size_t(size), ctypes.byref(S), ctypes.c_void_p(s.cuda_stream))
+    assert rc == 0 and S.err == SCRATCH_TOO_SMALL and S.n_events == n_ev
+    pr.restore()
+    br.step()                                   # DeviceIngest.plan: grow and plan again
+    got = eng.download(pr.db)
+    assert got.exec.tobytes() == want.exec.tobytes()
+    # a corrupt task payload: the first blob's preamble byte
+    rb = br.blobs.blobs
+    i = int(np.nonzero(rb.wf["blob_count"] > 0)[0][0])
+    j = int(rb.wf["blob_begin"][i])
+    bad = rb.bytes.copy()
+    bad[int(rb.blob_off[j])] ^= 0xFF
+    br.blobs = ing.upload(BlobSet(bytes=bad, blob_off=rb.blob_off, wf=rb.wf, strings=rb.strings))
+    with pytest.raises(IngestError) as e:
+        br.step()
+    assert e.value.blob == j

@@ -377,7 +377,7 @@ def passive_replication(ctx, batch, one_shot, make_canon=None):
            "ms_per_step": wall / args.config_steps * 1e3, "steps": args.config_steps,
            "events_per_gpu": pr.n_events, "tasks_per_gpu": v["split_workflows"],
            "vs_one_shot": v,
-           "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP,
+           "roofline": roofline(_resume_bytes(pr), float(np.mean(ms)), FAST_GROUP,   # (replication uploads splice)
                                 config_traffic("passive_replication", pr.batch.n_wf, pr.n_events))}
     if blob_path is not None:
         out["blob_path"] = blob_path
@@ -477,16 +477,18 @@ def replication_blob_path(ctx, pr, make_canon):
     return out
 
 
-def _resume_bytes(pr):
+def _resume_bytes(pr, token_crc=True):
     """Algorithmic bytes of one replication step: the new events' columns, the descriptor, the loaded
-    exec row read and written, the loaded + final live rows (read, then written back), the token."""
+    exec row read and written, the loaded + final live rows (read, then written back), the token (its 4-byte
+    precomputed CRC with crr_inputs.token_crc)."""
     from cadence_amd import abi
     b = pr.batch
     ex = pr.prefix.exec
     rows = (112 * ex["n_activity"].astype(np.int64).sum() + 40 * ex["n_timer"].astype(np.int64).sum()
             + 48 * ex["n_child"].astype(np.int64).sum() + 32 * (ex["n_rc"].astype(np.int64).sum() + ex["n_signal"].astype(np.int64).sum())
             + 16 * ex["n_vh_items"].astype(np.int64).sum() + 16 * ex["n_reset_points"].astype(np.int64).sum())
-    return int(pr.n_events * abi.BYTES_PER_EVENT + b.n_wf * (abi.WORKFLOW.itemsize + 2 * abi.EXEC_ROW.itemsize + 96) + 2 * rows)
+    return int(pr.n_events * abi.BYTES_PER_EVENT + b.n_wf * (abi.WORKFLOW.itemsize + 2 * abi.EXEC_ROW.itemsize
+                                                             + (4 if token_crc else 96)) + 2 * rows)
 
 
 # ---- config 5: NDC / XDC -----------------------------------------------------------------------------------------

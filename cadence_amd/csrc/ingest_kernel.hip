@@ -1715,7 +1715,12 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   }
   u64* tab = P.table + tbase;
   const u32 cap_i = pow2_at_least(2 * (n + nr + K) + 2);
-  for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
+  // resuming with a small loaded dictionary and no previous reset points: a linear search -- the loaded keys by
+  // length and bytes, then this batch's earlier new keys by hash and bytes -- instead of a hash table to clear
+  // and K loaded strings to hash (a replication task's batch holds a named key or two)
+  const bool linear = P.resume && nr == 0 && K <= 64;
+  if (!linear)
+    for (u32 i = 0; i < cap_i; ++i) tab[i] = 0;
   auto seed_ref = [&](u32 k) -> KeyRef {   // (the hash through 8-byte unaligned loads: the pad follows the seeds)
     KeyRef r;
     r.off = P.key_off[kb + k]; r.len = P.key_len[kb + k];
@@ -1751,6 +1756,18 @@ __global__ void wf_pass_kernel(crr_blob_batch in, Plan P) {
   u32 next_key = K + 1;
   auto intern = [&](const KeyRef& kr, u32 entry) -> u32 {
     if (kr.len == 0) return 0u;
+    if (linear) {
+      for (u32 k = 0; k < K; ++k)
+        if (P.key_len[kb + k] == kr.len && same_bytes(in.bytes, kr.off, P.key_off[kb + k], kr.len)) return k + 1;
+      for (u32 j = 0; j < entry; ++j) {   // this batch's earlier events: a new key is > K
+        if (P.key[e0 + j] <= K) continue;
+        const KeyRef o = P.keys[e0 + j];
+        if (o.len == kr.len && o.hash == kr.hash &&
+            (kr.len <= 16 ? (o.head[0] == kr.head[0] && o.head[1] == kr.head[1]) : same_bytes(in.bytes, kr.off, o.off, kr.len)))
+          return P.key[e0 + j];
+      }
+      return next_key++;
+    }
     if (!seeded) seed_all();
     u32 slot = kr.hash & (cap_i - 1);
     for (;;) {

@@ -75,6 +75,44 @@ class BlobSet:
         return out
 
 
+def blobset_from_sources(sources: List[decode.WorkflowSource]):
+    """Host-decoder inputs (blobs of any encoding, as persistence returned them) laid out for the device
+    ingest: the BlobSet (to_sources' inverse) and each blob's CRR_ENCODING_* (uint32; an encoding name
+    the serializer does not know maps to 0xFF, NewUnknownEncodingTypeError)."""
+    blobs, encs, strings = [], [], bytearray()
+    wf = np.zeros(len(sources), BLOB_WF)
+
+    def put(b: bytes):
+        strings.extend(b)
+        return len(strings) - len(b), len(b)
+
+    for w, s in enumerate(sources):
+        r = wf[w]
+        r["blob_begin"], r["blob_count"] = len(blobs), len(s.blobs)
+        blobs.extend(s.blobs)
+        encs.extend(decode.ENCODINGS.get("thriftrw" if s.encodings is None else e, 0xFF)
+                    for e in (s.encodings or [None] * len(s.blobs)))
+        r["init_version"], r["now_ns"] = s.domain_failover_version, s.now_ns
+        r["run_id_off"], r["run_id_len"] = put(s.run_id.encode())
+        r["branch_id_off"], r["branch_id_len"] = put(s.branch_id.encode())
+        if s.final_token is None:
+            r["final_token_off"], r["final_token_len"] = 0, abi.NO_TOKEN
+        else:
+            r["final_token_off"], r["final_token_len"] = put(bytes(s.final_token))
+        r["rebuild_last_event_id"], r["rebuild_last_event_version"] = s.rebuild_last_event_id, s.rebuild_last_event_version
+        r["new_run_wf"] = -1 if s.new_run is None else int(s.new_run)
+        r["flags"] = (abi.WF_FLAG_NEW_RUN if s.is_new_run else 0) | (abi.WF_FLAG_REFRESH_TASKS if s.refresh_tasks else 0)
+        r["retention_days"] = s.retention_days
+    lens = np.array([len(b) for b in blobs], np.uint64)
+    off = np.zeros(len(blobs) + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.zeros(int(off[-1]) + 32, np.uint8)
+    if blobs:
+        data[:int(off[-1])] = np.frombuffer(b"".join(blobs), np.uint8)
+    st = np.frombuffer(bytes(strings), np.uint8).copy() if strings else np.zeros(1, np.uint8)
+    return BlobSet(bytes=data, blob_off=off, wf=wf, strings=st), np.array(encs, np.uint32)
+
+
 def _lib():
     L = decode.lib()
     if not getattr(L, "_encode_bound", False):

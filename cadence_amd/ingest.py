@@ -37,6 +37,12 @@ class CIngestSummary(ctypes.Structure):
                 ("tiers", ctypes.c_uint32 * 6), ("has_new_run", ctypes.c_uint32), ("lds_small_tail", ctypes.c_uint32)]
 
 
+class CTranscodeSummary(ctypes.Structure):
+    """crr_transcode_summary (cadence_ingest.h): what crr_ingest_transcode_plan reports."""
+    _fields_ = [("err", ctypes.c_int32), ("reserved", ctypes.c_int32), ("err_blob", ctypes.c_int64),
+                ("n_bytes", ctypes.c_uint64), ("n_deep", ctypes.c_uint32), ("reserved1", ctypes.c_uint32)]
+
+
 class CIngestResume(ctypes.Structure):
     """crr_ingest_resume (cadence_ingest.h): the loaded states a resume ingest continues."""
     _fields_ = [("loaded_wf", ctypes.c_void_p), ("wave_begin", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
@@ -74,16 +80,33 @@ def _bind(L):
     L.crr_ingest_plan_resume.restype = ctypes.c_int
     L.crr_ingest_layout_resume.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
     L.crr_ingest_layout_resume.restype = ctypes.c_int
+    L.crr_ingest_transcode_scratch_bytes.argtypes = [ctypes.c_uint32]
+    L.crr_ingest_transcode_scratch_bytes.restype = ctypes.c_size_t
+    L.crr_ingest_transcode_plan.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp]
+    L.crr_ingest_transcode_plan.restype = ctypes.c_int
+    L.crr_ingest_transcode.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp]
+    L.crr_ingest_transcode.restype = ctypes.c_int
     L._ingest_bound = True
     return L
 
 
 @dataclasses.dataclass
 class DeviceBlobs:
-    """A BlobSet resident in HBM (the upload of what persistence returned) and its C view."""
+    """A BlobSet resident in HBM (the upload of what persistence returned) and its C view.  `pending`: a
+    rejection the transcode of its JSON blobs reported, (code, blob), raised by the plan unless the plan
+    finds a failing blob of a lower index (the host decoder stops at the first failing blob)."""
     blobs: BlobSet
     tensors: dict
     c: CBlobBatch
+    pending: Optional[tuple] = None
+
+
+@dataclasses.dataclass
+class _TranscodedShape:
+    """What DeviceIngest.plan reads of a transcoded batch's BlobSet."""
+    n_bytes: int
+    n_blobs: int
+    n_wf: int
 
 
 class DeviceIngest:
@@ -135,6 +158,55 @@ class DeviceIngest:
         c.n_domains = 0xFFFFFFFF if self.known is None else len(self.known)
         return c
 
+    # -- JSON-encoded blobs: rewritten as thriftrw on the device ---------------------------------------------
+    def transcode(self, db: DeviceBlobs, encodings, stream=None) -> DeviceBlobs:
+        """crr_ingest_transcode_plan + crr_ingest_transcode: the batch with every json / unknown / empty-encoded
+        blob rewritten in HBM as the thriftrw History the decoders read back into the same events
+        (``encodings``: CRR_ENCODING_* per blob, a uint32 array or device tensor).  A rejected blob (BAD_JSON,
+        UNKNOWN_ENCODING) becomes empty and is carried as ``pending`` for the plan to raise."""
+        torch, dev = self.torch, self.eng.dev
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        L = self.lib
+        nb = int(db.c.n_blobs)
+        if isinstance(encodings, torch.Tensor):
+            enc = encodings
+        else:
+            enc = torch.from_numpy(np.ascontiguousarray(encodings, np.uint32).view(np.int32)).to(dev)
+        need = int(L.crr_ingest_transcode_scratch_bytes(nb))
+        if getattr(self, "tscratch", None) is None or self.tscratch.numel() < need:
+            self.tscratch = torch.empty(need, dtype=torch.uint8, device=dev)
+        S = CTranscodeSummary()
+        vp = ctypes.c_void_p
+        rc = L.crr_ingest_transcode_plan(ctypes.byref(db.c), vp(enc.data_ptr()), vp(self.tscratch.data_ptr()),
+                                         ctypes.c_size_t(self.tscratch.numel()), ctypes.byref(S), vp(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_ingest_transcode_plan failed: {rc}")
+        n_bytes = int(S.n_bytes)
+        out_bytes = torch.empty(n_bytes + INGEST_PAD + 16, dtype=torch.uint8, device=dev)
+        out_off = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+        rc = L.crr_ingest_transcode(ctypes.byref(db.c), vp(enc.data_ptr()), vp(self.tscratch.data_ptr()),
+                                    ctypes.c_size_t(self.tscratch.numel()), ctypes.byref(S), vp(out_bytes.data_ptr()),
+                                    vp(out_off.data_ptr()), vp(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"crr_ingest_transcode failed: {rc}")
+        T = dict(db.tensors)
+        T["bytes"], T["blob_off"], T["encodings"] = out_bytes, out_off, enc
+        c = CBlobBatch.from_buffer_copy(db.c)
+        c.bytes, c.blob_off = out_bytes.data_ptr(), out_off.data_ptr()
+        self.last_transcode = S
+        pending = (int(S.err), int(S.err_blob)) if S.err else None
+        return DeviceBlobs(_TranscodedShape(n_bytes, nb, int(db.c.n_wf)), T, c, pending)
+
+    def transcoded_blobs(self, tdb: DeviceBlobs) -> BlobSet:
+        """Download a transcoded batch as a host BlobSet (tests: the host decoder reads it back)."""
+        self.torch.cuda.synchronize(self.eng.dev)
+        off = tdb.tensors["blob_off"].cpu().numpy().view(np.uint64).copy()
+        n = int(off[-1])
+        data = np.zeros(n + INGEST_PAD, np.uint8)
+        data[:n] = tdb.tensors["bytes"][:n].cpu().numpy()
+        wf = tdb.tensors["wf"][:tdb.blobs.n_wf * BLOB_WF.itemsize].cpu().numpy().view(BLOB_WF).copy()
+        return BlobSet(bytes=data, blob_off=off, wf=wf, strings=tdb.tensors["strings"].cpu().numpy().copy())
+
     # -- plan + layout ---------------------------------------------------------------------------------------
     def ensure_scratch(self, db: DeviceBlobs, max_events: int):
         need = int(self.lib.crr_ingest_scratch_bytes(db.c.n_blobs, db.c.n_wf, max_events))
@@ -165,8 +237,10 @@ class DeviceIngest:
             if S.err == SCRATCH_TOO_SMALL:
                 cap = max(2 * cap, int(S.n_events) + 1)
                 continue
-            if S.err:
+            if S.err and (db.pending is None or int(S.err_blob) < db.pending[1]):
                 raise IngestError(int(S.err), int(S.err_blob))
+            if db.pending is not None:
+                raise IngestError(*db.pending)
             return S
 
     def layout(self, db: DeviceBlobs, S: CIngestSummary, stream=None, emit_tasks: bool = False,

@@ -15,8 +15,8 @@
  * The result is byte-identical to the host path (crr_decode_histories, cadence_amd/flatten.interleave
  * with its default long-history threshold and tiering) on the same blobs: the same columns, side
  * records, descriptors, tier boundaries and slot-table sizes.  Only thriftrw (and empty) blobs are
- * decoded here; a batch holding json / unknown-encoded blobs goes through the host decoder
- * (cadence_decode.h).  New batches applied onto loaded states (CRR_WF_FLAG_RESUME, passive replication)
+ * decoded here; a batch holding json / unknown / empty-encoded blobs is first rewritten as thriftrw on
+ * the device (crr_ingest_transcode_plan / crr_ingest_transcode, below).  New batches applied onto loaded states (CRR_WF_FLAG_RESUME, passive replication)
  * take crr_ingest_plan_resume / crr_ingest_layout_resume at the end of this header.
  *
  * Two calls, because the caller sizes the replay's buffers between them:
@@ -157,6 +157,39 @@ int crr_ingest_plan_resume(const crr_blob_batch* in, const crr_ingest_resume* re
 int crr_ingest_layout_resume(const crr_blob_batch* in, const crr_ingest_resume* resume, void* scratch,
                              size_t scratch_bytes, const crr_ingest_summary* summary_host, const crr_inputs* dst,
                              void* stream);
+
+/* ---- JSON-encoded batches: transcoded to thriftrw on the device ------------------------------------------
+ *
+ * serializerImpl.deserialize (common/persistence/serializer.go:312-334) decodes a blob whose encoding is json,
+ * unknown or empty with json.Unmarshal into []*types.HistoryEvent (the host restatement:
+ * cadence_amd/csrc/json_decode.h, crr_decode_histories_enc).  This pair rewrites such blobs in HBM as the
+ * canonical thriftrw History the decoders read back into the same events (json_ingest_kernel.hip), so the
+ * batch then goes through crr_ingest_plan / crr_ingest_layout (or the _resume pair) unchanged:
+ *   crr_ingest_transcode_plan   walk every JSON blob (`encodings[i]`: CRR_ENCODING_* of blob i; NULL: all
+ *                               thriftrw), size its thriftrw form, report the rejected blob with the lowest
+ *                               index (CRR_DECODE_BAD_JSON / CRR_DECODE_UNKNOWN_ENCODING) -- synchronises the
+ *                               stream once to read the sizes back
+ *   crr_ingest_transcode        write the new blob bytes (`out_bytes`: summary.n_bytes + CRR_INGEST_PAD bytes,
+ *                               16-byte aligned) and offsets (`out_blob_off`: n_blobs + 1); thriftrw blobs are
+ *                               copied as they are, a rejected blob becomes empty
+ * The caller then plans the batch { out_bytes, out_blob_off, the same wf / strings / domains }; when the
+ * transcode reported a rejection, the plan's own error wins if its blob index is lower (the host decoder
+ * stops at the first failing blob).  Both calls take the same scratch (crr_ingest_transcode_scratch_bytes). */
+typedef struct crr_transcode_summary {
+    int32_t  err;                   /* CRR_DECODE_* of the rejected blob with the lowest index, 0: none */
+    int32_t  reserved;
+    int64_t  err_blob;              /* its index, -1 */
+    uint64_t n_bytes;               /* bytes of the transcoded batch (without the pad) */
+    uint32_t n_deep;                /* JSON blobs nested past 64 levels (walked with a stack in HBM) */
+    uint32_t reserved1;
+} crr_transcode_summary;
+
+size_t crr_ingest_transcode_scratch_bytes(uint32_t n_blobs);
+int crr_ingest_transcode_plan(const crr_blob_batch* in, const uint32_t* encodings, void* scratch, size_t scratch_bytes,
+                              crr_transcode_summary* summary, void* stream);
+int crr_ingest_transcode(const crr_blob_batch* in, const uint32_t* encodings, void* scratch, size_t scratch_bytes,
+                         const crr_transcode_summary* summary, uint8_t* out_bytes, uint64_t* out_blob_off,
+                         void* stream);
 
 #ifdef __cplusplus
 }

@@ -167,3 +167,23 @@ def test_archival_fixture_json_decodes_natively():
     want = flatten([WorkflowHistory(batches=batches)])
     assert_same_batch(got, want)
     assert got.n_events == 112
+
+
+def test_blobset_from_sources_round_trips():
+    """blobs.blobset_from_sources (the device ingest's upload layout of host-decoder inputs, any encoding)
+    inverts BlobSet.to_sources: the same blobs, encodings and per-workflow inputs decode to the same batch."""
+    from cadence_amd.blobs import blobset_from_sources
+    from cadence_amd.decode import ENCODINGS
+    hs = synth_mixed.mixed_histories(60, 35, multi_version=True, can_rate=0.3)
+    src = json_sources(hs)
+    src[3].blobs, src[3].encodings = serialize_history(hs[3]), None
+    src[5].encodings = [""] * len(src[5].blobs)
+    bs, enc = blobset_from_sources(src)
+    assert bs.n_blobs == sum(len(s.blobs) for s in src) == enc.size
+    back = bs.to_sources()
+    names = {v: k for k, v in ENCODINGS.items()}
+    k = 0
+    for s in back:
+        s.encodings = [names[int(e)] for e in enc[k:k + len(s.blobs)]]
+        k += len(s.blobs)
+    assert_same_batch(decode_histories(back, known_domains=KNOWN), decode_histories(src, known_domains=KNOWN))

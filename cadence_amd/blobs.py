@@ -119,6 +119,8 @@ def _lib():
         vp = ctypes.c_void_p
         L.crr_encode_blobs.argtypes = [vp, vp, vp, vp, ctypes.c_int]
         L.crr_encode_blobs.restype = vp
+        L.crr_encode_blobs_as.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
+        L.crr_encode_blobs_as.restype = vp
         L.crr_encoded_view.argtypes = [vp] + [vp] * 8
         L.crr_encoded_view.restype = None
         L.crr_encoded_free.argtypes = [vp]
@@ -127,8 +129,9 @@ def _lib():
     return L
 
 
-def encode_batch(batch: HistoryBatch, n_threads: int = 0) -> BlobSet:
-    """Persist a canonical batch as thriftrw blobs (one per ApplyEvents batch, in order)."""
+def encode_batch(batch: HistoryBatch, n_threads: int = 0, json: bool = False) -> BlobSet:
+    """Persist a canonical batch as thriftrw blobs (one per ApplyEvents batch, in order); ``json``: as
+    common/types JSON blobs instead (serializer.go:321-325's json encoding; encodings ENCODINGS["json"])."""
     assert batch.stride == 1
     L = _lib()
     keep = []
@@ -151,7 +154,7 @@ def encode_batch(batch: HistoryBatch, n_threads: int = 0) -> BlobSet:
     ko = ptr(batch.key_off) if batch.key_off is not None else None
     kl = ptr(batch.key_len) if batch.key_len is not None else None
     ka = ptr(batch.key_arena) if batch.key_arena is not None else None
-    h = L.crr_encode_blobs(ctypes.byref(ci), ko, kl, ka, int(n_threads))
+    h = L.crr_encode_blobs_as(ctypes.byref(ci), ko, kl, ka, int(n_threads), int(bool(json)))
     if not h:
         raise RuntimeError("crr_encode_blobs failed")
     try:

@@ -12,6 +12,7 @@
 // domain cache {domain-a, domain-b, parent-domain} resolves (or not); a reset point whose binary
 // checksum no event carries is named "rk-<key>".
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -230,7 +231,215 @@ void encode_event(W& w, const Inputs& in, i64 x, u64 wf_no, const std::unordered
   w.stop();   // the event
 }
 
-void encode_range(const Inputs& in, u32 w0, u32 w1, Out* o) {
+
+// ---- the same events as types JSON (json.Marshal of []*types.HistoryEvent, serializer.go:321-325) ---------
+const char* const kEventTypeNames[CRR_EV_TYPE_COUNT] = {
+    "WorkflowExecutionStarted", "WorkflowExecutionCompleted", "WorkflowExecutionFailed", "WorkflowExecutionTimedOut",
+    "DecisionTaskScheduled", "DecisionTaskStarted", "DecisionTaskCompleted", "DecisionTaskTimedOut",
+    "DecisionTaskFailed", "ActivityTaskScheduled", "ActivityTaskStarted", "ActivityTaskCompleted",
+    "ActivityTaskFailed", "ActivityTaskTimedOut", "ActivityTaskCancelRequested", "RequestCancelActivityTaskFailed",
+    "ActivityTaskCanceled", "TimerStarted", "TimerFired", "CancelTimerFailed", "TimerCanceled",
+    "WorkflowExecutionCancelRequested", "WorkflowExecutionCanceled", "RequestCancelExternalWorkflowExecutionInitiated",
+    "RequestCancelExternalWorkflowExecutionFailed", "ExternalWorkflowExecutionCancelRequested", "MarkerRecorded",
+    "WorkflowExecutionSignaled", "WorkflowExecutionTerminated", "WorkflowExecutionContinuedAsNew",
+    "StartChildWorkflowExecutionInitiated", "StartChildWorkflowExecutionFailed", "ChildWorkflowExecutionStarted",
+    "ChildWorkflowExecutionCompleted", "ChildWorkflowExecutionFailed", "ChildWorkflowExecutionCanceled",
+    "ChildWorkflowExecutionTimedOut", "ChildWorkflowExecutionTerminated", "SignalExternalWorkflowExecutionInitiated",
+    "SignalExternalWorkflowExecutionFailed", "ExternalWorkflowExecutionSignaled", "UpsertWorkflowSearchAttributes"};
+const char* const kTimeoutTypeNames[4] = {"START_TO_CLOSE", "SCHEDULE_TO_START", "SCHEDULE_TO_CLOSE", "HEARTBEAT"};
+const char* const kInitiatorNames[3] = {"DECIDER", "RETRYPOLICY", "CRONSCHEDULE"};
+
+struct J {   // a JSON object writer: keys in the order written
+  std::string& b;
+  bool first = true;
+  void key(const char* k) {
+    if (!first) b.push_back(',');
+    first = false;
+    b.push_back('"'); b.append(k); b.append("\":");
+  }
+  void quoted(const std::string& s) {
+    b.push_back('"');
+    for (char c : s) {
+      if (c == '"' || c == '\\') { b.push_back('\\'); b.push_back(c); }
+      else if ((unsigned char)c < 0x20) { char u[8]; snprintf(u, sizeof u, "\\u%04x", (unsigned)(unsigned char)c); b.append(u); }
+      else b.push_back(c);
+    }
+    b.push_back('"');
+  }
+  void i64v(const char* k, i64 v) { key(k); b.append(std::to_string(v)); }
+  void strv(const char* k, const std::string& s) { key(k); quoted(s); }
+  void open(const char* k) { key(k); b.push_back('{'); first = true; }
+  void close() { b.push_back('}'); first = false; }
+  void name_obj(const char* k, const char* name) { open(k); strv("name", name); close(); }
+  void task_list(const char* k, const char* name) { open(k); strv("name", name); strv("kind", "NORMAL"); close(); }
+};
+
+std::string enum_text(const char* const* names, int n, i32 v) {
+  return v >= 0 && v < n ? std::string(names[v]) : std::to_string(v);
+}
+
+// one event (encode_event's fields, as common/types JSON tags)
+void encode_event_json(std::string& b, const Inputs& in, i64 x, u64 wf_no,
+                       const std::unordered_map<u32, std::string>& keystr) {
+  const int t = in.etype[x] & CRR_ETYPE_MASK;
+  const bool valid = t < CRR_EV_TYPE_COUNT;
+  J j{b};
+  b.push_back('{');
+  j.i64v("eventId", in.id[x]);
+  j.i64v("timestamp", in.ts[x]);
+  j.key("eventType");
+  j.quoted(valid ? std::string(kEventTypeNames[t]) : std::string("99"));
+  j.i64v("version", in.ver[x]);
+  j.i64v("taskId", in.task[x]);
+  if (!valid) { b.push_back('}'); return; }
+  auto key = [&]() -> std::string {
+    const u32 n = in.key_len ? in.key_len[x] : 0;
+    if (n) return std::string(in.key_arena + in.key_off[x], n);
+    auto it = keystr.find(in.key[x]);
+    return it == keystr.end() ? std::string() : it->second;
+  };
+  const i64 ref = in.ref[x];
+  const i32 aux = in.aux[x];
+  char rid[37];
+  rid[36] = 0;
+  std::string ak(kEventTypeNames[t]);
+  ak[0] = (char)(ak[0] - 'A' + 'a');
+  ak += "EventAttributes";
+  j.open(ak.c_str());
+  switch (t) {
+    case CRR_EV_WORKFLOW_EXECUTION_STARTED: {
+      const crr_start_side& s = in.start[aux];
+      j.name_obj("workflowType", "workflow-type");
+      if (const char* d = domain_name(s.parent_domain_status, true)) j.strv("parentWorkflowDomain", d);
+      j.task_list("taskList", "task-list");
+      j.strv("input", "aW5wdXQtYnl0ZXM=");
+      j.i64v("executionStartToCloseTimeoutSeconds", s.workflow_timeout);
+      j.i64v("taskStartToCloseTimeoutSeconds", s.decision_start_to_close);
+      if (s.initiator != CRR_INITIATOR_NIL) { j.key("initiator"); j.quoted(enum_text(kInitiatorNames, 3, s.initiator)); }
+      j.strv("identity", "identity");
+      j.i64v("attempt", s.attempt);
+      if (s.expiration_ns) j.i64v("expirationTimestamp", s.expiration_ns);
+      j.i64v("firstDecisionTaskBackoffSeconds", s.first_decision_backoff);
+      if (s.prev_reset_count == -2) {
+        j.open("prevAutoResetPoints"); j.close();
+      } else if (s.prev_reset_count >= 0) {
+        j.open("prevAutoResetPoints");
+        j.key("points");
+        b.push_back('[');
+        for (i32 i = 0; i < s.prev_reset_count; ++i) {
+          const u32 k = in.reset_keys[s.prev_reset_key_off + i];
+          auto it = keystr.find(k);
+          const std::string bc = k == 0 ? std::string() : (it != keystr.end() ? it->second : "rk-" + std::to_string(k));
+          if (i) b.push_back(',');
+          J p{b};
+          b.push_back('{');
+          p.strv("binaryChecksum", bc);
+          p.strv("runId", "prev-run-" + std::to_string(i));
+          p.i64v("firstDecisionCompletedId", 4 + i);
+          p.i64v("createdTimeNano", 1500000000000000000LL + i);
+          p.key("resettable"); b.append("true");
+          b.push_back('}');
+        }
+        b.push_back(']');
+        j.close();
+      }
+      break;
+    }
+    case CRR_EV_DECISION_TASK_SCHEDULED:
+      j.task_list("taskList", "decision-tl"); j.i64v("startToCloseTimeoutSeconds", aux); j.i64v("attempt", ref);
+      break;
+    case CRR_EV_DECISION_TASK_STARTED:
+      request_id(rid, wf_no, (u64)in.id[x]);
+      j.i64v("scheduledEventId", ref); j.strv("identity", "worker-identity"); j.strv("requestId", rid);
+      break;
+    case CRR_EV_DECISION_TASK_COMPLETED: {
+      j.strv("executionContext", "Y3R4"); j.i64v("scheduledEventId", ref - 1); j.i64v("startedEventId", ref);
+      j.strv("identity", "worker-identity");
+      const std::string k = key();
+      if (!k.empty()) j.strv("binaryChecksum", k);
+      break;
+    }
+    case CRR_EV_DECISION_TASK_TIMED_OUT:
+      j.i64v("scheduledEventId", 0); j.i64v("startedEventId", 0);
+      j.key("timeoutType"); j.quoted(enum_text(kTimeoutTypeNames, 4, aux));
+      break;
+    case CRR_EV_ACTIVITY_TASK_SCHEDULED: {
+      const crr_activity_side& a = in.act[aux];
+      j.strv("activityId", key());
+      j.name_obj("activityType", "activity-type");
+      if (const char* d = domain_name(a.domain_status, false)) j.strv("domain", d);
+      j.task_list("taskList", "activity-tl");
+      j.strv("input", "YWN0aXZpdHktaW5wdXQ=");
+      j.i64v("scheduleToCloseTimeoutSeconds", a.schedule_to_close);
+      j.i64v("scheduleToStartTimeoutSeconds", a.schedule_to_start);
+      j.i64v("startToCloseTimeoutSeconds", a.start_to_close);
+      j.i64v("heartbeatTimeoutSeconds", a.heartbeat);
+      j.i64v("decisionTaskCompletedEventId", 4);
+      if (a.has_retry_policy) {
+        j.open("retryPolicy");
+        j.i64v("initialIntervalInSeconds", 1);
+        j.key("backoffCoefficient"); b.append("2");
+        j.i64v("maximumIntervalInSeconds", 100);
+        j.i64v("maximumAttempts", 5);
+        j.key("nonRetriableErrorReasons"); b.append("[\"bad-input\"]");
+        j.i64v("expirationIntervalInSeconds", a.expiration_interval);
+        j.close();
+      }
+      break;
+    }
+    case CRR_EV_ACTIVITY_TASK_STARTED:
+      request_id(rid, wf_no, (u64)in.id[x]);
+      j.i64v("scheduledEventId", ref); j.strv("identity", "worker"); j.strv("requestId", rid); j.i64v("attempt", 0);
+      break;
+    case CRR_EV_ACTIVITY_TASK_TIMED_OUT: case CRR_EV_ACTIVITY_TASK_COMPLETED: case CRR_EV_ACTIVITY_TASK_FAILED:
+    case CRR_EV_ACTIVITY_TASK_CANCELED:
+      j.i64v("scheduledEventId", ref);
+      break;
+    case CRR_EV_ACTIVITY_TASK_CANCEL_REQUESTED: j.strv("activityId", key()); j.i64v("decisionTaskCompletedEventId", 4); break;
+    case CRR_EV_TIMER_STARTED:
+      j.strv("timerId", key()); j.i64v("startToFireTimeoutSeconds", ref); j.i64v("decisionTaskCompletedEventId", 4);
+      break;
+    case CRR_EV_TIMER_FIRED: case CRR_EV_TIMER_CANCELED: j.strv("timerId", key()); j.i64v("startedEventId", 5); break;
+    case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_INITIATED:
+      if (const char* d = domain_name(aux, false)) j.strv("domain", d);
+      j.strv("workflowId", "child-wf"); j.name_obj("workflowType", "child-type"); j.task_list("taskList", "child-tl");
+      break;
+    case CRR_EV_REQUEST_CANCEL_EXTERNAL_INITIATED:
+    case CRR_EV_SIGNAL_EXTERNAL_INITIATED:
+      j.i64v("decisionTaskCompletedEventId", 4);
+      if (const char* d = domain_name(aux, false)) j.strv("domain", d);
+      j.open("workflowExecution"); j.strv("workflowId", "target-wf"); j.strv("runId", "target-run"); j.close();
+      if (t == CRR_EV_SIGNAL_EXTERNAL_INITIATED) { j.strv("signalName", "sig"); j.strv("input", "c2lnbmFsLWlucHV0"); }
+      break;
+    case CRR_EV_START_CHILD_WORKFLOW_EXECUTION_FAILED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_FAILED:
+    case CRR_EV_CHILD_WORKFLOW_EXECUTION_STARTED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_COMPLETED:
+    case CRR_EV_CHILD_WORKFLOW_EXECUTION_CANCELED: case CRR_EV_CHILD_WORKFLOW_EXECUTION_TIMED_OUT:
+    case CRR_EV_REQUEST_CANCEL_EXTERNAL_FAILED: case CRR_EV_SIGNAL_EXTERNAL_FAILED:
+    case CRR_EV_CHILD_WORKFLOW_EXECUTION_TERMINATED: case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_CANCEL_REQUESTED:
+    case CRR_EV_EXTERNAL_WORKFLOW_EXECUTION_SIGNALED:
+      j.i64v("initiatedEventId", ref);
+      break;
+    case CRR_EV_WORKFLOW_EXECUTION_SIGNALED:
+      j.strv("signalName", "signal"); j.strv("input", "cGF5bG9hZA=="); j.strv("identity", "identity");
+      break;
+    case CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW:
+      j.strv("newExecutionRunId", "new-run"); j.name_obj("workflowType", "workflow-type");
+      break;
+    case CRR_EV_UPSERT_WORKFLOW_SEARCH_ATTRIBUTES:
+      j.i64v("decisionTaskCompletedEventId", 4);
+      j.open("searchAttributes"); j.key("indexedFields"); b.append("{\"CustomKeywordField\":\"InYi\"}"); j.close();
+      break;
+    case CRR_EV_MARKER_RECORDED:
+      j.strv("markerName", "marker"); j.strv("details", "ZGV0YWlscw==");
+      break;
+    default:
+      break;
+  }
+  j.close();
+  b.push_back('}');
+}
+
+void encode_range(const Inputs& in, u32 w0, u32 w1, Out* o, bool json) {
   std::unordered_map<u32, std::string> keystr;
   for (u32 wi = w0; wi < w1; ++wi) {
     const crr_workflow& d = in.wf[wi];
@@ -284,16 +493,26 @@ void encode_range(const Inputs& in, u32 w0, u32 w1, Out* o) {
         if (last) break;
       }
       W w{o->bytes};
-      w.u8(0x59);
-      w.field(T_LIST, 10);
-      w.u8(T_STRUCT);
-      w.be32((u32)(e - k));
+      if (json) {
+        o->bytes.push_back('[');
+      } else {
+        w.u8(0x59);
+        w.field(T_LIST, 10);
+        w.u8(T_STRUCT);
+        w.be32((u32)(e - k));
+      }
       for (i32 j = k; j < e; ++j) {
         const i64 x = d.ev_begin + j;
         if ((in.etype[x] & CRR_ETYPE_MASK) == CRR_EV_WORKFLOW_EXECUTION_CONTINUED_AS_NEW) s.new_run_wf = in.aux[x];
-        encode_event(w, in, x, wi, keystr);
+        if (json) {
+          if (j > k) o->bytes.push_back(',');
+          encode_event_json(o->bytes, in, x, wi, keystr);
+        } else {
+          encode_event(w, in, x, wi, keystr);
+        }
       }
-      w.stop();
+      if (json) o->bytes.push_back(']');
+      else w.stop();
       o->blob_len.push_back(o->bytes.size() - at);
       ++blobs;
       k = e;
@@ -316,9 +535,10 @@ struct crr_encoded {
 extern "C" {
 
 /* Encode a canonical batch (stride 1; host arrays as crr_inputs describes them, plus the per-event key
- * strings: key_off / key_len into key_arena, NULL if absent) into persisted thriftrw blobs. */
-crr_encoded* crr_encode_blobs(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len,
-                              const char* key_arena, int n_threads) {
+ * strings: key_off / key_len into key_arena, NULL if absent) into persisted blobs: thriftrw, or with json != 0
+ * common/types JSON arrays of the same events (serializer.go:321-325's json encoding). */
+crr_encoded* crr_encode_blobs_as(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len,
+                                 const char* key_arena, int n_threads, int json) {
   if (!in || in->stride != 1) return nullptr;
   Inputs I;
   I.etype = in->ev.etype; I.id = in->ev.event_id; I.ver = in->ev.version; I.ts = in->ev.timestamp;
@@ -332,7 +552,7 @@ crr_encoded* crr_encode_blobs(const crr_inputs* in, const uint32_t* key_off, con
   std::vector<std::thread> th;
   for (u32 t = 0; t < T; ++t) {
     const u32 a = (u32)((u64)n * t / T), b = (u32)((u64)n * (t + 1) / T);
-    th.emplace_back(encode_range, std::cref(I), a, b, &outs[t]);
+    th.emplace_back(encode_range, std::cref(I), a, b, &outs[t], json != 0);
     if (th.size() >= (size_t)n_threads) {
       for (auto& x : th) x.join();
       th.clear();
@@ -365,6 +585,12 @@ crr_encoded* crr_encode_blobs(const crr_inputs* in, const uint32_t* key_off, con
   r->bytes.resize(r->bytes.size() + CRR_INGEST_PAD, 0);   // the device parser's window reads past the end
   if (r->strings.empty()) r->strings.push_back(0);
   return r;
+}
+
+/* crr_encode_blobs_as with thriftrw blobs. */
+crr_encoded* crr_encode_blobs(const crr_inputs* in, const uint32_t* key_off, const uint32_t* key_len,
+                              const char* key_arena, int n_threads) {
+  return crr_encode_blobs_as(in, key_off, key_len, key_arena, n_threads, 0);
 }
 
 void crr_encoded_view(const crr_encoded* e, const uint8_t** bytes, uint64_t* n_bytes, const uint64_t** blob_off,

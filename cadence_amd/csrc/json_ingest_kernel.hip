@@ -16,11 +16,11 @@
 // points' binary checksums) is written unescaped, as encoding/json decodes it.
 //
 // Kernels (a lane per blob; integer / byte work, no MFMA):
-//   size_kernel   walk + the thriftrw size (nesting kept in one 64-bit register: 64 levels), or the blob
-//                 appended to the deep list; deep_size_kernel takes that list with a global-memory level
-//                 stack per thread (up to json_decode.h's 10000 levels)
-//   scan          hipCUB inclusive sum -> blob offsets of the output
-//   write_kernel / deep_write_kernel   the same walk again, writing the thriftrw bytes at the blob's offset
+//   blobs_kernel<false>  walk + the thriftrw size (nesting kept in one 64-bit register: 64 levels), or the
+//                        blob appended to the deep list; deep_kernel<false> takes that list with a level stack
+//                        per thread in HBM (up to json_decode.h's 10000 levels)
+//   scan                 hipCUB inclusive sum -> blob offsets of the output
+//   blobs_kernel<true> / deep_kernel<true>   the same walk again, writing the thriftrw bytes at the offset
 // Reads go through a 16-byte window in registers (one aligned dwordx4 per 16 bytes walked).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>

@@ -187,3 +187,22 @@ def test_blobset_from_sources_round_trips():
         s.encodings = [names[int(e)] for e in enc[k:k + len(s.blobs)]]
         k += len(s.blobs)
     assert_same_batch(decode_histories(back, known_domains=KNOWN), decode_histories(src, known_domains=KNOWN))
+
+
+@pytest.mark.parametrize("gen", ["native", "python"])
+def test_native_json_encoder_decodes_back(gen):
+    """blobs.encode_batch(json=True) (blob_encode.cpp: the events as common/types JSON, the bench's JSON
+    workloads) read back by the host JSON decoder equals the host decoding of the thriftrw encoding."""
+    from cadence_amd import synth_native
+    from cadence_amd.blobs import KNOWN_DOMAINS, encode_batch
+    if gen == "native":
+        b = synth_native.mixed(2000, multi_version=True, invalid_rate=0.1, can_rate=0.3, unknown_domain_rate=0.2)
+    else:
+        b = flatten(synth_mixed.mixed_histories(300, 36, multi_version=True, invalid_rate=0.2, can_rate=0.4),
+                    known_domains=set(KNOWN_DOMAINS))
+    tj, tt = encode_batch(b, json=True), encode_batch(b)
+    src = tj.to_sources()
+    for s in src:
+        s.encodings = ["json"] * len(s.blobs)
+    assert_same_batch(decode_histories(src, known_domains=KNOWN_DOMAINS),
+                      decode_histories(tt.to_sources(), known_domains=KNOWN_DOMAINS))

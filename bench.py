@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--headline-only", action="store_true", help="config 2 only (no configs 3/4, e2e, CPU)")
     p.add_argument("--config-steps", type=int, default=5, help="timed steps of the config 3 / 4 / replication lines")
     p.add_argument("--c3-workflows", type=int, default=1_250_000, help="config 3 mixed workflows per GPU")
+    p.add_argument("--json-workflows", type=int, default=125_000,
+                   help="workflows of the JSON-encoded device ingest line (config-3 shape, rank 0, N = 1)")
     p.add_argument("--c4-workflows", type=int, default=2000, help="config 4 logical workflows per GPU")
     p.add_argument("--c5-workflows", type=int, default=1_000_000, help="config 5 multi-version workflows per GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -762,6 +764,71 @@ def blob_to_rows(ctx, canon, resident_digest, name, chunks=8):
     return fig
 
 
+# ---- JSON-encoded persisted batches on the device (rank 0, N = 1) ------------------------------------------------
+def json_ingest(ctx, n_wf, reps=3, cpu_wf=20_000):
+    """Blobs persisted with the json encoding (serializer.go:321-328: json.Unmarshal into []*types.HistoryEvent),
+    the config-3 shape, resident in HBM; timed per pass: crr_ingest_transcode_plan (one host sync) +
+    crr_ingest_transcode (JSON -> thriftrw in HBM) + crr_ingest_plan + crr_ingest_layout + crr_replay.  Checked:
+    the laid-out inputs and the replayed exec rows equal the thriftrw path's on the same workload.  Beside it
+    the host JSON decoder (json_decode.cpp, crr_decode_histories_enc) on a bounded sample, all host cores."""
+    from cadence_amd import dist as cdist
+    from cadence_amd import synth_native
+    from cadence_amd.blobs import KNOWN_DOMAINS, encode_batch
+    from cadence_amd.decode import time_native_decode
+    from cadence_amd.ingest import DeviceIngest
+    torch, eng = ctx.torch, ctx.eng
+    canon = synth_native.mixed(n_wf, shard=(cdist.NUM_SHARDS, 1, 0))
+    bj, bt = encode_batch(canon, json=True), encode_batch(canon)
+    ing_j, ing_t = DeviceIngest(eng), DeviceIngest(eng)
+    dj, dt = ing_j.upload(bj), ing_t.upload(bt)
+    enc = torch.ones(bj.n_blobs, dtype=torch.int32, device=eng.dev)     # CRR_ENCODING_JSON
+    tj = ing_j.transcode(dj, enc)
+    out_j = ing_j.layout(tj, ing_j.plan(tj))
+    S_t = ing_t.plan(dt)
+    out_t = ing_t.layout(dt, S_t)
+    eng.launch(out_t)
+    torch.cuda.synchronize()
+    walls, tc = [], []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tj = ing_j.transcode(dj, enc)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ing_j.layout(tj, ing_j.plan(tj), out=out_j)
+        eng.launch(out_j)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        tc.append(t1 - t0)
+    from cadence_amd import abi
+    n_slots = int(S_t.n_slots)    # (the buffers' slack past the slots is uninitialised)
+    same_in = all(bool(torch.equal(out_j.tensors["ev_" + k][:n_slots * np.dtype(t).itemsize],
+                                   out_t.tensors["ev_" + k][:n_slots * np.dtype(t).itemsize]))
+                  for k, t in abi.EVENT_COLUMNS)
+    same_rows = bool(torch.equal(out_j.tensors["exec"], out_t.tensors["exec"]))
+    n_ev = int(canon.n_events)
+    wall = float(np.median(walls))
+    out = {"workload": f"config 3 shard shape: {n_wf} mixed histories persisted as common/types JSON blobs "
+                       "(one per ApplyEvents batch), resident in HBM",
+           "events": n_ev, "blobs": bj.n_blobs, "json_bytes": bj.n_bytes, "transcoded_bytes": int(ing_j.last_transcode.n_bytes),
+           "events_per_s": n_ev / wall, "ms": wall * 1e3, "transcode_ms": float(np.median(tc)) * 1e3,
+           "json_GBs": bj.n_bytes / float(np.median(tc)) / 1e9,
+           "inputs_equal_thrift_path": same_in, "rows_equal_thrift_path": same_rows,
+           "note": "median of passes; transcode (two lane-per-blob JSON walks) + the thriftrw ingest + the replay"}
+    del dj, dt, tj, out_j, out_t, bj, bt
+    torch.cuda.empty_cache()
+    if not ctx.args.no_cpu_baseline:
+        sj = encode_batch(synth_native.mixed(cpu_wf, shard=(cdist.NUM_SHARDS, 1, 0)), json=True).to_sources()
+        for s_ in sj:
+            s_.encodings = ["json"] * len(s_.blobs)
+        cores = host_cpus()
+        r = time_native_decode(sj, known_domains=KNOWN_DOMAINS, n_threads=cores, min_seconds=2.0)
+        out["cpu_json_decode"] = {"events_per_s": r["events_per_s"], "MB_per_s": r["MB_per_s"], "cores": cores,
+                                  "sample": f"{cpu_wf} workflows of the same shape, decode only (no replay)"}
+        out["vs_cpu_json_decode"] = out["events_per_s"] / r["events_per_s"]
+    return out
+
+
 # ---- rank 0, N = 1: end to end, host ingest, CPU baseline ---------------------------------------------------
 def end_to_end(ctx, n_wf, k, chunks=8):
     """Config 2 from host buffers: pinned staging, `chunks` chunks overlapped on three streams, the event
@@ -929,6 +996,11 @@ def summary(line):
                               "parity_tasks": (nd.get("parity_full") or {}).get("tasks")}
         cv = x["checksum_verify"]
         out["checksum_verify"] = {"value": cv["value"], **rf(cv), "matches": cv["matches_replay_checksums"]}
+    if "json_ingest" in line:
+        x = line["json_ingest"]
+        out["json_ingest"] = {"events_per_s": x["events_per_s"], "json_GBs": x["json_GBs"],
+                              "rows_equal_thrift_path": x["rows_equal_thrift_path"] and x["inputs_equal_thrift_path"],
+                              "vs_cpu_json_decode": x.get("vs_cpu_json_decode")}
     for k, fig in (line.get("blob_to_rows") or {}).items():
         out["blob_to_rows_" + k] = {"events_per_s": fig["events_per_s"],
                                     "device_resident": fig["device_resident"]["events_per_s"],
@@ -1007,6 +1079,8 @@ def main():
             ctx, c3_canon, None, f"config 3 shard persisted: {args.c3_workflows} mixed histories, one thriftrw blob per batch")
         del c3_canon
         progress("blob -> rows config 3 done")
+        line["json_ingest"] = json_ingest(ctx, args.json_workflows)
+        progress("JSON ingest done")
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(ctx, res2, batch2, args.activities)
         if "pcie_inclusive" in line:

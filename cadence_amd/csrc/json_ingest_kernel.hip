@@ -16,11 +16,14 @@
 // points' binary checksums) is written unescaped, as encoding/json decodes it.
 //
 // Kernels (a lane per blob; integer / byte work, no MFMA):
-//   blobs_kernel<false>  walk + the thriftrw size (nesting kept in one 64-bit register: 64 levels), or the
-//                        blob appended to the deep list; deep_kernel<false> takes that list with a level stack
-//                        per thread in HBM (up to json_decode.h's 10000 levels)
+//   blobs_kernel<M_PLAN>  the walk, writing the thriftrw form into the blob's staging region in the scratch
+//                        (its JSON length + 64 bytes; realistic JSON shrinks ~3x) and counting its size (nesting
+//                        kept in one 64-bit register: 64 levels; a deeper blob goes on the deep list, which
+//                        deep_kernel<M_PLAN_DEEP> sizes with a level stack per thread in HBM, up to 10000)
 //   scan                 hipCUB inclusive sum -> blob offsets of the output
-//   blobs_kernel<true> / deep_kernel<true>   the same walk again, writing the thriftrw bytes at the offset
+//   gather_kernel        the staged blobs to their offsets (a wavefront per blob); blobs_kernel<M_WRITE> walks a
+//                        blob whose form outgrew its region again into the output, deep_kernel<M_WRITE_DEEP> the
+//                        deep ones
 // Reads go through a 16-byte window in registers (one aligned dwordx4 per 16 bytes walked).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -49,7 +52,11 @@ constexpr u32 kDeepThreads = 2048;                     // threads of the deep pa
 constexpr u64 kNone = ~0ull;
 
 enum : int { E_OK = 0, E_DEEP = 1, E_BAD = 2 };
-enum : u32 { ST_OK = 0, ST_DEEP = 1, ST_FAILED = 2 };
+// a blob's state after the plan: its thriftrw form staged (ST_OK), too large for its staging region and to be
+// walked again into the output (ST_OVER), nested past 64 levels (ST_DEEP: sized and written by the deep
+// passes), rejected (ST_FAILED: an empty blob)
+enum : u32 { ST_OK = 0, ST_DEEP = 1, ST_FAILED = 2, ST_OVER = 3 };
+constexpr u64 kStageSlack = 64;   // a blob's staging region: its own length + this (realistic JSON shrinks ~3x)
 enum : u8 { T_STOP = 0, T_BOOL = 2, T_I32 = 8, T_I64 = 10, T_STRING = 11, T_STRUCT = 12, T_LIST = 15 };
 
 // ---- name tables: ASCII-folded FNV-1a of each name, built at compile time --------------------------------
@@ -642,13 +649,18 @@ template <bool W>
 struct TW {
   u8* o;
   u64 n;
+  u64 lim;           // W: bytes past `lim` are counted, not written (the staging region's end)
   __device__ __forceinline__ void u8_(u32 v) {
-    if constexpr (W) o[n] = (u8)v;
+    if constexpr (W) {
+      if (n < lim) o[n] = (u8)v;
+    }
     ++n;
   }
   __device__ __forceinline__ void be32_at(u64 at, u32 v) {
     if constexpr (W) {
-      o[at] = (u8)(v >> 24); o[at + 1] = (u8)(v >> 16); o[at + 2] = (u8)(v >> 8); o[at + 3] = (u8)v;
+      if (at + 4 <= lim) {
+        o[at] = (u8)(v >> 24); o[at + 1] = (u8)(v >> 16); o[at + 2] = (u8)(v >> 8); o[at + 3] = (u8)v;
+      }
     }
   }
   __device__ __forceinline__ void be32(u32 v) { be32_at(n, v); n += 4; }
@@ -864,45 +876,72 @@ struct Scratch {    // carved from the caller's scratch (both calls carve it the
   u64* stacks;      // [kDeepThreads][kDeepWords]
   void* scan_tmp;
   size_t scan_tmp_bytes;
-  size_t bytes;
+  size_t bytes;     // the carve up to the staging area
+  u8* stage;        // the rest of the scratch: blob i's thriftrw form at (blob_off[i] - blob_off[0]) + 64 i
+  u64 stage_cap;
 };
 
 __device__ __forceinline__ void record_error(u64* err, u32 blob, int code) {
   atomicMin((unsigned long long*)err, ((u64)blob << 8) | (u64)(-code));
 }
 
-// the blob's walk; W: write at out + off (the plan's sizes were exact)
-// `deep_pass`: the deep list's walk with the whole level stack (a blob it takes keeps ST_DEEP, so the
-// write's first pass leaves it to the deep one)
-template <bool W>
-__device__ void one_blob(const crr_blob_batch& in, const u32* enc, const Scratch& S, u8* out, u32 bi, u64* stack,
-                         bool deep_pass) {
+// The blob's walk, by mode:
+//   M_PLAN        written into its staging region (to the region's end), sized: ST_OK / ST_OVER / ST_DEEP /
+//                 ST_FAILED
+//   M_PLAN_DEEP   a deep-list blob sized with the whole level stack
+//   M_WRITE       an ST_OVER blob walked again into the output at its offset
+//   M_WRITE_DEEP  a deep-list blob written into the output
+enum Mode : int { M_PLAN, M_PLAN_DEEP, M_WRITE, M_WRITE_DEEP };
+template <int M>
+__device__ void one_blob(const crr_blob_batch& in, const u32* enc, const Scratch& S, u8* out, u32 bi, u64* stack) {
+  constexpr bool kPlan = M == M_PLAN || M == M_PLAN_DEEP;
   const u64 b0 = in.blob_off[bi], b1 = in.blob_off[bi + 1];
   const u32 e = enc ? enc[bi] : CRR_ENCODING_THRIFTRW;
-  if (W) {
-    if (S.status[bi] != (deep_pass ? ST_DEEP : ST_OK)) return;
-  } else if (e > CRR_ENCODING_EMPTY) {   // NewUnknownEncodingTypeError (serializer.go:326-327), any length
+  if (M == M_WRITE && S.status[bi] != ST_OVER) return;
+  if (M == M_WRITE_DEEP && S.status[bi] != ST_DEEP) return;
+  if (M == M_PLAN && e > CRR_ENCODING_EMPTY) {   // NewUnknownEncodingTypeError (serializer.go:326-327), any length
     S.size[bi] = 0;
     S.status[bi] = ST_FAILED;
     record_error(S.err, bi, CRR_DECODE_UNKNOWN_ENCODING);
     return;
   }
+  // the staging region (M_PLAN): blobs past the scratch's end get none
+  const u64 reg = (b0 - in.blob_off[0]) + kStageSlack * bi;
+  const u64 reg_len = b1 - b0 + kStageSlack;
+  const u64 lim = reg + reg_len <= S.stage_cap ? reg_len : 0;
+  u8* const dst = M == M_PLAN ? S.stage + reg : M == M_PLAN_DEEP ? nullptr : out + S.off[bi];
   if (e == CRR_ENCODING_THRIFTRW || b1 == b0) {   // as persisted (an empty blob: no events)
-    if (W) {
-      u8* o = out + S.off[bi];
-      for (u64 q = b0; q < b1; ++q) o[q - b0] = in.bytes[q];
-    } else {
+    if (M == M_PLAN) {
       S.size[bi] = b1 - b0;
-      S.status[bi] = ST_OK;
+      if (b1 - b0 <= lim) {
+        for (u64 q = b0; q < b1; ++q) dst[q - b0] = in.bytes[q];
+        S.status[bi] = ST_OK;
+      } else {
+        S.status[bi] = ST_OVER;
+      }
+    } else if (M == M_WRITE) {
+      for (u64 q = b0; q < b1; ++q) dst[q - b0] = in.bytes[q];
     }
     return;
   }
   JR r;
   r.init(in.bytes, b0, b1, stack);
-  TW<W> w{W ? out + S.off[bi] : nullptr, 0};
+  if (M == M_PLAN_DEEP) {
+    TW<false> w{nullptr, 0, 0};
+    transcode_json(r, w);
+    if (r.err) {
+      S.size[bi] = 0;
+      S.status[bi] = ST_FAILED;
+      record_error(S.err, bi, CRR_DECODE_BAD_JSON);
+    } else {
+      S.size[bi] = w.n;
+    }
+    return;
+  }
+  TW<true> w{dst, 0, M == M_PLAN ? lim : ~0ull};
   transcode_json(r, w);
-  if (W) return;
-  if (r.err == E_DEEP) {   // nested past the register stack: the deep pass
+  if (!kPlan) return;
+  if (r.err == E_DEEP) {   // nested past the register stack: the deep passes
     S.status[bi] = ST_DEEP;
     S.deep_list[atomicAdd(S.n_deep, 1u)] = bi;
     return;
@@ -914,25 +953,35 @@ __device__ void one_blob(const crr_blob_batch& in, const u32* enc, const Scratch
     return;
   }
   S.size[bi] = w.n;
-  S.status[bi] = deep_pass ? ST_DEEP : ST_OK;
+  S.status[bi] = w.n <= lim ? ST_OK : ST_OVER;
 }
 
-template <bool W>
+template <int M>
 __global__ __launch_bounds__(kBlock) void blobs_kernel(crr_blob_batch in, const u32* enc, Scratch S, u8* out) {
   const u32 bi = blockIdx.x * kBlock + threadIdx.x;
   if (bi >= in.n_blobs) return;
-  one_blob<W>(in, enc, S, out, bi, nullptr, false);
+  one_blob<M>(in, enc, S, out, bi, nullptr);
+}
+
+// the staged blobs into the output at their offsets: a wavefront per blob, its lanes copying 8 bytes apart
+__global__ __launch_bounds__(kBlock) void gather_kernel(crr_blob_batch in, Scratch S, u8* out) {
+  const u32 lane = threadIdx.x & 63, nw = gridDim.x * (kBlock / 64);
+  for (u32 bi = blockIdx.x * (kBlock / 64) + threadIdx.x / 64; bi < in.n_blobs; bi += nw) {
+    if (S.status[bi] != ST_OK) continue;
+    const u8* src = S.stage + (in.blob_off[bi] - in.blob_off[0]) + kStageSlack * bi;
+    u8* dst = out + S.off[bi];
+    const u64 n = S.size[bi];
+    for (u64 j = lane; j < n; j += 64) dst[j] = src[j];
+  }
 }
 
 // the deep list, grid-stride; each thread's level stack in HBM
-template <bool W>
+template <int M>
 __global__ __launch_bounds__(kBlock) void deep_kernel(crr_blob_batch in, const u32* enc, Scratch S, u8* out) {
   const u32 t = blockIdx.x * kBlock + threadIdx.x;
   const u32 n = *S.n_deep;
   u64* stack = S.stacks + (u64)t * kDeepWords;
-  for (u32 i = t; i < n; i += kDeepThreads) {
-    one_blob<W>(in, enc, S, out, S.deep_list[i], stack, true);
-  }
+  for (u32 i = t; i < n; i += kDeepThreads) one_blob<M>(in, enc, S, out, S.deep_list[i], stack);
 }
 
 size_t scan_tmp_bytes(uint32_t n_blobs) {
@@ -941,7 +990,7 @@ size_t scan_tmp_bytes(uint32_t n_blobs) {
   return tmp;
 }
 
-Scratch carve(void* base, uint32_t n_blobs) {
+Scratch carve(void* base, uint32_t n_blobs, size_t scratch_bytes) {
   Scratch c{};
   size_t used = 0;
   auto take = [&](size_t nb) -> void* {
@@ -960,6 +1009,8 @@ Scratch carve(void* base, uint32_t n_blobs) {
   c.scan_tmp_bytes = scan_tmp_bytes(n_blobs);
   c.scan_tmp = take(c.scan_tmp_bytes);
   c.bytes = used;
+  c.stage = base ? static_cast<u8*>(base) + used : nullptr;
+  c.stage_cap = scratch_bytes > used ? scratch_bytes - used : 0;
   return c;
 }
 
@@ -974,13 +1025,15 @@ bool valid_batch(const crr_blob_batch* in) {
 
 extern "C" {
 
-size_t crr_ingest_transcode_scratch_bytes(uint32_t n_blobs) { return crr_json::carve(nullptr, n_blobs).bytes; }
+size_t crr_ingest_transcode_scratch_bytes(uint32_t n_blobs, uint64_t n_bytes) {
+  return crr_json::carve(nullptr, n_blobs, 0).bytes + n_bytes + crr_json::kStageSlack * n_blobs;
+}
 
 int crr_ingest_transcode_plan(const crr_blob_batch* in, const uint32_t* encodings, void* scratch, size_t scratch_bytes,
                               crr_transcode_summary* summary, void* stream) {
   using namespace crr_json;
   if (!valid_batch(in) || !scratch || !summary) return -1;
-  const Scratch S = carve(scratch, in->n_blobs);
+  const Scratch S = carve(scratch, in->n_blobs, scratch_bytes);
   if (S.bytes > scratch_bytes) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   crr_internal::StreamDevice on_dev_(s);
@@ -991,9 +1044,9 @@ int crr_ingest_transcode_plan(const crr_blob_batch* in, const uint32_t* encoding
   if ((e = hipMemsetAsync(S.n_deep, 0, 4, s)) != hipSuccess) return (int)e;
   if ((e = hipMemsetAsync(S.off, 0, 8, s)) != hipSuccess) return (int)e;
   if (nb) {
-    hipLaunchKernelGGL(blobs_kernel<false>, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
-                       (u8*)nullptr);
-    hipLaunchKernelGGL(deep_kernel<false>, dim3(kDeepThreads / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
+    hipLaunchKernelGGL(blobs_kernel<M_PLAN>, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, encodings,
+                       S, (u8*)nullptr);
+    hipLaunchKernelGGL(deep_kernel<M_PLAN_DEEP>, dim3(kDeepThreads / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
                        (u8*)nullptr);
     size_t tmp = S.scan_tmp_bytes;
     if ((e = hipcub::DeviceScan::InclusiveSum(S.scan_tmp, tmp, S.size, S.off + 1, (int)nb, s)) != hipSuccess)
@@ -1021,7 +1074,7 @@ int crr_ingest_transcode(const crr_blob_batch* in, const uint32_t* encodings, vo
   using namespace crr_json;
   if (!valid_batch(in) || !scratch || !summary || !out_bytes || !out_blob_off) return -1;
   if (reinterpret_cast<uintptr_t>(out_bytes) & 15) return -1;
-  const Scratch S = carve(scratch, in->n_blobs);
+  const Scratch S = carve(scratch, in->n_blobs, scratch_bytes);
   if (S.bytes > scratch_bytes) return -1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   crr_internal::StreamDevice on_dev_(s);
@@ -1031,9 +1084,12 @@ int crr_ingest_transcode(const crr_blob_batch* in, const uint32_t* encodings, vo
   // the pad the ingest's window reads past the last blob
   if ((e = hipMemsetAsync(out_bytes + summary->n_bytes, 0, CRR_INGEST_PAD, s)) != hipSuccess) return (int)e;
   if (nb) {
-    hipLaunchKernelGGL(blobs_kernel<true>, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
+    const u32 gather_blocks = (nb + kBlock / 64 - 1) / (kBlock / 64);
+    hipLaunchKernelGGL(gather_kernel, dim3(gather_blocks < 8192 ? gather_blocks : 8192), dim3(kBlock), 0, s, *in, S,
                        out_bytes);
-    hipLaunchKernelGGL(deep_kernel<true>, dim3(kDeepThreads / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
+    hipLaunchKernelGGL(blobs_kernel<M_WRITE>, dim3((nb + kBlock - 1) / kBlock), dim3(kBlock), 0, s, *in, encodings,
+                       S, out_bytes);
+    hipLaunchKernelGGL(deep_kernel<M_WRITE_DEEP>, dim3(kDeepThreads / kBlock), dim3(kBlock), 0, s, *in, encodings, S,
                        out_bytes);
   }
   if ((e = hipMemcpyAsync(out_blob_off, S.off, 8ull * (nb + 1), hipMemcpyDeviceToDevice, s)) != hipSuccess)

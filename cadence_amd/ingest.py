@@ -80,7 +80,7 @@ def _bind(L):
     L.crr_ingest_plan_resume.restype = ctypes.c_int
     L.crr_ingest_layout_resume.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp, vp]
     L.crr_ingest_layout_resume.restype = ctypes.c_int
-    L.crr_ingest_transcode_scratch_bytes.argtypes = [ctypes.c_uint32]
+    L.crr_ingest_transcode_scratch_bytes.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
     L.crr_ingest_transcode_scratch_bytes.restype = ctypes.c_size_t
     L.crr_ingest_transcode_plan.argtypes = [vp, vp, vp, ctypes.c_size_t, vp, vp]
     L.crr_ingest_transcode_plan.restype = ctypes.c_int
@@ -159,11 +159,13 @@ class DeviceIngest:
         return c
 
     # -- JSON-encoded blobs: rewritten as thriftrw on the device ---------------------------------------------
-    def transcode(self, db: DeviceBlobs, encodings, stream=None) -> DeviceBlobs:
+    def transcode(self, db: DeviceBlobs, encodings, stream=None, stage_bytes: Optional[int] = None) -> DeviceBlobs:
         """crr_ingest_transcode_plan + crr_ingest_transcode: the batch with every json / unknown / empty-encoded
         blob rewritten in HBM as the thriftrw History the decoders read back into the same events
         (``encodings``: CRR_ENCODING_* per blob, a uint32 array or device tensor).  A rejected blob (BAD_JSON,
-        UNKNOWN_ENCODING) becomes empty and is carried as ``pending`` for the plan to raise."""
+        UNKNOWN_ENCODING) becomes empty and is carried as ``pending`` for the plan to raise.  ``stage_bytes``:
+        the blob bytes the scratch's staging area is sized for (default all of them; less: the blobs without
+        room are walked again by the transcode)."""
         torch, dev = self.torch, self.eng.dev
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         L = self.lib
@@ -172,20 +174,21 @@ class DeviceIngest:
             enc = encodings
         else:
             enc = torch.from_numpy(np.ascontiguousarray(encodings, np.uint32).view(np.int32)).to(dev)
-        need = int(L.crr_ingest_transcode_scratch_bytes(nb))
+        need = int(L.crr_ingest_transcode_scratch_bytes(nb, int(db.blobs.n_bytes if stage_bytes is None else stage_bytes)))
         if getattr(self, "tscratch", None) is None or self.tscratch.numel() < need:
             self.tscratch = torch.empty(need, dtype=torch.uint8, device=dev)
+        size = need if stage_bytes is not None else self.tscratch.numel()
         S = CTranscodeSummary()
         vp = ctypes.c_void_p
         rc = L.crr_ingest_transcode_plan(ctypes.byref(db.c), vp(enc.data_ptr()), vp(self.tscratch.data_ptr()),
-                                         ctypes.c_size_t(self.tscratch.numel()), ctypes.byref(S), vp(s.cuda_stream))
+                                         ctypes.c_size_t(size), ctypes.byref(S), vp(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"crr_ingest_transcode_plan failed: {rc}")
         n_bytes = int(S.n_bytes)
         out_bytes = torch.empty(n_bytes + INGEST_PAD + 16, dtype=torch.uint8, device=dev)
         out_off = torch.empty(nb + 1, dtype=torch.int64, device=dev)
         rc = L.crr_ingest_transcode(ctypes.byref(db.c), vp(enc.data_ptr()), vp(self.tscratch.data_ptr()),
-                                    ctypes.c_size_t(self.tscratch.numel()), ctypes.byref(S), vp(out_bytes.data_ptr()),
+                                    ctypes.c_size_t(size), ctypes.byref(S), vp(out_bytes.data_ptr()),
                                     vp(out_off.data_ptr()), vp(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"crr_ingest_transcode failed: {rc}")

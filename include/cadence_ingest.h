@@ -166,12 +166,12 @@ int crr_ingest_layout_resume(const crr_blob_batch* in, const crr_ingest_resume* 
  * canonical thriftrw History the decoders read back into the same events (json_ingest_kernel.hip), so the
  * batch then goes through crr_ingest_plan / crr_ingest_layout (or the _resume pair) unchanged:
  *   crr_ingest_transcode_plan   walk every JSON blob (`encodings[i]`: CRR_ENCODING_* of blob i; NULL: all
- *                               thriftrw), size its thriftrw form, report the rejected blob with the lowest
- *                               index (CRR_DECODE_BAD_JSON / CRR_DECODE_UNKNOWN_ENCODING) -- synchronises the
- *                               stream once to read the sizes back
+ *                               thriftrw), stage its thriftrw form in the scratch and size it, report the
+ *                               rejected blob with the lowest index (CRR_DECODE_BAD_JSON /
+ *                               CRR_DECODE_UNKNOWN_ENCODING) -- synchronises the stream once to read the sizes
  *   crr_ingest_transcode        write the new blob bytes (`out_bytes`: summary.n_bytes + CRR_INGEST_PAD bytes,
- *                               16-byte aligned) and offsets (`out_blob_off`: n_blobs + 1); thriftrw blobs are
- *                               copied as they are, a rejected blob becomes empty
+ *                               16-byte aligned) and offsets (`out_blob_off`: n_blobs + 1): the staged forms
+ *                               gathered; thriftrw blobs are copied as they are, a rejected blob becomes empty
  * The caller then plans the batch { out_bytes, out_blob_off, the same wf / strings / domains }; when the
  * transcode reported a rejection, the plan's own error wins if its blob index is lower (the host decoder
  * stops at the first failing blob).  Both calls take the same scratch (crr_ingest_transcode_scratch_bytes). */
@@ -184,7 +184,10 @@ typedef struct crr_transcode_summary {
     uint32_t reserved1;
 } crr_transcode_summary;
 
-size_t crr_ingest_transcode_scratch_bytes(uint32_t n_blobs);
+/* Scratch for a batch of n_blobs blobs holding n_bytes bytes: the fixed part plus a staging area (each blob's
+ * length + 64 bytes) where the plan's walk leaves the thriftrw form for the transcode to gather; a smaller
+ * scratch (at least the fixed part) works too -- blobs without room are walked a second time by the transcode. */
+size_t crr_ingest_transcode_scratch_bytes(uint32_t n_blobs, uint64_t n_bytes);
 int crr_ingest_transcode_plan(const crr_blob_batch* in, const uint32_t* encodings, void* scratch, size_t scratch_bytes,
                               crr_transcode_summary* summary, void* stream);
 int crr_ingest_transcode(const crr_blob_batch* in, const uint32_t* encodings, void* scratch, size_t scratch_bytes,

@@ -29,21 +29,21 @@ def eng():
     return ReplayEngine(0)
 
 
-def _device(eng, sources):
+def _device(eng, sources, stage_bytes=None):
     """sources -> BlobSet upload -> transcode -> plan + layout; the laid-out host batch and the engine state."""
     from cadence_amd.ingest import DeviceIngest
     bs, enc = blobset_from_sources(sources)
     ing = DeviceIngest(eng)
     db = ing.upload(bs)
-    tdb = ing.transcode(db, enc)
+    tdb = ing.transcode(db, enc, stage_bytes=stage_bytes)
     out = ing.ingest(tdb)
     return ing, tdb, out
 
 
-def _check(eng, sources, replay=False):
+def _check(eng, sources, replay=False, stage_bytes=None):
     canon = decode_histories(sources, known_domains=KNOWN_DOMAINS)
     want = interleave(canon)
-    ing, tdb, out = _device(eng, sources)
+    ing, tdb, out = _device(eng, sources, stage_bytes)
     _assert_same_inputs(ing.to_host_batch(out), want)
     if replay:
         from oracle import oracle
@@ -197,3 +197,19 @@ def test_archival_fixture_json_on_device(eng):
         blobs.append(json.dumps(raw[i:i + len(b)]).encode())
         i += len(b)
     _check(eng, [WorkflowSource(blobs=blobs, encodings=["json"] * len(blobs))], replay=True)
+
+
+@pytest.mark.gpu
+def test_blobs_outgrowing_their_staging_region(eng):
+    """JSON far shorter than its thriftrw form (bare event objects: every field defaulted) outgrows the
+    plan's staging region and is walked again by the transcode; and a scratch with a staging area for only a
+    fraction of the bytes leaves the rest unstaged -- both byte-identical to the host path."""
+    good = json.dumps([event_json(e) for e in _events()]).encode()
+    srcs = [WorkflowSource(blobs=[good, b"[{},{},{}]", b'[{"eventType":"TimerFired"},{"eventId":9}]', good],
+                           encodings=["json"] * 4)]
+    _check(eng, srcs)
+    hs = synth_mixed.mixed_histories(300, 45, multi_version=True, can_rate=0.3)
+    src = json_sources(hs)
+    n = sum(len(b) for s in src for b in s.blobs)
+    for stage in (0, n // 3):
+        _check(eng, src, stage_bytes=stage)

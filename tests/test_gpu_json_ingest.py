@@ -213,3 +213,21 @@ def test_blobs_outgrowing_their_staging_region(eng):
     n = sum(len(b) for s in src for b in s.blobs)
     for stage in (0, n // 3):
         _check(eng, src, stage_bytes=stage)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gen", ["mixed", "long_tail"])
+def test_native_json_workloads_on_device(eng, gen):
+    """The bench's JSON workloads at test size (blobs.encode_batch(json=True) over the native generators: every
+    event type, unknown domains, invalid histories, CAN chains, histories past the lane limit): the device
+    layout equals the host JSON path's and the rows the oracle's."""
+    from cadence_amd import synth_native
+    from cadence_amd.blobs import encode_batch
+    if gen == "mixed":
+        b = synth_native.mixed(20000, multi_version=True, invalid_rate=0.05, can_rate=0.2, unknown_domain_rate=0.1)
+    else:
+        b = synth_native.long_tail(30, max_len=12_000, run_cap=4_000)
+    src = encode_batch(b, json=True).to_sources()
+    for s in src:
+        s.encodings = ["json"] * len(s.blobs)
+    _check(eng, src, replay=True)

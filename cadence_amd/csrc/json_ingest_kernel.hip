@@ -783,6 +783,11 @@ __device__ void event(JR& r, TW<W>& w) {
   i64 id = 0, ts = 0, ver = 0, task = 0;
   i32 type = 0;
   bool have_type = false;
+  // the last attribute key seen and where its value starts; `mixed`: keys of two types seen (then, unless
+  // the last one is the event's type, a second pass finds the type's last occurrence)
+  int attr_t = -1;
+  u64 attr_at = kNone;
+  bool mixed = false;
   r.expect('{');
   if (!r.consume('}')) {
     do {
@@ -796,6 +801,13 @@ __device__ void event(JR& r, TW<W>& w) {
       else if (r.keq(k, kFieldNames, F_EVENT_TYPE)) {
         if (!r.null() && !r.err) { type = r.enum_value(kEvNames, CRR_EV_TYPE_COUNT); have_type = true; }
       } else {
+        const int t = r.find(k, kAttrNames, CRR_EV_TYPE_COUNT);
+        if (t >= 0) {
+          if (attr_t >= 0 && attr_t != t) mixed = true;
+          attr_t = t;
+          r.ws();
+          attr_at = r.p;
+        }
         r.skip();
       }
     } while (!r.err && r.consume(','));
@@ -808,19 +820,22 @@ __device__ void event(JR& r, TW<W>& w) {
   a.clear();
   const bool valid = type >= 0 && type < CRR_EV_TYPE_COUNT;
   if (valid) {
-    // the attribute key's last occurrence (the object was validated above: this walk cannot fail)
-    u64 at = kNone;
-    JR q = r;
-    q.p = obj;
-    q.depth = d_obj;
-    q.expect('{');
-    if (!q.consume('}')) {
-      do {
-        const SRef k = q.str();
-        q.expect(':');
-        if (q.keq(k, kAttrNames, type)) { q.ws(); at = q.p; }
-        q.skip();
-      } while (!q.err && q.consume(','));
+    // the attribute key's last occurrence: the last attribute key if it is the type's, else (keys of several
+    // types seen) a second walk of the object (validated above: this walk cannot fail)
+    u64 at = attr_t == type ? attr_at : kNone;
+    if (attr_t != type && mixed) {
+      JR q = r;
+      q.p = obj;
+      q.depth = d_obj;
+      q.expect('{');
+      if (!q.consume('}')) {
+        do {
+          const SRef k = q.str();
+          q.expect(':');
+          if (q.keq(k, kAttrNames, type)) { q.ws(); at = q.p; }
+          q.skip();
+        } while (!q.err && q.consume(','));
+      }
     }
     if (at != kNone) {
       JR q2 = r;

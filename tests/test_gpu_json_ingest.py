@@ -231,3 +231,25 @@ def test_native_json_workloads_on_device(eng, gen):
     for s in src:
         s.encodings = ["json"] * len(s.blobs)
     _check(eng, src, replay=True)
+
+
+@pytest.mark.gpu
+def test_attribute_objects_of_several_types(eng):
+    """An event carrying attribute objects of other types before / after its own (and its own twice): the
+    last occurrence of its own type's key is read, whatever came after it."""
+    base = {"eventId": 2, "version": 7, "timestamp": 5, "taskId": 3}
+    own = {"startToCloseTimeoutSeconds": 9, "attempt": 4}
+    other = {"timeoutType": "HEARTBEAT"}
+    evs = []
+    for order in (("own", "other"), ("other", "own"), ("own", "other", "own2"), ("other", "other")):
+        parts = [json.dumps(base)[:-1], '"eventType": "DecisionTaskScheduled"']
+        for o in order:
+            if o == "own":
+                parts.append('"decisionTaskScheduledEventAttributes": ' + json.dumps(own))
+            elif o == "own2":
+                parts.append('"decisionTaskScheduledEventAttributes": ' + json.dumps({"attempt": 8}))
+            else:
+                parts.append('"decisionTaskTimedOutEventAttributes": ' + json.dumps(other))
+        evs.append(", ".join(parts) + "}")
+    blobs = ["[" + e + "]" for e in evs]
+    _check(eng, [WorkflowSource(blobs=[b.encode() for b in blobs], encodings=["json"] * len(blobs))])

@@ -64,12 +64,16 @@ constexpr u32 fold(u32 c) { return c >= 'A' && c <= 'Z' ? c + 32 : c; }
 constexpr u32 kFnv0 = 2166136261u;
 constexpr u32 hstep(u32 h, u32 c) { return (h ^ fold(c)) * 16777619u; }
 
+// every name is at most 64 bytes (the longest, RequestCancelExternalWorkflowExecutionInitiatedEventAttributes,
+// is 62): its folded bytes fit 8 words, and a key is compared word for word (a longer key matches no name)
+constexpr int kNameWords = 8;
 template <int N, int C>
 struct Names {
   char ch[C];
   u16 off[N];
   u16 len[N];
   u32 hash[N];
+  u64 w[N][kNameWords];   // the folded bytes, little-endian, zero-padded
 };
 template <int N, int C>
 constexpr Names<N, C> make_names(const char* const (&src)[N], const char* suffix) {
@@ -79,9 +83,15 @@ constexpr Names<N, C> make_names(const char* const (&src)[N], const char* suffix
     t.off[i] = (u16)o;
     u32 h = kFnv0;
     int n = 0;
-    for (const char* s = src[i]; *s; ++s, ++n) { t.ch[o++] = *s; h = hstep(h, (u8)*s); }
-    for (const char* s = suffix; *s; ++s, ++n) { t.ch[o++] = *s; h = hstep(h, (u8)*s); }
-    t.len[i] = (u16)n;
+    for (const char* s = src[i]; *s; ++s, ++n) {
+      t.ch[o++] = *s; h = hstep(h, (u8)*s);
+      if (n < 8 * kNameWords) t.w[i][n / 8] |= (u64)fold((u8)*s) << (8 * (n % 8));
+    }
+    for (const char* s = suffix; *s; ++s, ++n) {
+      t.ch[o++] = *s; h = hstep(h, (u8)*s);
+      if (n < 8 * kNameWords) t.w[i][n / 8] |= (u64)fold((u8)*s) << (8 * (n % 8));
+    }
+    t.len[i] = (u16)(n <= 8 * kNameWords ? n : 0xFFFF);   // (a longer name would never match)
     t.hash[i] = h;
   }
   return t;
@@ -132,10 +142,17 @@ __constant__ TimeoutNames kTimeoutNames = make_names<4, 64>(kTimeoutSrc, "");
 __constant__ InitNames kInitNames = make_names<3, 32>(kInitiatorSrc, "");
 
 // ---- the reader: JsonReader (json_decode.h) over one blob [p, end) ----------------------------------------
-struct SRef {      // a JSON string token: its opening quote, its decoded length and folded hash
-  u64 pos;
+struct SRef {      // a JSON string token: its opening quote, its decoded length, folded hash and first 64
+  u64 pos;         // folded bytes (zero-padded words)
   u32 len;
   u32 hash;
+  u64 h0, h1, h2, h3, h4, h5, h6, h7;
+  __device__ __forceinline__ void put(u32 word, u64 v) {   // constant register indices only
+    switch (word) {
+      case 0: h0 = v; break; case 1: h1 = v; break; case 2: h2 = v; break; case 3: h3 = v; break;
+      case 4: h4 = v; break; case 5: h5 = v; break; case 6: h6 = v; break; default: h7 = v; break;
+    }
+  }
 };
 
 struct JR {
@@ -288,31 +305,34 @@ struct JR {
   __device__ __forceinline__ SIt sit(u64 quote) const { return SIt{quote + 1, 0, 0}; }
   // a string token at the cursor: its reference, the cursor past it
   __device__ SRef str() {
-    SRef k{kNone, 0, kFnv0};
+    SRef k{kNone, 0, kFnv0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (err) return k;
     if (peek() != '"') { fail(); return k; }
     k.pos = p;
     SIt it = sit(p);
+    u64 cur = 0;
     for (;;) {
       const int c = snext(it);
       if (c < 0) break;
-      ++k.len;
+      const u32 j = k.len++;
       k.hash = hstep(k.hash, (u32)c);
+      if (j < 8 * kNameWords) {
+        cur |= (u64)fold((u32)c) << (8 * (j & 7));
+        if ((j & 7) == 7) { k.put(j >> 3, cur); cur = 0; }
+      }
     }
+    if ((k.len & 7) && k.len < 8 * kNameWords) k.put(k.len >> 3, cur);
     p = it.q;
     return k;
   }
   // the string at `k` equals name i of table T, ASCII case folded (JsonReader::iequal)
+  // (every folded byte compared: the words hold all of a key as long as any name)
   template <class T>
-  __device__ bool keq(const SRef& k, const T& t, int i) {
+  __device__ __forceinline__ bool keq(const SRef& k, const T& t, int i) {
     if (err || k.len != t.len[i] || k.hash != t.hash[i]) return false;
-    SIt it = sit(k.pos);
-    const char* s = t.ch + t.off[i];
-    for (u32 j = 0; j < k.len; ++j) {
-      const int c = snext(it);
-      if (c < 0 || fold((u32)c) != fold((u8)s[j])) return false;
-    }
-    return true;
+    const u64* w = t.w[i];
+    return k.h0 == w[0] && k.h1 == w[1] && k.h2 == w[2] && k.h3 == w[3] && k.h4 == w[4] && k.h5 == w[5] &&
+           k.h6 == w[6] && k.h7 == w[7];
   }
   template <class T>
   __device__ int find(const SRef& k, const T& t, int n) {

@@ -808,6 +808,12 @@ __device__ void event(JR& r, TW<W>& w) {
   int attr_t = -1;
   u64 attr_at = kNone;
   bool mixed = false;
+  // the event's own attributes read as they come when its type is already known (Go's marshal order puts
+  // eventType first): `a` then holds the object at `a_at`, used if that is the occurrence the host reads
+  Attr a;
+  a.clear();
+  u64 a_at = kNone;
+  int a_t = -1;
   r.expect('{');
   if (!r.consume('}')) {
     do {
@@ -822,13 +828,29 @@ __device__ void event(JR& r, TW<W>& w) {
         if (!r.null() && !r.err) { type = r.enum_value(kEvNames, CRR_EV_TYPE_COUNT); have_type = true; }
       } else {
         const int t = r.find(k, kAttrNames, CRR_EV_TYPE_COUNT);
+        bool read = false;
         if (t >= 0) {
           if (attr_t >= 0 && attr_t != t) mixed = true;
           attr_t = t;
           r.ws();
           attr_at = r.p;
+          if (have_type && t == type) {
+            const JR save = r;
+            Attr ta;
+            ta.clear();
+            read_attributes(r, t, ta);
+            if (r.err == E_DEEP) return;
+            if (r.err == E_OK) {
+              a = ta;
+              a_at = attr_at;
+              a_t = t;
+              read = true;
+            } else {
+              r = save;   // a type error counts only if this is the occurrence read: the syntax check below
+            }
+          }
         }
-        r.skip();
+        if (!read) r.skip();
       }
     } while (!r.err && r.consume(','));
     r.expect('}');
@@ -836,8 +858,6 @@ __device__ void event(JR& r, TW<W>& w) {
   if (r.err) return;
   if (!have_type) type = 0;   // a nil *EventType reads as its zero value
   const u64 obj_end = r.p;
-  Attr a;
-  a.clear();
   const bool valid = type >= 0 && type < CRR_EV_TYPE_COUNT;
   if (valid) {
     // the attribute key's last occurrence: the last attribute key if it is the type's, else (keys of several
@@ -857,13 +877,16 @@ __device__ void event(JR& r, TW<W>& w) {
         } while (!q.err && q.consume(','));
       }
     }
-    if (at != kNone) {
+    if (at != kNone && !(at == a_at && a_t == type)) {
       JR q2 = r;
       q2.p = at;
       q2.end = obj_end;
       q2.depth = d_obj + 1;
+      a.clear();
       read_attributes(q2, type, a);
       if (q2.err) { r.err = q2.err; return; }
+    } else if (at == kNone) {
+      a.clear();
     }
   }
   w.i64f(10, id);

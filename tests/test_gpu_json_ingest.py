@@ -253,3 +253,26 @@ def test_attribute_objects_of_several_types(eng):
         evs.append(", ".join(parts) + "}")
     blobs = ["[" + e + "]" for e in evs]
     _check(eng, [WorkflowSource(blobs=[b.encode() for b in blobs], encodings=["json"] * len(blobs))])
+
+
+@pytest.mark.gpu
+def test_type_errors_in_unread_occurrences(eng):
+    """An attribute object of the event's own type with a type error in a read field fails the blob only when
+    it is the occurrence the host reads (the last): an earlier bad one followed by a good one decodes, a good
+    one followed by a bad one is rejected -- and an eventType after the attributes, or changed by a duplicate,
+    reads the attributes of the final type."""
+    from cadence_amd.ingest import IngestError
+    good = '"activityTaskScheduledEventAttributes": {"activityId": "a1", "scheduleToCloseTimeoutSeconds": 5}'
+    bad = '"activityTaskScheduledEventAttributes": {"activityId": 7}'
+    head = '{"eventId": 1, "version": 1, "eventType": "ActivityTaskScheduled", '
+    ok_blobs = ["[" + head + bad + ", " + good + "}]",
+                '[{"eventId": 1, "version": 1, ' + good + ', "eventType": "ActivityTaskScheduled"}]',
+                "[" + head + good + ', "eventType": "TimerStarted", "timerStartedEventAttributes": {"timerId": "t"}}]',
+                "[" + head + good + ', "eventType": "TimerStarted"}]']
+    _check(eng, [WorkflowSource(blobs=[b.encode() for b in ok_blobs], encodings=["json"] * len(ok_blobs))])
+    src = [WorkflowSource(blobs=[("[" + head + good + ", " + bad + "}]").encode()], encodings=["json"])]
+    with pytest.raises(DeserializationError) as he:
+        decode_histories(src)
+    with pytest.raises(IngestError) as de:
+        _device(eng, src)
+    assert (de.value.code, de.value.blob) == (he.value.code, he.value.blob)
